@@ -1,0 +1,127 @@
+"""ctypes binding of libdrandgpu.so (the C-ABI of include/drand_gpu.h).
+
+The library is built in-tree by __graft_entry__.build() (hipcc --offload-arch=gfx950).  There is no
+CPU fallback: if the library or a gfx950 device is missing, every call raises DrandGpuError.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdrandgpu.so")
+
+# status codes (include/drand_gpu.h)
+ST_OK = 0
+ST_BAD_SIG = 1
+ST_SIG_DECODE = 2
+ST_BAD_INDEX = 3
+ST_PK_DECODE = 4
+ST_NOT_ENOUGH = 5
+ST_NOT_EXAMINED = 255
+
+DST_NUL = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"
+
+# Every entry point the header declares, with ctypes signatures.
+_P = ctypes.c_void_p
+_SZ = ctypes.c_size_t
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_I = ctypes.c_int
+SIGNATURES = {
+    "dg_init": ([_I], _I),
+    "dg_shutdown": ([], None),
+    "dg_last_error": ([], ctypes.c_char_p),
+    "dg_device_ready": ([], _I),
+    "dg_hash_to_g2": ([_SZ, _P, _SZ, _P, _SZ, _P], _I),
+    "dg_sign": ([_SZ, _P, _P, _P, _SZ, _P], _I),
+    "dg_verify": ([_P, _SZ, _P, _SZ, _P, _P, _U64], _I),
+    "dg_verify_beacons": ([_P, _SZ, _P, _P, _P, _P, _P, _P, _U64], _I),
+    "dg_check_links": ([_U64, _P, _SZ, _SZ, _P, _P, _P, _P, _P, _P], _I),
+    "dg_beacon_messages": ([_SZ, _P, _P, _P, _P, _P], _I),
+    "dg_randomness": ([_SZ, _P, _P], _I),
+    "dg_pubpoly_eval": ([_P, _U32, _SZ, _P, _P], _I),
+    "dg_verify_partials": ([_P, _U32, _SZ, _P, _SZ, _U32, _P, _P, _U64], _I),
+    "dg_recover": ([_P, _U32, _U32, _SZ, _P, _SZ, _U32, _P, _P, _P, _P, _U64], _I),
+    "dg_verify_beacons_dev": ([_P, _SZ, _P, _P, _P, _P, _P, _P, _U64, _P], _I),
+    "dg_set_timing": ([_I], _I),
+    "dg_last_timings": ([_P, _P, _P, _I], _I),
+}
+
+
+class DrandGpuError(RuntimeError):
+    pass
+
+
+_lib = None
+_device = None
+
+
+def load():
+    """Load the shared library (no device needed).  Raises if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DrandGpuError("libdrandgpu.so not built: run __graft_entry__.build() (hipcc, gfx950)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = lib
+    return _lib
+
+
+def lib(device=None):
+    """The library with a device selected (LOCAL_RANK, else 0)."""
+    global _device
+    L = load()
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", "0")) if _device is None else _device
+    if _device != device:
+        check(L.dg_init(device))
+        _device = device
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        msg = load().dg_last_error()
+        raise DrandGpuError("libdrandgpu error %d: %s" % (rc, msg.decode() if msg else ""))
+    return rc
+
+
+def ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(ctypes.c_void_p)
+    if isinstance(a, (bytes, bytearray)):
+        return ctypes.cast(ctypes.c_char_p(bytes(a)), ctypes.c_void_p)
+    if hasattr(a, "data_ptr"):  # torch tensor (device-resident API)
+        return ctypes.c_void_p(a.data_ptr())
+    raise TypeError(type(a))
+
+
+def u8(a, shape=None):
+    """bytes / list of bytes / ndarray -> contiguous uint8 ndarray."""
+    if isinstance(a, np.ndarray):
+        arr = np.ascontiguousarray(a, dtype=np.uint8)
+    elif isinstance(a, (bytes, bytearray)):
+        arr = np.frombuffer(bytes(a), dtype=np.uint8).copy()
+    else:
+        arr = np.frombuffer(b"".join(bytes(x) for x in a), dtype=np.uint8).copy()
+    if shape is not None:
+        arr = arr.reshape(shape)
+    return arr
+
+
+def timings():
+    """Per-kernel average launch time (us) accumulated since dg_set_timing(1)."""
+    L = load()
+    cap = 64
+    names = (ctypes.c_char_p * cap)()
+    us = (ctypes.c_double * cap)()
+    launches = (ctypes.c_int * cap)()
+    k = L.dg_last_timings(ctypes.cast(names, _P), ctypes.cast(us, _P), ctypes.cast(launches, _P), cap)
+    return {names[i].decode(): (us[i], launches[i]) for i in range(k)}

@@ -1,0 +1,283 @@
+// G1 (over Fp) and G2 (over Fp2, the sextic M-twist E': y^2 = x^3 + 4(1+u)) group arithmetic.
+// Jacobian coordinates (x = X/Z^2, y = Y/Z^3), Z = 0 is the point at infinity.
+// ZCash compressed encodings (G1 48 B, G2 96 B with x = c1 || c0; flags 0x80 compressed,
+// 0x40 infinity, 0x20 "y lexicographically largest") as produced by kyber's MarshalBinary for the
+// suite chosen at key/curve.go:12 (keys on G1 key/curve.go:21, signatures on G2 key/curve.go:26).
+#pragma once
+#include "field.h"
+
+namespace dg {
+
+// ---- field-generic helpers so one template serves G1 and G2
+DGI Fp f_add(const Fp& a, const Fp& b) { return fp_add(a, b); }
+DGI Fp f_sub(const Fp& a, const Fp& b) { return fp_sub(a, b); }
+DGI Fp f_mul(const Fp& a, const Fp& b) { return fp_mul(a, b); }
+DGI Fp f_sqr(const Fp& a) { return fp_sqr(a); }
+DGI Fp f_dbl(const Fp& a) { return fp_dbl(a); }
+DGI Fp f_neg(const Fp& a) { return fp_neg(a); }
+DGI bool f_is_zero(const Fp& a) { return fp_is_zero(a); }
+DGI bool f_eq(const Fp& a, const Fp& b) { return fp_eq(a, b); }
+DGI Fp f_sel(bool c, const Fp& a, const Fp& b) { return fp_sel(c, a, b); }
+DGI Fp2 f_add(const Fp2& a, const Fp2& b) { return fp2_add(a, b); }
+DGI Fp2 f_sub(const Fp2& a, const Fp2& b) { return fp2_sub(a, b); }
+DGI Fp2 f_mul(const Fp2& a, const Fp2& b) { return fp2_mul(a, b); }
+DGI Fp2 f_sqr(const Fp2& a) { return fp2_sqr(a); }
+DGI Fp2 f_dbl(const Fp2& a) { return fp2_dbl(a); }
+DGI Fp2 f_neg(const Fp2& a) { return fp2_neg(a); }
+DGI bool f_is_zero(const Fp2& a) { return fp2_is_zero(a); }
+DGI bool f_eq(const Fp2& a, const Fp2& b) { return fp2_eq(a, b); }
+DGI Fp2 f_sel(bool c, const Fp2& a, const Fp2& b) { return fp2_sel(c, a, b); }
+
+template <class F>
+struct Jac {
+  F x, y, z;
+};
+template <class F>
+struct Aff {
+  F x, y;
+  bool inf;
+};
+typedef Jac<Fp> G1J;
+typedef Jac<Fp2> G2J;
+typedef Aff<Fp> G1A;
+typedef Aff<Fp2> G2A;
+
+DGI Fp f_zero_of(const Fp&) { return fp_zero(); }
+DGI Fp2 f_zero_of(const Fp2&) { return fp2_zero(); }
+DGI Fp f_one_of(const Fp&) { return fp_one(); }
+DGI Fp2 f_one_of(const Fp2&) { return fp2_one(); }
+
+template <class F>
+DGI Jac<F> jac_infinity() {
+  F z = f_zero_of(F{});
+  return Jac<F>{z, z, z};
+}
+template <class F>
+DGI bool jac_is_inf(const Jac<F>& p) {
+  return f_is_zero(p.z);
+}
+template <class F>
+DGI Jac<F> jac_from_aff(const Aff<F>& a) {
+  if (a.inf) return jac_infinity<F>();
+  return Jac<F>{a.x, a.y, f_one_of(F{})};
+}
+template <class F>
+DGI Jac<F> jac_neg(const Jac<F>& p) {
+  return Jac<F>{p.x, f_neg(p.y), p.z};
+}
+
+// dbl-2009-l (a = 0): 2M + 5S
+template <class F>
+DGI Jac<F> jac_dbl(const Jac<F>& p) {
+  F A = f_sqr(p.x);
+  F B = f_sqr(p.y);
+  F C = f_sqr(B);
+  F D = f_dbl(f_sub(f_sub(f_sqr(f_add(p.x, B)), A), C));
+  F E = f_add(f_dbl(A), A);
+  F Fv = f_sqr(E);
+  F X3 = f_sub(Fv, f_dbl(D));
+  F C8 = f_dbl(f_dbl(f_dbl(C)));
+  F Y3 = f_sub(f_mul(E, f_sub(D, X3)), C8);
+  F Z3 = f_dbl(f_mul(p.y, p.z));
+  return Jac<F>{X3, Y3, Z3};  // infinity (z = 0) maps to z = 0
+}
+
+// add-2007-bl with the exceptional cases handled
+template <class F>
+DGI Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
+  if (jac_is_inf(p)) return q;
+  if (jac_is_inf(q)) return p;
+  F Z1Z1 = f_sqr(p.z);
+  F Z2Z2 = f_sqr(q.z);
+  F U1 = f_mul(p.x, Z2Z2);
+  F U2 = f_mul(q.x, Z1Z1);
+  F S1 = f_mul(f_mul(p.y, q.z), Z2Z2);
+  F S2 = f_mul(f_mul(q.y, p.z), Z1Z1);
+  F H = f_sub(U2, U1);
+  F r = f_dbl(f_sub(S2, S1));
+  if (f_is_zero(H)) {
+    if (f_is_zero(r)) return jac_dbl(p);
+    return jac_infinity<F>();
+  }
+  F I = f_sqr(f_dbl(H));
+  F J = f_mul(H, I);
+  F V = f_mul(U1, I);
+  F X3 = f_sub(f_sub(f_sqr(r), J), f_dbl(V));
+  F Y3 = f_sub(f_mul(r, f_sub(V, X3)), f_dbl(f_mul(S1, J)));
+  F Z3 = f_mul(f_sub(f_sub(f_sqr(f_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  return Jac<F>{X3, Y3, Z3};
+}
+
+// madd-2007-bl: q affine (not infinity)
+template <class F>
+DGI Jac<F> jac_add_aff(const Jac<F>& p, const F& qx, const F& qy) {
+  if (jac_is_inf(p)) return Jac<F>{qx, qy, f_one_of(F{})};
+  F Z1Z1 = f_sqr(p.z);
+  F U2 = f_mul(qx, Z1Z1);
+  F S2 = f_mul(f_mul(qy, p.z), Z1Z1);
+  F H = f_sub(U2, p.x);
+  F r = f_dbl(f_sub(S2, p.y));
+  if (f_is_zero(H)) {
+    if (f_is_zero(r)) return jac_dbl(p);
+    return jac_infinity<F>();
+  }
+  F HH = f_sqr(H);
+  F I = f_dbl(f_dbl(HH));
+  F J = f_mul(H, I);
+  F V = f_mul(p.x, I);
+  F X3 = f_sub(f_sub(f_sqr(r), J), f_dbl(V));
+  F Y3 = f_sub(f_mul(r, f_sub(V, X3)), f_dbl(f_mul(p.y, J)));
+  F Z3 = f_sub(f_sub(f_sqr(f_add(p.z, H)), Z1Z1), HH);
+  return Jac<F>{X3, Y3, Z3};
+}
+
+template <class F>
+DGI bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
+  bool pi = jac_is_inf(p), qi = jac_is_inf(q);
+  if (pi || qi) return pi && qi;
+  F Z1Z1 = f_sqr(p.z);
+  F Z2Z2 = f_sqr(q.z);
+  if (!f_eq(f_mul(p.x, Z2Z2), f_mul(q.x, Z1Z1))) return false;
+  return f_eq(f_mul(f_mul(p.y, q.z), Z2Z2), f_mul(f_mul(q.y, p.z), Z1Z1));
+}
+
+// [k]P for a 64-bit scalar (double-and-add, MSB first)
+template <class F>
+DGI Jac<F> jac_mul_u64(const Jac<F>& p, uint64_t k) {
+  Jac<F> acc = jac_infinity<F>();
+  for (int b = 63; b >= 0; --b) {
+    acc = jac_dbl(acc);
+    if ((k >> b) & 1) acc = jac_add(acc, p);
+  }
+  return acc;
+}
+// [k]P for a 256-bit scalar given as 8 little-endian 32-bit limbs (plain integer)
+template <class F>
+DGI Jac<F> jac_mul_u256(const Jac<F>& p, const uint32_t* k) {
+  Jac<F> acc = jac_infinity<F>();
+  // fixed 4-bit window with a 16-entry table would need 16 points in registers; keep double-and-add
+  for (int w = 7; w >= 0; --w) {
+    uint32_t kw = k[w];
+    for (int b = 31; b >= 0; --b) {
+      acc = jac_dbl(acc);
+      if ((kw >> b) & 1) acc = jac_add(acc, p);
+    }
+  }
+  return acc;
+}
+
+template <class F>
+DGI Aff<F> jac_to_aff_with_inv(const Jac<F>& p, const F& zinv) {
+  F zi2 = f_sqr(zinv);
+  return Aff<F>{f_mul(p.x, zi2), f_mul(p.y, f_mul(zi2, zinv)), false};
+}
+DGI G1A g1_to_aff(const G1J& p) {
+  if (jac_is_inf(p)) return G1A{fp_zero(), fp_zero(), true};
+  return jac_to_aff_with_inv(p, fp_inv(p.z));
+}
+DGI G2A g2_to_aff(const G2J& p) {
+  if (jac_is_inf(p)) return G2A{fp2_zero(), fp2_zero(), true};
+  return jac_to_aff_with_inv(p, fp2_inv(p.z));
+}
+
+// ---- G2 endomorphism psi = untwist o Frobenius o twist, subgroup check, cofactor clearing
+DGI G2J g2_psi(const G2J& p) {
+  return G2J{fp2_mul(fp2_conj(p.x), fp2_const(PSI_CX)), fp2_mul(fp2_conj(p.y), fp2_const(PSI_CY)), fp2_conj(p.z)};
+}
+// [z]P with z = -Z_ABS
+DGI G2J g2_mul_z(const G2J& p) { return jac_neg(jac_mul_u64(p, Z_ABS)); }
+// P in G2  <=>  psi(P) == [z]P   (Scott, "A note on group membership tests for G1, G2 and GT")
+DGI bool g2_in_subgroup(const G2J& p) { return jac_eq(g2_psi(p), g2_mul_z(p)); }
+// RFC 9380 Appendix G.3 (Budroni-Pintore): h_eff * P = [z^2 - z - 1]P + [z - 1]psi(P) + psi^2(2P)
+DGI G2J g2_clear_cofactor(const G2J& p) {
+  G2J t1 = g2_mul_z(p);
+  G2J t2 = g2_psi(p);
+  G2J t3 = g2_psi(g2_psi(jac_dbl(p)));
+  t3 = jac_add(t3, jac_neg(t2));
+  t2 = jac_add(t1, t2);
+  t2 = g2_mul_z(t2);
+  t3 = jac_add(t3, t2);
+  t3 = jac_add(t3, jac_neg(t1));
+  return jac_add(t3, jac_neg(p));
+}
+// G1 subgroup check by [r]P == O (keys and commits only: a handful per batch)
+DGI bool g1_in_subgroup(const G1J& p) {
+  // r as 8 little-endian limbs
+  return jac_is_inf(jac_mul_u256(p, R_LIMBS));
+}
+
+// ---- ZCash decoding.  Status: 0 ok, 1 = decode error.
+DGI bool g1_decompress(G1A& out, const uint8_t* in, bool subgroup_check) {
+  uint8_t f = in[0];
+  if (!(f & 0x80)) return false;
+  if (f & 0x40) {
+    if (f != 0xc0) return false;
+    uint32_t o = 0;
+    for (int i = 1; i < 48; ++i) o |= in[i];
+    if (o) return false;
+    out = G1A{fp_zero(), fp_zero(), true};
+    return true;
+  }
+  uint8_t b[48];
+  for (int i = 0; i < 48; ++i) b[i] = in[i];
+  b[0] &= 0x1f;
+  Fp x;
+  if (!fp_from_be48_plain(x, b)) return false;
+  x = fp_to_mont(x);
+  Fp rhs = fp_add(fp_mul(fp_sqr(x), x), fp_const(FP_B_G1));
+  Fp y;
+  if (!fp_sqrt(y, rhs)) return false;
+  if (((f & 0x20) != 0) != fp_lex_largest(y)) y = fp_neg(y);
+  out = G1A{x, y, false};
+  if (subgroup_check && !g1_in_subgroup(jac_from_aff(out))) return false;
+  return true;
+}
+DGI bool g2_decompress(G2A& out, const uint8_t* in, bool subgroup_check) {
+  uint8_t f = in[0];
+  if (!(f & 0x80)) return false;
+  if (f & 0x40) {
+    if (f != 0xc0) return false;
+    uint32_t o = 0;
+    for (int i = 1; i < 96; ++i) o |= in[i];
+    if (o) return false;
+    out = G2A{fp2_zero(), fp2_zero(), true};
+    return true;
+  }
+  uint8_t b[48];
+  for (int i = 0; i < 48; ++i) b[i] = in[i];
+  b[0] &= 0x1f;
+  Fp x1, x0;
+  if (!fp_from_be48_plain(x1, b)) return false;
+  if (!fp_from_be48_plain(x0, in + 48)) return false;
+  Fp2 x{fp_to_mont(x0), fp_to_mont(x1)};
+  Fp2 rhs = fp2_add(fp2_mul(fp2_sqr(x), x), fp2_const(FP2_B_G2));
+  Fp2 y;
+  if (!fp2_sqrt(y, rhs)) return false;
+  if (((f & 0x20) != 0) != fp2_lex_largest(y)) y = fp2_neg(y);
+  out = G2A{x, y, false};
+  if (subgroup_check && !g2_in_subgroup(jac_from_aff(out))) return false;
+  return true;
+}
+DGI void g1_compress_aff(uint8_t* out, const G1A& a) {
+  if (a.inf) {
+    out[0] = 0xc0;
+    for (int i = 1; i < 48; ++i) out[i] = 0;
+    return;
+  }
+  fp_to_be48(out, a.x);
+  out[0] |= 0x80;
+  if (fp_lex_largest(a.y)) out[0] |= 0x20;
+}
+DGI void g2_compress_aff(uint8_t* out, const G2A& a) {
+  if (a.inf) {
+    out[0] = 0xc0;
+    for (int i = 1; i < 96; ++i) out[i] = 0;
+    return;
+  }
+  fp_to_be48(out, a.x.c1);
+  fp_to_be48(out + 48, a.x.c0);
+  out[0] |= 0x80;
+  if (fp2_lex_largest(a.y)) out[0] |= 0x20;
+}
+
+}  // namespace dg

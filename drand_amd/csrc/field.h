@@ -1,0 +1,457 @@
+// BLS12-381 field tower for the HIP kernels (gfx950), one field element per lane.
+//
+// Fp:  12 x 32-bit limbs, Montgomery form (R = 2^384), values kept fully reduced in [0, p).
+//      Multiplication is CIOS with the "no final carry" shortcut (p's top limb 0x1a0111ea < 2^31 - 1),
+//      every 32x32+32+32 step is one v_mad_u64_u32 on gfx950 (full issue rate, see
+//      tools/microbench/intmul.hip and DESIGN.md §roofline).
+// Fp2 = Fp[u]/(u^2+1), Fp6 = Fp2[v]/(v^3 - xi), Fp12 = Fp6[w]/(w^2 - v), xi = 1 + u.
+//
+// This restates the arithmetic of the reference's pairing suite (github.com/drand/bls12-381 v0.2.0,
+// selected at key/curve.go:12); the restatement is checked against oracle/ in tests/.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define DGI __host__ __device__ __forceinline__
+#define DGN __host__ __device__ __noinline__
+#else
+#define DGI static inline
+#define DGN static
+#endif
+
+#include "bls_constants.h"
+#include "fp_asm.h"
+
+namespace dg {
+
+struct Fp {
+  uint32_t l[12];
+};
+struct Fp2 {
+  Fp c0, c1;
+};
+struct Fp6 {
+  Fp2 c0, c1, c2;
+};
+struct Fp12 {
+  Fp6 c0, c1;
+};
+
+#if defined(DG_OPCOUNT)
+// host-only instrumented build (tools/opcount): counts Montgomery multiplications (squarings included)
+extern thread_local uint64_t g_fp_mul_count;
+#define DG_COUNT_MUL() (++g_fp_mul_count)
+#else
+#define DG_COUNT_MUL() ((void)0)
+#endif
+
+DGI uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+  uint64_t s = (uint64_t)a + b + cin;
+  *cout = (uint32_t)(s >> 32);
+  return (uint32_t)s;
+}
+DGI uint32_t subb32(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+  uint64_t d = (uint64_t)a - b - bin;
+  *bout = (uint32_t)(d >> 63);
+  return (uint32_t)d;
+}
+
+DGI Fp fp_const(const uint32_t (&c)[12]) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.l[i] = c[i];
+  return r;
+}
+DGI Fp fp_zero() {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.l[i] = 0;
+  return r;
+}
+DGI Fp fp_one() { return fp_const(FP_ONE); }
+
+DGI bool fp_is_zero(const Fp& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) o |= a.l[i];
+  return o == 0;
+}
+DGI bool fp_eq(const Fp& a, const Fp& b) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) o |= a.l[i] ^ b.l[i];
+  return o == 0;
+}
+// r = c ? b : a
+DGI Fp fp_sel(bool c, const Fp& a, const Fp& b) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.l[i] = c ? b.l[i] : a.l[i];
+  return r;
+}
+
+// a - p if a >= p (a < 2^384)
+DGI Fp fp_reduce_once(const Fp& a) {
+  Fp d;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) d.l[i] = subb32(a.l[i], P_LIMBS[i], br, &br);
+  return fp_sel(br == 0, a, d);
+}
+
+DGI Fp fp_add(const Fp& a, const Fp& b) {
+  Fp s;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) s.l[i] = addc32(a.l[i], b.l[i], c, &c);
+  return fp_reduce_once(s);
+}
+DGI Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
+DGI Fp fp_sub(const Fp& a, const Fp& b) {
+  Fp d;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) d.l[i] = subb32(a.l[i], b.l[i], br, &br);
+  uint32_t mask = 0u - br;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) d.l[i] = addc32(d.l[i], P_LIMBS[i] & mask, c, &c);
+  return d;
+}
+DGI Fp fp_neg(const Fp& a) {
+  // p - a, and 0 -> 0
+  Fp d;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) d.l[i] = subb32(P_LIMBS[i], a.l[i], br, &br);
+  return fp_sel(fp_is_zero(a), d, a);
+}
+
+// Montgomery multiplication.  Device: product-scanning inline-asm block (tools/gen_fp_asm.py).
+// Host (tests/native only): CIOS without the extra carry word (valid since p[11] < 2^31 - 1).
+DGI Fp fp_mul(const Fp& a, const Fp& b) {
+  DG_COUNT_MUL();
+#if defined(DG_FP_ASM)
+  Fp r;
+  fp_mont_mul_asm(r.l, a.l, b.l, P_LIMBS, P_INV32);
+  return fp_reduce_once(r);
+#else
+  uint32_t t[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t p = (uint64_t)a.l[0] * b.l[i] + t[0];
+    uint32_t A = (uint32_t)(p >> 32);
+    uint32_t t0 = (uint32_t)p;
+    uint32_t m = t0 * P_INV32;
+    uint64_t q = (uint64_t)m * P_LIMBS[0] + t0;
+    uint32_t C = (uint32_t)(q >> 32);
+#pragma unroll
+    for (int j = 1; j < 12; ++j) {
+      p = (uint64_t)a.l[j] * b.l[i] + t[j] + A;
+      A = (uint32_t)(p >> 32);
+      q = (uint64_t)m * P_LIMBS[j] + (uint32_t)p + C;
+      C = (uint32_t)(q >> 32);
+      t[j - 1] = (uint32_t)q;
+    }
+    t[11] = C + A;
+  }
+  Fp r;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) r.l[j] = t[j];
+  return fp_reduce_once(r);
+#endif
+}
+DGI Fp fp_sqr(const Fp& a) {
+#if defined(DG_FP_ASM)
+  DG_COUNT_MUL();
+  Fp r;
+  fp_mont_sqr_asm(r.l, a.l, P_LIMBS, P_INV32);
+  return fp_reduce_once(r);
+#else
+  return fp_mul(a, a);
+#endif
+}
+
+// plain integer (little-endian limbs) -> Montgomery
+DGI Fp fp_to_mont(const Fp& a) { return fp_mul(a, fp_const(FP_R2)); }
+DGI Fp fp_from_mont(const Fp& a) {
+  Fp one = fp_zero();
+  one.l[0] = 1;
+  return fp_mul(a, one);
+}
+DGI Fp fp_small(uint32_t v) {
+  Fp a = fp_zero();
+  a.l[0] = v;
+  return fp_to_mont(a);
+}
+
+// x^e for a fixed exponent given as a width-3 sliding-window schedule (tools/gen_constants.py).
+// The schedule is wave-uniform (scalar loads); the odd-power table is selected with v_cndmask.
+template <int NSTEPS>
+DGI Fp fp_pow_sched(const Fp& x, int first, const int8_t (&steps)[NSTEPS][2]) {
+  Fp x2 = fp_sqr(x);
+  Fp t0 = x;
+  Fp t1 = fp_mul(t0, x2);
+  Fp t2 = fp_mul(t1, x2);
+  Fp t3 = fp_mul(t2, x2);
+  Fp acc = first == 0 ? t0 : first == 1 ? t1 : first == 2 ? t2 : t3;
+  for (int s = 0; s < NSTEPS; ++s) {
+    int k = steps[s][0];
+    int idx = steps[s][1];
+    for (int j = 0; j < k; ++j) acc = fp_sqr(acc);
+    if (idx >= 0) {
+      Fp m = fp_sel(idx == 1, t0, t1);
+      m = fp_sel(idx == 2, m, t2);
+      m = fp_sel(idx == 3, m, t3);
+      acc = fp_mul(acc, m);
+    }
+  }
+  return acc;
+}
+DGI Fp fp_inv(const Fp& a) { return fp_pow_sched(a, EXP_PM2_FIRST, EXP_PM2_STEPS); }
+// returns x^((p-3)/4)
+DGI Fp fp_pow_pm3d4(const Fp& a) { return fp_pow_sched(a, EXP_PM3D4_FIRST, EXP_PM3D4_STEPS); }
+// sqrt(a) if a is a square (r^2 == a checked by the caller or via return)
+DGI bool fp_sqrt(Fp& r, const Fp& a) {
+  Fp t = fp_pow_pm3d4(a);
+  Fp s = fp_mul(t, a);  // a^((p+1)/4)
+  r = s;
+  return fp_eq(fp_sqr(s), a);
+}
+
+// compare plain (non-Montgomery) value against (p-1)/2: returns a > (p-1)/2
+DGI bool fp_plain_gt_half(const Fp& a) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) (void)subb32(FP_HALF_PM1[i], a.l[i], br, &br);
+  return br != 0;
+}
+DGI bool fp_lex_largest(const Fp& a) { return fp_plain_gt_half(fp_from_mont(a)); }
+DGI uint32_t fp_parity(const Fp& a) { return fp_from_mont(a).l[0] & 1u; }
+
+// big-endian 48 B (top 3 bits of byte 0 masked by caller) -> limbs; returns false if >= p
+DGI bool fp_from_be48_plain(Fp& r, const uint8_t* b) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const uint8_t* q = b + 44 - 4 * i;
+    r.l[i] = (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | q[3];
+  }
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) (void)subb32(r.l[i], P_LIMBS[i], br, &br);
+  return br != 0;
+}
+DGI void fp_to_be48(uint8_t* b, const Fp& a) {
+  Fp x = fp_from_mont(a);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint8_t* q = b + 44 - 4 * i;
+    q[0] = (uint8_t)(x.l[i] >> 24);
+    q[1] = (uint8_t)(x.l[i] >> 16);
+    q[2] = (uint8_t)(x.l[i] >> 8);
+    q[3] = (uint8_t)x.l[i];
+  }
+}
+// 64 B big-endian (hash_to_field, RFC 9380 §5.2, L = 64) -> Fp: hi * 2^256 + lo mod p
+DGI Fp fp_from_be64(const uint8_t* b) {
+  Fp hi = fp_zero(), lo = fp_zero();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint8_t* q = b + 28 - 4 * i;
+    hi.l[i] = (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | q[3];
+    const uint8_t* w = b + 60 - 4 * i;
+    lo.l[i] = (uint32_t)w[0] << 24 | (uint32_t)w[1] << 16 | (uint32_t)w[2] << 8 | w[3];
+  }
+  // values < 2^256 < p: to Montgomery, then hi * (2^256 in Montgomery)
+  return fp_add(fp_mul(fp_to_mont(hi), fp_const(FP_2POW256)), fp_to_mont(lo));
+}
+
+// ------------------------------------------------------------------------------------------- Fp2
+DGI Fp2 fp2_const(const uint32_t (&c)[2][12]) {
+  Fp2 r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    r.c0.l[i] = c[0][i];
+    r.c1.l[i] = c[1][i];
+  }
+  return r;
+}
+DGI Fp2 fp2_zero() { return Fp2{fp_zero(), fp_zero()}; }
+DGI Fp2 fp2_one() { return Fp2{fp_one(), fp_zero()}; }
+DGI bool fp2_is_zero(const Fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+DGI bool fp2_eq(const Fp2& a, const Fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+DGI Fp2 fp2_sel(bool c, const Fp2& a, const Fp2& b) { return Fp2{fp_sel(c, a.c0, b.c0), fp_sel(c, a.c1, b.c1)}; }
+DGI Fp2 fp2_add(const Fp2& a, const Fp2& b) { return Fp2{fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+DGI Fp2 fp2_sub(const Fp2& a, const Fp2& b) { return Fp2{fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+DGI Fp2 fp2_dbl(const Fp2& a) { return Fp2{fp_dbl(a.c0), fp_dbl(a.c1)}; }
+DGI Fp2 fp2_neg(const Fp2& a) { return Fp2{fp_neg(a.c0), fp_neg(a.c1)}; }
+DGI Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
+DGI Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
+  Fp t0 = fp_mul(a.c0, b.c0);
+  Fp t1 = fp_mul(a.c1, b.c1);
+  Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+DGI Fp2 fp2_sqr(const Fp2& a) {
+  Fp m = fp_mul(a.c0, a.c1);
+  return Fp2{fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(m)};
+}
+DGI Fp2 fp2_mul_fp(const Fp2& a, const Fp& b) { return Fp2{fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
+DGI Fp2 fp2_mul_xi(const Fp2& a) { return Fp2{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }  // (1+u) a
+DGI Fp fp2_norm(const Fp2& a) { return fp_add(fp_sqr(a.c0), fp_sqr(a.c1)); }
+DGI Fp2 fp2_inv(const Fp2& a) {
+  Fp n = fp_inv(fp2_norm(a));
+  return Fp2{fp_mul(a.c0, n), fp_neg(fp_mul(a.c1, n))};
+}
+// RFC 9380 §4.1 sgn0 for m = 2
+DGI uint32_t fp2_sgn0(const Fp2& a) {
+  Fp x0 = fp_from_mont(a.c0);
+  Fp x1 = fp_from_mont(a.c1);
+  uint32_t sign0 = x0.l[0] & 1u;
+  uint32_t zero0 = fp_is_zero(x0) ? 1u : 0u;
+  uint32_t sign1 = x1.l[0] & 1u;
+  return sign0 | (zero0 & sign1);
+}
+// ZCash sort flag for Fp2: c1 decides unless zero
+DGI bool fp2_lex_largest(const Fp2& a) {
+  Fp x1 = fp_from_mont(a.c1);
+  if (!fp_is_zero(x1)) return fp_plain_gt_half(x1);
+  return fp_plain_gt_half(fp_from_mont(a.c0));
+}
+
+// Square root in Fp2 with two Fp exponentiations ("complex method"):
+//   s = sqrt(a0^2 + a1^2), c = (a0 + s)/2, t = c^((p-3)/4)
+//   c square:      x = c t + (a1 t / 2) u
+//   c non-square:  x = (a1 t / 2) - c t u           (since c t^2 = -1)
+// `norm_sqrt` may be supplied by the caller (SSWU gx2 shortcut); result verified by squaring.
+DGI bool fp2_sqrt_with_norm_root(Fp2& r, const Fp2& a, const Fp& s) {
+  Fp half = fp_const(FP_TWO_INV);
+  Fp x0, x1;
+  if (fp_is_zero(a.c1)) {
+    // a in Fp: sqrt(a0) or sqrt(-a0) * u
+    Fp y;
+    bool sq = fp_sqrt(y, a.c0);
+    if (sq) {
+      x0 = y;
+      x1 = fp_zero();
+    } else {
+      fp_sqrt(y, fp_neg(a.c0));
+      x0 = fp_zero();
+      x1 = y;
+    }
+  } else {
+    Fp c = fp_mul(fp_add(a.c0, s), half);
+    Fp t = fp_pow_pm3d4(c);
+    Fp ct = fp_mul(c, t);
+    Fp at2 = fp_mul(fp_mul(a.c1, t), half);
+    bool c_square = fp_eq(fp_mul(ct, t), fp_one());
+    x0 = fp_sel(c_square, at2, ct);
+    x1 = fp_sel(c_square, fp_neg(ct), at2);
+  }
+  r = Fp2{x0, x1};
+  return fp2_eq(fp2_sqr(r), a);
+}
+DGI bool fp2_sqrt(Fp2& r, const Fp2& a) {
+  Fp n = fp2_norm(a);
+  Fp s;
+  if (!fp_sqrt(s, n)) return false;
+  return fp2_sqrt_with_norm_root(r, a, s);
+}
+
+// ------------------------------------------------------------------------------------------- Fp6
+DGI Fp6 fp6_zero() { return Fp6{fp2_zero(), fp2_zero(), fp2_zero()}; }
+DGI Fp6 fp6_add(const Fp6& a, const Fp6& b) { return Fp6{fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)}; }
+DGI Fp6 fp6_sub(const Fp6& a, const Fp6& b) { return Fp6{fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
+DGI Fp6 fp6_neg(const Fp6& a) { return Fp6{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
+DGI Fp6 fp6_mul_v(const Fp6& a) { return Fp6{fp2_mul_xi(a.c2), a.c0, a.c1}; }
+DGI Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
+  Fp2 v0 = fp2_mul(a.c0, b.c0);
+  Fp2 v1 = fp2_mul(a.c1, b.c1);
+  Fp2 v2 = fp2_mul(a.c2, b.c2);
+  Fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), v1), v2)), v0);
+  Fp2 c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), v0), v1), fp2_mul_xi(v2));
+  Fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), v0), v2), v1);
+  return Fp6{c0, c1, c2};
+}
+DGI Fp6 fp6_sqr(const Fp6& a) {
+  // CH-SQR2
+  Fp2 s0 = fp2_sqr(a.c0);
+  Fp2 ab = fp2_mul(a.c0, a.c1);
+  Fp2 s1 = fp2_dbl(ab);
+  Fp2 s2 = fp2_sqr(fp2_add(fp2_sub(a.c0, a.c1), a.c2));
+  Fp2 bc = fp2_mul(a.c1, a.c2);
+  Fp2 s3 = fp2_dbl(bc);
+  Fp2 s4 = fp2_sqr(a.c2);
+  Fp2 c0 = fp2_add(fp2_mul_xi(s3), s0);
+  Fp2 c1 = fp2_add(fp2_mul_xi(s4), s1);
+  Fp2 c2 = fp2_sub(fp2_sub(fp2_add(fp2_add(s1, s2), s3), s0), s4);
+  return Fp6{c0, c1, c2};
+}
+DGN Fp6 fp6_inv(const Fp6& a) {
+  Fp2 c0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+  Fp2 c1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+  Fp2 c2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+  Fp2 t = fp2_add(fp2_mul_xi(fp2_add(fp2_mul(a.c2, c1), fp2_mul(a.c1, c2))), fp2_mul(a.c0, c0));
+  t = fp2_inv(t);
+  return Fp6{fp2_mul(c0, t), fp2_mul(c1, t), fp2_mul(c2, t)};
+}
+// (a0 + a1 v + a2 v^2) * (b0 + b1 v)
+DGI Fp6 fp6_mul_01(const Fp6& a, const Fp2& b0, const Fp2& b1) {
+  Fp2 v0 = fp2_mul(a.c0, b0);
+  Fp2 v1 = fp2_mul(a.c1, b1);
+  Fp2 c0 = fp2_add(fp2_mul_xi(fp2_mul(a.c2, b1)), v0);
+  Fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b0, b1)), v0), v1);
+  Fp2 c2 = fp2_add(fp2_mul(a.c2, b0), v1);
+  return Fp6{c0, c1, c2};
+}
+// (a0 + a1 v + a2 v^2) * (b1 v)
+DGI Fp6 fp6_mul_1(const Fp6& a, const Fp2& b1) {
+  return Fp6{fp2_mul_xi(fp2_mul(a.c2, b1)), fp2_mul(a.c0, b1), fp2_mul(a.c1, b1)};
+}
+
+// ------------------------------------------------------------------------------------------- Fp12
+DGI Fp12 fp12_one() { return Fp12{Fp6{fp2_one(), fp2_zero(), fp2_zero()}, fp6_zero()}; }
+DGI bool fp12_is_one(const Fp12& a) {
+  return fp2_eq(a.c0.c0, fp2_one()) && fp2_is_zero(a.c0.c1) && fp2_is_zero(a.c0.c2) && fp2_is_zero(a.c1.c0) &&
+         fp2_is_zero(a.c1.c1) && fp2_is_zero(a.c1.c2);
+}
+DGI Fp12 fp12_conj(const Fp12& a) { return Fp12{a.c0, fp6_neg(a.c1)}; }
+DGN Fp12 fp12_mul(const Fp12& a, const Fp12& b) {
+  Fp6 t0 = fp6_mul(a.c0, b.c0);
+  Fp6 t1 = fp6_mul(a.c1, b.c1);
+  Fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
+  return Fp12{fp6_add(t0, fp6_mul_v(t1)), c1};
+}
+DGN Fp12 fp12_sqr(const Fp12& a) {
+  // complex squaring: (a0 + a1 w)^2 = (a0^2 + v a1^2) + 2 a0 a1 w
+  Fp6 ab = fp6_mul(a.c0, a.c1);
+  Fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  Fp6 c0 = fp6_sub(fp6_sub(s, ab), fp6_mul_v(ab));
+  return Fp12{c0, fp6_add(ab, ab)};
+}
+DGN Fp12 fp12_inv(const Fp12& a) {
+  Fp6 t = fp6_sub(fp6_mul(a.c0, a.c0), fp6_mul_v(fp6_mul(a.c1, a.c1)));
+  t = fp6_inv(t);
+  return Fp12{fp6_mul(a.c0, t), fp6_neg(fp6_mul(a.c1, t))};
+}
+// multiply by the sparse line l = c0 + c1 v + c4 v w (M-type twist; slots 0, 1, 4)
+DGN Fp12 fp12_mul_014(const Fp12& f, const Fp2& c0, const Fp2& c1, const Fp2& c4) {
+  Fp6 aa = fp6_mul_01(f.c0, c0, c1);
+  Fp6 bb = fp6_mul_1(f.c1, c4);
+  Fp6 s = fp6_mul_01(fp6_add(f.c0, f.c1), c0, fp2_add(c1, c4));
+  Fp6 n1 = fp6_sub(fp6_sub(s, aa), bb);
+  Fp6 n0 = fp6_add(fp6_mul_v(bb), aa);
+  return Fp12{n0, n1};
+}
+DGN Fp12 fp12_frob(const Fp12& a) {
+  Fp2 g1 = fp2_const(FROB_G1), g2 = fp2_const(FROB_G2), d = fp2_const(FROB_D);
+  Fp6 b0{fp2_conj(a.c0.c0), fp2_mul(fp2_conj(a.c0.c1), g1), fp2_mul(fp2_conj(a.c0.c2), g2)};
+  Fp2 dg1 = fp2_mul(d, g1), dg2 = fp2_mul(d, g2);
+  Fp6 b1{fp2_mul(fp2_conj(a.c1.c0), d), fp2_mul(fp2_conj(a.c1.c1), dg1), fp2_mul(fp2_conj(a.c1.c2), dg2)};
+  return Fp12{b0, b1};
+}
+
+}  // namespace dg

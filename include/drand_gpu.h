@@ -1,0 +1,122 @@
+/* drand_gpu.h -- C-ABI of the MI355X threshold-BLS engine (libdrandgpu.so).
+ *
+ * The drop-in boundary for drand's signature scheme: drand reaches it through `key.Scheme`
+ * (key/curve.go:30, `tbls.NewThresholdSchemeOnG2(Pairing)`, a kyber `sign.ThresholdScheme`), which the
+ * beacon is handed via `beacon.Config.Scheme` (beacon/beacon.go:33, set at core/drand.go:335).  A Go
+ * `gpu/` package implements that interface with cgo calls into the functions below;
+ * points cross the boundary only as bytes (kyber `MarshalBinary`: 48 B G1, 96 B G2, 98 B partials =
+ * BE16 index || 96 B G2).
+ *
+ * Conventions
+ *   - Return value: 0 on success, < 0 on a fatal error (see DG_E_*); dg_last_error() has the text.
+ *   - Per-item results are written to caller-owned `status` arrays (DG_ST_*).  Error *text* parity
+ *     with kyber is not provided; nil / non-nil parity is: status != DG_ST_OK <=> kyber returns an error.
+ *   - Buffers are borrowed for the duration of the call only (cgo pointer rules); nothing is retained.
+ *   - Thread-safe: calls on one process-wide context are serialised by a mutex (beacon/beacon.go:124
+ *     calls the scheme from concurrent gRPC handlers).
+ *   - All arithmetic runs in HIP kernels on the selected MI355X (gfx950).  There is no CPU fallback:
+ *     without a device every compute entry point returns DG_E_NODEV.
+ *   - `msg_len` is the per-item message length (drand: 32 B SHA-256 outputs); all items of one call
+ *     share it.  Messages are laid out back to back (n x msg_len bytes).
+ */
+#ifndef DRAND_GPU_H
+#define DRAND_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* per-item status */
+#define DG_ST_OK 0
+#define DG_ST_BAD_SIG 1      /* pairing check failed                               */
+#define DG_ST_SIG_DECODE 2   /* sigma: bad flags / non-canonical / off-curve / off-subgroup */
+#define DG_ST_BAD_INDEX 3    /* partial signature too short to carry an index      */
+#define DG_ST_PK_DECODE 4    /* public key / commitment does not decode             */
+#define DG_ST_NOT_ENOUGH 5   /* Recover: fewer than t distinct valid shares         */
+#define DG_ST_NOT_EXAMINED 255 /* Recover: partial after the t-th collected one       */
+
+/* fatal return codes */
+#define DG_E_NODEV (-1)
+#define DG_E_ARG (-2)
+#define DG_E_HIP (-3)
+#define DG_E_NOMEM (-4)
+
+/* Select the HIP device this process uses (one process per GPU).  Idempotent for the same device. */
+int dg_init(int device);
+void dg_shutdown(void);
+const char* dg_last_error(void);
+/* 1 if the library runs on a gfx950 device after dg_init, else 0 */
+int dg_device_ready(void);
+
+/* A9 -- hash-to-G2 (RFC 9380 XMD:SHA-256_SSWU_RO_ with `dst`), compressed 96 B per message.
+ * Replaces kyber's hashablePoint.Hash used inside bls.Sign / bls.Verify [UPSTREAM]. */
+int dg_hash_to_g2(size_t n, const uint8_t* msgs, size_t msg_len, const uint8_t* dst, size_t dst_len, uint8_t* out96);
+
+/* A7 -- tbls.Sign (beacon/beacon.go:433): out = BE16(index) || compress(x_i * H(msg)), 98 B each.
+ * scalars32: n x 32 B big-endian (reduced mod r).  If `index` is NULL the 96 B bls.Sign output is written. */
+int dg_sign(size_t n, const uint8_t* scalars32, const uint16_t* index, const uint8_t* msgs, size_t msg_len,
+            uint8_t* out);
+
+/* A3/A4 -- tbls.VerifyRecovered / bls.Verify batch against one key (beacon/beacon.go:494,575,
+ * beacon/chain.go:70, core/client_public.go:116).  Random-linear-combination multi-pairing with one
+ * shared final exponentiation; on a failed batch, every item is re-checked on its own so `status` is
+ * exactly the per-item bls.Verify verdict.  `seed` keys the 64-bit RLC coefficients (0: from the OS). */
+int dg_verify(const uint8_t pk48[48], size_t n, const uint8_t* msgs, size_t msg_len, const uint8_t* sigs96,
+              uint8_t* status, uint64_t seed);
+
+/* A1 + A3 -- beacon.VerifyBeacon over a batch (beacon/chain.go:65-71): msg = SHA256(BE64(prev_round) ||
+ * prev_sig || BE64(round)) computed on the device, then as dg_verify.  prev_sig of item i is
+ * prev_sigs[prev_sig_off[i] .. prev_sig_off[i+1]) (96 B, or the 32 B genesis seed for round 1). */
+int dg_verify_beacons(const uint8_t pk48[48], size_t n, const uint64_t* prev_round, const uint64_t* round,
+                      const uint8_t* prev_sigs, const uint32_t* prev_sig_off, const uint8_t* sigs96,
+                      uint8_t* status, uint64_t seed);
+
+/* A13 -- chain-link check of syncFrom (beacon/beacon.go:561-573) for items i = 0..n-1 against the
+ * previous item (item 0 against cur_round / cur_sig): 0 = linked, 1 = broken. */
+int dg_check_links(uint64_t cur_round, const uint8_t* cur_sig, size_t cur_sig_len, size_t n,
+                   const uint64_t* prev_round, const uint64_t* round, const uint8_t* prev_sigs,
+                   const uint32_t* prev_sig_off, const uint8_t* sigs96, uint8_t* link_status);
+
+/* A1 -- beacon.Message batch (beacon/chain.go:86-94). */
+int dg_beacon_messages(size_t n, const uint64_t* prev_round, const uint64_t* round, const uint8_t* prev_sigs,
+                       const uint32_t* prev_sig_off, uint8_t* out32);
+
+/* A2 -- RandomnessFromSignature batch (beacon/chain.go:52-55): SHA-256 of each 96 B signature. */
+int dg_randomness(size_t n, const uint8_t* sigs96, uint8_t* out32);
+
+/* A12 -- share.PubPoly.Eval batch: Horner over t G1 commits at x = index + 1, compressed 48 B. */
+int dg_pubpoly_eval(const uint8_t* commits48, uint32_t t, size_t n, const uint32_t* index, uint8_t* out48);
+
+/* A5 -- tbls.VerifyPartial batch (beacon/beacon.go:148): `rounds` messages, k partials (98 B) per round,
+ * status[r*k + j].  X_i = PubPoly.Eval(i) is computed once per distinct index on the device. */
+int dg_verify_partials(const uint8_t* commits48, uint32_t t, size_t rounds, const uint8_t* msgs, size_t msg_len,
+                       uint32_t k, const uint8_t* partials98, uint8_t* status, uint64_t seed);
+
+/* A6 -- tbls.Recover batch (beacon/beacon.go:488): per round, the first t partials (input order) that
+ * pass VerifyPartial, deduplicated by index, Lagrange-interpolated at 0 on G2.  round_status[r] is
+ * DG_ST_OK or DG_ST_NOT_ENOUGH; share_status[r*k + j] is the VerifyPartial status of partials Recover
+ * examined and DG_ST_NOT_EXAMINED for the rest. */
+int dg_recover(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t rounds, const uint8_t* msgs,
+               size_t msg_len, uint32_t k, const uint8_t* partials98, uint8_t* out_sig96, uint8_t* round_status,
+               uint8_t* share_status, uint64_t seed);
+
+/* ---- device-resident variants (bench / multi-GPU path): pointers are device memory on the current
+ * device, work is enqueued on `stream` (a hipStream_t; NULL = the library's stream) and completes before
+ * return.  Semantics as the host versions. */
+int dg_verify_beacons_dev(const uint8_t* pk48_host, size_t n, const uint64_t* d_prev_round, const uint64_t* d_round,
+                          const uint8_t* d_prev_sigs, const uint32_t* d_prev_sig_off, const uint8_t* d_sigs96,
+                          uint8_t* d_status, uint64_t seed, void* stream);
+
+/* Per-kernel HIP-event timing on the launch stream (off by default); resets the accumulated table. */
+int dg_set_timing(int on);
+
+/* kernel timing of the last call on this context: number of entries written (<= cap);
+ * names/us are kernel-name pointers (static strings) and average microseconds per launch. */
+int dg_last_timings(const char** names, double* us, int* launches, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -70,8 +70,13 @@ class PriPoly:
         return [B.G1C.mul(B.G1_GEN, c) for c in self.coeffs]
 
 
+def _points(commits):
+    return [B.g1_decompress(bytes(c)) if isinstance(c, (bytes, bytearray)) else c for c in commits]
+
+
 def pubpoly_eval(commits, i):
-    """Horner in G1 at x = i+1 (kyber share.PubPoly.Eval)."""
+    """Horner in G1 at x = i+1 (kyber share.PubPoly.Eval); commits as points or 48 B encodings."""
+    commits = _points(commits)
     x = i + 1
     acc = None
     for c in reversed(commits):

@@ -1,0 +1,96 @@
+// Host build of the HIP kernels' device arithmetic (drand_amd/csrc/*.h) for step-by-step debugging
+// against oracle/ on CPU.  TEST TOOL ONLY: never linked into the product library.
+#include <string.h>
+#include "../../drand_amd/csrc/pairing.h"
+#include "../../drand_amd/csrc/h2c.h"
+using namespace dg;
+extern "C" {
+void hc_fp_mul(const uint8_t* a48, const uint8_t* b48, uint8_t* out48) {
+  Fp a, b;
+  fp_from_be48_plain(a, a48);
+  fp_from_be48_plain(b, b48);
+  fp_to_be48(out48, fp_mul(fp_to_mont(a), fp_to_mont(b)));
+}
+int hc_fp2_sqrt(const uint8_t* a96, uint8_t* out96) {
+  Fp a0, a1;
+  fp_from_be48_plain(a0, a96);
+  fp_from_be48_plain(a1, a96 + 48);
+  Fp2 a{fp_to_mont(a0), fp_to_mont(a1)}, r;
+  bool ok = fp2_sqrt(r, a);
+  fp_to_be48(out96, r.c0);
+  fp_to_be48(out96 + 48, r.c1);
+  return ok;
+}
+void hc_hash_to_g2(const uint8_t* msg, uint32_t n, const uint8_t* dst, uint32_t dl, uint8_t* out96) {
+  g2_compress_aff(out96, g2_to_aff(hash_to_g2(msg, n, dst, dl)));
+}
+int hc_g2_roundtrip(const uint8_t* in96, uint8_t* out96) {
+  G2A a;
+  if (!g2_decompress(a, in96, true)) return 0;
+  g2_compress_aff(out96, a);
+  return 1;
+}
+int hc_g1_roundtrip(const uint8_t* in48, uint8_t* out48) {
+  G1A a;
+  if (!g1_decompress(a, in48, true)) return 0;
+  g1_compress_aff(out48, a);
+  return 1;
+}
+static const uint8_t DSTN[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_";
+int hc_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t n, const uint8_t* sig96) {
+  G1A pk;
+  if (!g1_decompress(pk, pk48, true)) return 4;
+  G2A s;
+  if (!g2_decompress(s, sig96, true)) return 2;
+  G2A h = g2_to_aff(hash_to_g2(msg, n, DSTN, 43));
+  G1A P[2];
+  G2A Q[2];
+  int np = 0;
+  if (!pk.inf && !h.inf) { P[np] = pk; Q[np] = h; ++np; }
+  if (!s.inf) { P[np] = G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false}; Q[np] = s; ++np; }
+  if (np == 0) return 0;
+  Fp12 f = miller_loop<2>(P, Q, np);
+  return fp12_is_one(final_exp_cubed(f)) ? 0 : 1;
+}
+}
+extern "C" int hc_pairing_cubed(const uint8_t* g1_48, const uint8_t* g2_96, uint8_t* out576, int variant) {
+  G1A p;
+  G2A q;
+  if (!g1_decompress(p, g1_48, true)) return 4;
+  if (!g2_decompress(q, g2_96, true)) return 2;
+  Fp12 f = miller_loop<1>(&p, &q, 1);
+  Fp12 r = variant == 1 ? f : final_exp_cubed(f);
+  const Fp2* s[6] = {&r.c0.c0, &r.c0.c1, &r.c0.c2, &r.c1.c0, &r.c1.c1, &r.c1.c2};
+  for (int i = 0; i < 6; ++i) { fp_to_be48(out576 + 96 * i, s[i]->c0); fp_to_be48(out576 + 96 * i + 48, s[i]->c1); }
+  return 0;
+}
+extern "C" void hc_fp12_test(const uint8_t* a576, const uint8_t* b576, uint8_t* out576, int op) {
+  Fp12 a, b;
+  Fp2* sa[6] = {&a.c0.c0, &a.c0.c1, &a.c0.c2, &a.c1.c0, &a.c1.c1, &a.c1.c2};
+  Fp2* sb[6] = {&b.c0.c0, &b.c0.c1, &b.c0.c2, &b.c1.c0, &b.c1.c1, &b.c1.c2};
+  for (int i = 0; i < 6; ++i) {
+    Fp x;
+    fp_from_be48_plain(x, a576 + 96 * i); sa[i]->c0 = fp_to_mont(x);
+    fp_from_be48_plain(x, a576 + 96 * i + 48); sa[i]->c1 = fp_to_mont(x);
+    fp_from_be48_plain(x, b576 + 96 * i); sb[i]->c0 = fp_to_mont(x);
+    fp_from_be48_plain(x, b576 + 96 * i + 48); sb[i]->c1 = fp_to_mont(x);
+  }
+  Fp12 r = op == 0 ? fp12_mul(a, b) : op == 1 ? fp12_sqr(a) : op == 2 ? fp12_inv(a) : op == 3 ? fp12_frob(a)
+         : fp12_mul_014(a, b.c0.c0, b.c0.c1, b.c1.c1);
+  const Fp2* s[6] = {&r.c0.c0, &r.c0.c1, &r.c0.c2, &r.c1.c0, &r.c1.c1, &r.c1.c2};
+  for (int i = 0; i < 6; ++i) { fp_to_be48(out576 + 96 * i, s[i]->c0); fp_to_be48(out576 + 96 * i + 48, s[i]->c1); }
+}
+extern "C" int hc_verify_dbg(const uint8_t* pk48, const uint8_t* msg, uint32_t n, const uint8_t* sig96, uint8_t* h96) {
+  G1A pk;
+  g1_decompress(pk, pk48, true);
+  G2A s;
+  g2_decompress(s, sig96, true);
+  G2A h = g2_to_aff(hash_to_g2(msg, n, DSTN, 43));
+  g2_compress_aff(h96, h);
+  G1A P[2] = {pk, G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false}};
+  G2A Q[2] = {h, s};
+  Fp12 f1 = final_exp_cubed(miller_loop<1>(&P[0], &Q[0], 1));
+  Fp12 f2 = final_exp_cubed(miller_loop<1>(&P[1], &Q[1], 1));
+  Fp12 f12 = final_exp_cubed(miller_loop<2>(P, Q, 2));
+  return (fp12_is_one(fp12_mul(f1, f2)) ? 1 : 0) | (fp12_is_one(f12) ? 2 : 0);
+}

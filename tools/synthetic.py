@@ -1,0 +1,45 @@
+"""Deterministic synthetic drand group + chain definitions shared by tests, smoke() and bench.py.
+
+Replaces kyber's `random.New()` (beacon/beacon_test.go:45, test/dkg.go) with a SHA-256 counter DRBG so
+every run sees the same group and chain.  One master secret x signs the chain; the (n, t) groups of
+BASELINE.json's configs are degree-(t-1) polynomials with p(0) = x, so every config's recovered
+signature for round r equals the chain's sigma_r.
+
+This module holds no curve arithmetic: commits / signatures are produced by whoever calls it
+(the CPU twin for fixtures, the GPU for bulk partials).
+"""
+import hashlib
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+# GenesisSeed of the reference's deploy/200409/group.toml:5 used as round-0 "signature".
+GENESIS_SEED = bytes.fromhex("770f3c2578a95387b358e02aba5d5008a53ce40047a1fa326dde0dfd0b482a8e")
+LABEL = b"drand-amd/synthetic/v1"
+
+
+def drbg_scalar(label, counter):
+    h = hashlib.sha256(LABEL + b"/" + label + b"/" + counter.to_bytes(8, "big")).digest()
+    h2 = hashlib.sha256(h + b"/2").digest()
+    return int.from_bytes(h + h2, "big") % R
+
+
+def master_secret():
+    return drbg_scalar(b"master", 0)
+
+
+def poly_coeffs(t):
+    """Coefficients a_0..a_{t-1} with a_0 = the master secret."""
+    return [master_secret()] + [drbg_scalar(b"poly-t%d" % t, j) for j in range(1, t)]
+
+
+def share_value(coeffs, i):
+    """PriPoly share of index i (x = i + 1), kyber share.PriPoly.Eval."""
+    x = i + 1
+    acc = 0
+    for c in reversed(coeffs):
+        acc = (acc * x + c) % R
+    return acc
+
+
+def chain_path(n):
+    import os
+    return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "chain_v1_%d.bin" % n)
