@@ -1,0 +1,203 @@
+"""Benchmark of the threshold-BLS hot path (BASELINE.json): verified beacon rounds/s.
+
+A step = one dg_verify_beacons_dev pass over this rank's contiguous range of the synthetic linked chain
+(beacon.Message on the device, hash-to-G2, sigma decode + subgroup check, RLC multi-pairing with one
+shared final exponentiation; BASELINE configs[1] at N = 1: 100k rounds, one shared group key), inputs
+resident in HBM, followed by the RCCL all-gather of the per-round verdict bitmaps (configs[3] at N > 1,
+one contiguous round range per GPU, weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rounds R] [--no-cpu-baseline]
+
+Rank 0 prints ONE JSON line (contract in the task statement); the roofline object is the integer
+multiply-add rate of the dominant kernel (algorithmic MACs from profiles/opcounts.json / its average
+HIP-event duration measured live on the launch stream) against the measured v_mad_u64_u32 peak.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from tools import synthetic as S  # noqa: E402
+
+METRIC = "verified beacon rounds/sec (pairing checks/s)"
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def load_chain(total):
+    """(sigs (total, 96), prev_sig of round 1) for rounds 1..total of the synthetic chain."""
+    best = None
+    d = os.path.join(ROOT, "data")
+    if os.path.isdir(d):
+        for f in os.listdir(d):
+            if f.startswith("chain_v1_") and f.endswith(".bin"):
+                n = int(f[len("chain_v1_"):-4])
+                if n >= total and (best is None or n < best[0]):
+                    best = (n, os.path.join(d, f))
+    if best is None:
+        return None
+    mm = np.memmap(best[1], dtype=np.uint8, mode="r", shape=(best[0], 96))
+    return np.array(mm[:total])
+
+
+def gpu_signed_rounds(lib_tbls, first, n, x):
+    """Fallback when no chain file is present: rounds first..first+n-1 whose prev_sig is a per-round
+    pseudo-random 96 B string (not the previous signature), signed on the GPU.  Same per-round work."""
+    import hashlib
+
+    prev = np.frombuffer(b"".join(hashlib.sha256(b"prev/%d" % r).digest() * 3 for r in range(first, first + n)),
+                         np.uint8).reshape(n, 96)
+    rr = np.arange(first, first + n, dtype=np.uint64)
+    msgs = lib_tbls.beacon_messages(rr - 1, rr, [bytes(p) for p in prev])
+    sigs = lib_tbls.sign_batch([x] * n, msgs)
+    return prev, sigs
+
+
+def cpu_baseline(pk, msgs, sigs, seconds=10.0, threads=16):
+    """The CPU twin (C port of the reference algorithm: one full pairing check per beacon) on a bounded
+    sample of the same rounds, `threads` POSIX threads."""
+    from oracle import twin
+
+    n0 = 64
+    t0 = time.time()
+    twin.verify_batch(pk, msgs[:n0], sigs[:n0], threads=1)
+    per = (time.time() - t0) / n0
+    n = int(min(len(sigs), max(n0, seconds * threads / per)))
+    t0 = time.time()
+    st = twin.verify_batch(pk, msgs[:n], sigs[:n], threads=threads)
+    dt = time.time() - t0
+    assert not st.any(), "CPU twin rejected a valid round"
+    return {"value": n / dt, "unit": "rounds/s", "cores": threads, "kind": "port",
+            "sample": "%d rounds of the same chain, CPU twin (oracle/twin, C restatement of the kyber per-item "
+                      "bls.Verify: 2 Miller loops + final exp per round), %d threads, %.1f s" % (n, threads, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--rounds", type=int, default=100000, help="rounds per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from drand_amd import _lib as L
+    from drand_amd import tbls, shard
+
+    lib = L.lib(local)
+    R = args.rounds
+    x = S.master_secret()
+    pk = S.GROUP_PK  # x * g1, the chain's group key (public fixture constant)
+    a, b = shard.round_range(world * R, world, rank)
+    chain = load_chain(world * R)
+    if chain is not None:
+        sigs = chain[a:b]
+        prev = chain[a - 1:b - 1] if a > 0 else np.concatenate([np.zeros((1, 96), np.uint8), chain[:b - 1]])
+        data = "synthetic linked chain data/chain_v1 (CPU-twin generated, seed tools/synthetic.py)"
+        linked = True
+    else:
+        prev, sigs = gpu_signed_rounds(tbls, a + 1, b - a, x)
+        data = "synthetic rounds, GPU-signed (no chain file: prev_sig pseudo-random, links not checked)"
+        linked = False
+    n = b - a
+    rounds = np.arange(a + 1, b + 1, dtype=np.uint64)
+    prev_sigs = [bytes(p) for p in prev]
+    if a == 0 and linked:
+        prev_sigs[0] = S.GENESIS_SEED
+    _, _, psb, off = tbls._beacon_arrays(rounds - 1, rounds, prev_sigs)
+    d_pr = torch.from_numpy((rounds - 1).astype(np.int64)).to(dev)
+    d_r = torch.from_numpy(rounds.astype(np.int64)).to(dev)
+    d_ps = torch.from_numpy(psb).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int32)).to(dev)
+    d_sig = torch.from_numpy(np.ascontiguousarray(sigs)).to(dev)
+    d_st = torch.full((n,), 99, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    pkb = ctypes.c_char_p(pk)
+
+    def step(seed):
+        L.check(lib.dg_verify_beacons_dev(pkb, n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off), L.ptr(d_sig),
+                                          L.ptr(d_st), seed, ctypes.c_void_p(stream.cuda_stream)))
+        return shard.allgather_verdicts(d_st, world)
+
+    for w in range(args.warmup):
+        step(1000 + w)
+    torch.cuda.synchronize()
+    bitmap = step(7)
+    assert int(d_st.max().item()) == 0, "valid chain rounds rejected"
+    assert bitmap.sum().item() == 0
+    if world > 1:
+        dist.barrier()
+    L.check(lib.dg_set_timing(1))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(17 + s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    kt = L.timings()
+    L.check(lib.dg_set_timing(0))
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    total = world * n * args.steps
+    if rank == 0:
+        oc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["per_unit"]
+        # dominant kernel over the timed region
+        name, (us, launches) = max(kt.items(), key=lambda kv: kv[1][0] * kv[1][1])
+        per_launch_units = n
+        macs = oc.get(name, {}).get("macs")
+        peak = shard.mad_peak()
+        roof = None
+        if macs is not None:
+            achieved = macs * per_launch_units / (us * 1e-6) / 1e12
+            roof = {"bound": "valu-int", "achieved": achieved, "peak": peak["tmac_s"], "unit": "TMAC/s",
+                    "frac": achieved / peak["tmac_s"], "traffic": None, "kernel": name,
+                    "kernel_avg_us": us, "units_per_launch": per_launch_units, "macs_per_unit": macs,
+                    "peak_source": peak["source"]}
+        share = {k: round(v[0] * v[1] / (dt * 1e6 / 1.0), 4) for k, v in kt.items()}
+        cpu = None
+        if not args.no_cpu_baseline:
+            m = tbls.beacon_messages(rounds[:4096] - 1, rounds[:4096], prev_sigs[:4096])
+            cpu = cpu_baseline(pk, m, np.ascontiguousarray(sigs[:4096]), threads=args.cpu_threads)
+        out = {"metric": METRIC, "value": total / dt, "unit": "rounds/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "u32 (381-bit Fp, 12x32-bit limbs)", "data": data,
+               "config": {"workload": "batch bls.Verify / beacon.VerifyBeacon of %d linked chain rounds per GPU, one "
+                                      "shared group key (BASELINE configs[1]; configs[3] at N>1)" % n,
+                          "rounds_per_gpu": n, "global_rounds": world * n, "parallelism": "rounds sharded dp%d" % world},
+               "roofline": roof, "cpu_baseline": cpu,
+               "kernel_time_share": share,
+               "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()}}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

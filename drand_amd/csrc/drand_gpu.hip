@@ -54,8 +54,9 @@ int fail(int code, const std::string& msg) {
 
 // workspace slots
 enum Slot {
-  S_MSGS, S_DST, S_Q, S_S, S_STATUS, S_R, S_T, S_SUM_A, S_SUM_B, S_PK, S_PKST, S_FLAG, S_IN0, S_IN1, S_IN2, S_IN3, S_IN4,
-  S_OUT0, S_OUT1, S_COUNT
+  S_MSGS, S_DST, S_Q, S_S, S_U, S_STATUS, S_ISO, S_CELL, S_W, S_A, S_TMP, S_KP, S_F, S_H, S_FLAG, S_KEYS, S_KEYST,
+  S_COMMITS, S_COMMITST, S_SLOTIDX, S_ITEMSLOT, S_SEL, S_SELIDX, S_RST, S_SST, S_TERMS, S_IN0, S_IN1, S_IN2, S_IN3,
+  S_IN4, S_OUT0, S_COUNT
 };
 
 int ws(Slot s, size_t bytes, void** out) {
@@ -149,79 +150,6 @@ uint64_t fresh_seed(uint64_t seed) {
     if (r_ != 0) return r_; \
   } while (0)
 
-// Sum n Jacobian points in `buf` (overwritten) down to one point at buf[0], using `tmp` as scratch.
-int reduce_points(G2JStore* buf, G2JStore* tmp, uint32_t n, hipStream_t st) {
-  const uint32_t chunk = 32;
-  G2JStore* src = buf;
-  G2JStore* dst = tmp;
-  while (n > 1) {
-    uint32_t m = (n + chunk - 1) / chunk;
-    RET(launch("k_sum_points", k_sum_points, m, 128, st, n, chunk, (const G2JStore*)src, dst));
-    n = m;
-    G2JStore* t = src;
-    src = dst;
-    dst = t;
-  }
-  if (src != buf) HIPCHK(hipMemcpyAsync(buf, src, sizeof(G2JStore), hipMemcpyDeviceToDevice, st));
-  return 0;
-}
-
-// Core of dg_verify / dg_verify_beacons on device buffers: d_msgs (n x msg_len), d_sigs96 -> d_status.
-int verify_core(const uint8_t* pk48_host, size_t n, const uint8_t* d_msgs, uint32_t msg_len, const uint8_t* d_sigs96,
-                uint8_t* d_status, uint64_t seed, hipStream_t st) {
-  void *p_dst, *p_q, *p_s, *p_r, *p_t, *p_pk, *p_pkst, *p_flag;
-  RET(ws(S_DST, 64, &p_dst));
-  RET(ws(S_Q, sizeof(G2JStore) * n, &p_q));
-  RET(ws(S_S, sizeof(G2AStore) * n, &p_s));
-  RET(ws(S_R, sizeof(G2JStore) * n, &p_r));
-  RET(ws(S_T, sizeof(G2JStore) * n, &p_t));
-  RET(ws(S_PK, sizeof(G1AStore) + 48, &p_pk));
-  RET(ws(S_PKST, 16, &p_pkst));
-  RET(ws(S_FLAG, 16, &p_flag));
-  uint8_t* dst = (uint8_t*)p_dst;
-  HIPCHK(hipMemcpyAsync(dst, kDstNul, kDstNulLen, hipMemcpyHostToDevice, st));
-  uint8_t* pk_raw = (uint8_t*)p_pk + sizeof(G1AStore);
-  HIPCHK(hipMemcpyAsync(pk_raw, pk48_host, 48, hipMemcpyHostToDevice, st));
-  G1AStore* pk = (G1AStore*)p_pk;
-  RET(launch("k_decode_g1", k_decode_g1, 1, 64, st, 1u, (const uint8_t*)pk_raw, pk, (uint8_t*)p_pkst));
-  uint8_t pk_status = 0;
-  HIPCHK(hipMemcpyAsync(&pk_status, p_pkst, 1, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  if (pk_status != DG_ST_OK) {
-    HIPCHK(hipMemsetAsync(d_status, DG_ST_PK_DECODE, n, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return 0;
-  }
-  uint32_t nn = (uint32_t)n;
-  G2JStore* Q = (G2JStore*)p_q;
-  G2AStore* S = (G2AStore*)p_s;
-  RET(launch("k_h2c_uncleared", k_h2c_uncleared, nn, 128, st, nn, d_msgs, msg_len, (const uint8_t*)dst, kDstNulLen, Q));
-  RET(launch("k_decode_sigs", k_decode_sigs, nn, 128, st, nn, d_sigs96, 96u, 0u, S, d_status));
-  G2JStore* R = (G2JStore*)p_r;
-  G2JStore* T = (G2JStore*)p_t;
-  RET(launch("k_rlc_scale", k_rlc_scale, nn, 128, st, nn, seed, (const G2JStore*)Q, (const G2AStore*)S,
-             (const uint8_t*)d_status, R, T));
-  // reduce R and T in place (use the other's tail as scratch is unsafe: reduce separately with Q as tmp)
-  RET(reduce_points(R, Q, nn, st));
-  // Q has been clobbered by the reduction scratch; T reduction reuses it too
-  RET(reduce_points(T, Q, nn, st));
-  uint32_t* flag = (uint32_t*)p_flag;
-  RET(launch("k_rlc_final", k_rlc_final, 1, 64, st, (const G1AStore*)pk, (const G2JStore*)R, (const G2JStore*)T, flag));
-  uint32_t ok = 0;
-  HIPCHK(hipMemcpyAsync(&ok, flag, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  if (!ok) {
-    // isolate: per-item pairing check (recompute the hashes clobbered by the reduction)
-    RET(launch("k_h2c_uncleared", k_h2c_uncleared, nn, 128, st, nn, d_msgs, msg_len, (const uint8_t*)dst, kDstNulLen,
-               Q));
-    RET(launch("k_verify_items", k_verify_items, nn, 64, st, nn, (const G1AStore*)pk, (const uint32_t*)nullptr,
-               (const G2JStore*)Q, (const uint32_t*)nullptr, (const G2AStore*)S, d_status));
-    HIPCHK(hipStreamSynchronize(st));
-  }
-  if (g_ctx.timing) collect_timings();
-  return 0;
-}
-
 template <typename T>
 int upload(Slot s, const T* host, size_t count, T** dev, hipStream_t st) {
   void* p;
@@ -230,6 +158,171 @@ int upload(Slot s, const T* host, size_t count, T** dev, hipStream_t st) {
   *dev = (T*)p;
   return 0;
 }
+
+template <typename T>
+int wsT(Slot s, size_t count, T** out) {
+  void* p;
+  RET(ws(s, sizeof(T) * count, &p));
+  *out = (T*)p;
+  return 0;
+}
+
+// Collapse each of `rows` rows of `cols` Jacobian points (row-major in buf) to its sum, left in buf[row].
+int reduce_rows(G2JStore* buf, G2JStore* tmp, uint32_t rows, uint32_t cols, hipStream_t st) {
+  G2JStore* src = buf;
+  G2JStore* dst = tmp;
+  while (cols > 1) {
+    uint32_t chunk = cols < 32 ? cols : 32;
+    uint32_t ocols = (cols + chunk - 1) / chunk;
+    RET(launch("k_sum_rows", k_sum_rows, rows * ocols, 128, st, rows, cols, chunk, (const G2JStore*)src, dst));
+    cols = ocols;
+    std::swap(src, dst);
+  }
+  if (src != buf) HIPCHK(hipMemcpyAsync(buf, src, sizeof(G2JStore) * rows, hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+
+// One batch of the verification engine (kernels.h): R rounds with uncleared hashes Q, k items per round,
+// nslots keys.  Fills S / status / isolate for the N = R*k items; status ends as the exact per-item
+// bls.Verify verdict.
+struct Batch {
+  uint32_t R, k, nslots;
+  const G2JStore* Q;
+  const G1AStore* keys;
+  const uint8_t* key_status;
+  const uint32_t* item_slot;  // N entries, or null when nslots == 1
+  const uint8_t* sigs;        // N records of `stride` bytes, sigma at `offset`
+  uint32_t stride, offset;
+  G2AStore* S;
+  uint8_t* status;
+};
+
+int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
+  const uint32_t N = b.R * b.k;
+  uint8_t* iso;
+  uint32_t *cell, *flag;
+  G2JStore *U, *W, *A, *tmp, *Kp;
+  Fp12* f;
+  RET(wsT(S_ISO, N, &iso));
+  RET(wsT(S_CELL, (size_t)b.R * b.nslots, &cell));
+  RET(wsT(S_FLAG, 4, &flag));
+  RET(wsT(S_U, N, &U));
+  RET(wsT(S_W, b.R, &W));
+  RET(wsT(S_A, b.R, &A));
+  uint32_t nchunks = 16384 / b.nslots;
+  if (nchunks < 1) nchunks = 1;
+  if (nchunks > b.R) nchunks = b.R;
+  uint32_t chunk = (b.R + nchunks - 1) / nchunks;
+  nchunks = (b.R + chunk - 1) / chunk;
+  RET(wsT(S_KP, (size_t)b.nslots * nchunks, &Kp));
+  size_t ntmp = (size_t)b.nslots * nchunks > b.R ? (size_t)b.nslots * nchunks : b.R;
+  RET(wsT(S_TMP, ntmp, &tmp));
+  RET(wsT(S_F, b.nslots + 1, &f));
+  HIPCHK(hipMemsetAsync(cell, 0, sizeof(uint32_t) * (size_t)b.R * b.nslots, st));
+  RET(launch("k_decode_items", k_decode_items, N, 128, st, N, b.k, b.nslots, b.sigs, b.stride, b.offset, b.item_slot,
+             b.key_status, b.S, b.status, cell, iso));
+  RET(launch("k_scale_items", k_scale_items, N, 128, st, N, b.nslots, seed, b.item_slot, (const G2AStore*)b.S,
+             (const uint8_t*)b.status, (const uint8_t*)iso, U));
+  RET(launch("k_round_combine", k_round_combine, b.R, 128, st, b.R, b.k, seed, (const G2JStore*)U,
+             (const uint8_t*)b.status, (const uint8_t*)iso, b.Q, W, A));
+  RET(reduce_rows(W, tmp, 1, b.R, st));  // T = W[0]
+  RET(launch("k_key_accum", k_key_accum, b.nslots * nchunks, 128, st, b.R, b.nslots, chunk, nchunks,
+             (const uint32_t*)cell, (const G2JStore*)A, Kp));
+  RET(reduce_rows(Kp, tmp, b.nslots, nchunks, st));  // K_s = Kp[s]
+  RET(launch("k_pair_miller", k_pair_miller, b.nslots + 1, 64, st, b.nslots, seed, b.keys, (const G2JStore*)Kp,
+             (const G2JStore*)W, f));
+  RET(launch("k_final_check", k_final_check, 1, 64, st, b.nslots + 1, (const Fp12*)f, flag));
+  // isolated items present?
+  HIPCHK(hipMemsetAsync(flag + 1, 0, 4, st));
+  RET(launch("k_any", k_any, N, 256, st, N, (const uint8_t*)iso, flag + 1));
+  uint32_t h_flag[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(h_flag, flag, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  bool batch_ok = h_flag[0] != 0, any_iso = h_flag[1] != 0;
+  if (!batch_ok || any_iso) {
+    G2AStore* H;
+    RET(wsT(S_H, b.R, &H));
+    RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, b.Q, H));
+    RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, batch_ok ? 0u : 1u, b.keys, b.item_slot,
+               (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status));
+  }
+  return 0;
+}
+
+int decode_key(const uint8_t* pk48_host, hipStream_t st, G1AStore** keys, uint8_t** key_status) {
+  uint8_t* d_pk;
+  RET(upload(S_IN3, pk48_host, 48, &d_pk, st));
+  RET(wsT(S_KEYS, 1, keys));
+  RET(wsT(S_KEYST, 1, key_status));
+  return launch("k_decode_g1", k_decode_g1, 1, 64, st, 1u, (const uint8_t*)d_pk, *keys, *key_status);
+}
+
+int hash_rounds(uint32_t R, const uint8_t* d_msgs, uint32_t msg_len, hipStream_t st, G2JStore** Q) {
+  uint8_t* d_dst;
+  RET(upload(S_DST, kDstNul, kDstNulLen, &d_dst, st));
+  RET(wsT(S_Q, R, Q));
+  return launch("k_h2c_uncleared", k_h2c_uncleared, R, 128, st, R, d_msgs, msg_len, (const uint8_t*)d_dst, kDstNulLen,
+                *Q);
+}
+
+// bls.Verify batch against one key, everything device-resident
+int verify_single_key(const uint8_t* pk48_host, uint32_t n, const uint8_t* d_msgs, uint32_t msg_len,
+                      const uint8_t* d_sigs, uint8_t* d_status, uint64_t seed, hipStream_t st) {
+  G1AStore* keys;
+  uint8_t* kst;
+  G2JStore* Q;
+  G2AStore* S;
+  RET(decode_key(pk48_host, st, &keys, &kst));
+  RET(hash_rounds(n, d_msgs, msg_len, st, &Q));
+  RET(wsT(S_S, n, &S));
+  Batch b{n, 1, 1, Q, keys, kst, nullptr, d_sigs, 96, 0, S, d_status};
+  RET(batch_verify(b, seed, st));
+  return 0;
+}
+
+// VerifyPartial over R rounds x k partials: keys X_i = PubPoly.Eval(i) for every distinct index
+int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const uint8_t* msgs, uint32_t msg_len,
+                        uint32_t k, const uint8_t* partials98, uint64_t seed, hipStream_t st, uint8_t** d_status,
+                        uint8_t** d_partials, G2AStore** d_S) {
+  const size_t N = (size_t)R * k;
+  // distinct indices (host bookkeeping over the 2-byte index fields only)
+  std::vector<int32_t> slot_of(65536, -1);
+  std::vector<uint32_t> slot_idx, item_slot(N);
+  for (size_t i = 0; i < N; ++i) {
+    uint32_t idx = (uint32_t)partials98[98 * i] << 8 | partials98[98 * i + 1];
+    if (slot_of[idx] < 0) {
+      slot_of[idx] = (int32_t)slot_idx.size();
+      slot_idx.push_back(idx);
+    }
+    item_slot[i] = (uint32_t)slot_of[idx];
+  }
+  uint32_t nslots = (uint32_t)slot_idx.size();
+  uint8_t *d_c, *d_cst, *d_m, *d_p, *kst;
+  G1AStore *cA, *keys;
+  uint32_t *d_slotidx, *d_itemslot;
+  RET(upload(S_IN0, commits48, (size_t)t * 48, &d_c, st));
+  RET(wsT(S_COMMITS, t, &cA));
+  RET(wsT(S_COMMITST, t, &d_cst));
+  RET(launch("k_decode_g1", k_decode_g1, t, 64, st, t, (const uint8_t*)d_c, cA, d_cst));
+  RET(upload(S_SLOTIDX, slot_idx.data(), nslots, &d_slotidx, st));
+  RET(upload(S_ITEMSLOT, item_slot.data(), N, &d_itemslot, st));
+  RET(wsT(S_KEYS, nslots, &keys));
+  RET(wsT(S_KEYST, nslots, &kst));
+  RET(launch("k_pubpoly_eval", k_pubpoly_eval, nslots, 64, st, nslots, t, (const G1AStore*)cA, (const uint8_t*)d_cst,
+             (const uint32_t*)d_slotidx, keys, kst, (uint8_t*)nullptr));
+  RET(upload(S_MSGS, msgs, (size_t)R * msg_len, &d_m, st));
+  RET(upload(S_IN1, partials98, N * 98, &d_p, st));
+  G2JStore* Q;
+  RET(hash_rounds(R, d_m, msg_len, st, &Q));
+  RET(wsT(S_S, N, d_S));
+  RET(wsT(S_STATUS, N, d_status));
+  Batch b{R, k, nslots, Q, keys, kst, d_itemslot, d_p, 98, 2, *d_S, *d_status};
+  RET(batch_verify(b, seed, st));
+  *d_partials = d_p;
+  return 0;
+}
+
+int check_args_n(size_t n) { return n > 0x7fffffffu ? fail(DG_E_ARG, "batch too large (>= 2^31 items)") : 0; }
 
 }  // namespace
 
@@ -307,30 +400,62 @@ int dg_hash_to_g2(size_t n, const uint8_t* msgs, size_t msg_len, const uint8_t* 
   return 0;
 }
 
+int dg_sign(size_t n, const uint8_t* scalars32, const uint16_t* index, const uint8_t* msgs, size_t msg_len,
+            uint8_t* out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  if (n == 0) return 0;
+  if (!scalars32 || !msgs || !out) return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(n));
+  hipStream_t st = g_ctx.stream;
+  uint8_t *d_sc, *d_m, *d_dst, *d_out;
+  uint16_t* d_idx = nullptr;
+  RET(upload(S_IN0, scalars32, n * 32, &d_sc, st));
+  RET(upload(S_MSGS, msgs, n * msg_len, &d_m, st));
+  RET(upload(S_DST, kDstNul, kDstNulLen, &d_dst, st));
+  if (index) RET(upload(S_IN1, index, n, &d_idx, st));
+  size_t rec = index ? 98 : 96;
+  RET(wsT(S_OUT0, n * rec, &d_out));
+  RET(launch("k_sign", k_sign, (uint32_t)n, 128, st, (uint32_t)n, (const uint8_t*)d_sc, (const uint16_t*)d_idx,
+             (const uint8_t*)d_m, (uint32_t)msg_len, (const uint8_t*)d_dst, kDstNulLen, d_out));
+  HIPCHK(hipMemcpyAsync(out, d_out, n * rec, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (g_ctx.timing) collect_timings();
+  return 0;
+}
+
 int dg_verify(const uint8_t pk48[48], size_t n, const uint8_t* msgs, size_t msg_len, const uint8_t* sigs96,
               uint8_t* status, uint64_t seed) {
   std::lock_guard<std::mutex> lk(g_mu);
   RET(require_ready());
   if (n == 0) return 0;
-  if (!pk48 || !msgs || !sigs96 || !status || n > 0xffffffffu) return fail(DG_E_ARG, "bad arguments");
+  if (!pk48 || !msgs || !sigs96 || !status) return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(n));
   hipStream_t st = g_ctx.stream;
-  uint8_t *d_msgs, *d_sigs;
+  uint8_t *d_msgs, *d_sigs, *d_st;
   RET(upload(S_MSGS, msgs, n * msg_len, &d_msgs, st));
   RET(upload(S_IN0, sigs96, n * 96, &d_sigs, st));
-  void* p_st;
-  RET(ws(S_STATUS, n, &p_st));
-  RET(verify_core(pk48, n, d_msgs, (uint32_t)msg_len, d_sigs, (uint8_t*)p_st, fresh_seed(seed), st));
-  HIPCHK(hipMemcpyAsync(status, p_st, n, hipMemcpyDeviceToHost, st));
+  RET(wsT(S_STATUS, n, &d_st));
+  RET(verify_single_key(pk48, (uint32_t)n, d_msgs, (uint32_t)msg_len, d_sigs, d_st, fresh_seed(seed), st));
+  HIPCHK(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (g_ctx.timing) collect_timings();
   return 0;
 }
 
 static int beacons_to_msgs(size_t n, const uint64_t* d_pr, const uint64_t* d_r, const uint8_t* d_ps,
                            const uint32_t* d_off, uint8_t** d_msgs, hipStream_t st) {
-  void* p;
-  RET(ws(S_MSGS, 32 * n, &p));
-  RET(launch("k_beacon_msgs", k_beacon_msgs, (uint32_t)n, 256, st, (uint32_t)n, d_pr, d_r, d_ps, d_off, (uint8_t*)p));
-  *d_msgs = (uint8_t*)p;
+  RET(wsT(S_MSGS, 32 * n, d_msgs));
+  return launch("k_beacon_msgs", k_beacon_msgs, (uint32_t)n, 256, st, (uint32_t)n, d_pr, d_r, d_ps, d_off, *d_msgs);
+}
+
+static int upload_beacons(size_t n, const uint64_t* prev_round, const uint64_t* round, const uint8_t* prev_sigs,
+                          const uint32_t* prev_sig_off, hipStream_t st, uint64_t** d_pr, uint64_t** d_r,
+                          uint8_t** d_ps, uint32_t** d_off) {
+  RET(upload(S_IN1, prev_round, n, d_pr, st));
+  RET(upload(S_IN2, round, n, d_r, st));
+  RET(upload(S_IN3, prev_sig_off, n + 1, d_off, st));
+  RET(upload(S_IN4, prev_sigs, prev_sig_off[n], d_ps, st));
   return 0;
 }
 
@@ -340,23 +465,21 @@ int dg_verify_beacons(const uint8_t pk48[48], size_t n, const uint64_t* prev_rou
   std::lock_guard<std::mutex> lk(g_mu);
   RET(require_ready());
   if (n == 0) return 0;
-  if (!pk48 || !prev_round || !round || !prev_sigs || !prev_sig_off || !sigs96 || !status || n > 0xffffffffu)
+  if (!pk48 || !prev_round || !round || !prev_sigs || !prev_sig_off || !sigs96 || !status)
     return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(n));
   hipStream_t st = g_ctx.stream;
   uint64_t *d_pr, *d_r;
-  uint8_t *d_ps, *d_sigs, *d_msgs;
+  uint8_t *d_ps, *d_sigs, *d_msgs, *d_st;
   uint32_t* d_off;
   RET(upload(S_IN0, sigs96, n * 96, &d_sigs, st));
-  RET(upload(S_IN1, prev_round, n, &d_pr, st));
-  RET(upload(S_IN2, round, n, &d_r, st));
-  RET(upload(S_IN3, prev_sig_off, n + 1, &d_off, st));
-  RET(upload(S_IN4, prev_sigs, prev_sig_off[n], &d_ps, st));
+  RET(upload_beacons(n, prev_round, round, prev_sigs, prev_sig_off, st, &d_pr, &d_r, &d_ps, &d_off));
   RET(beacons_to_msgs(n, d_pr, d_r, d_ps, d_off, &d_msgs, st));
-  void* p_st;
-  RET(ws(S_STATUS, n, &p_st));
-  RET(verify_core(pk48, n, d_msgs, 32, d_sigs, (uint8_t*)p_st, fresh_seed(seed), st));
-  HIPCHK(hipMemcpyAsync(status, p_st, n, hipMemcpyDeviceToHost, st));
+  RET(wsT(S_STATUS, n, &d_st));
+  RET(verify_single_key(pk48, (uint32_t)n, d_msgs, 32, d_sigs, d_st, fresh_seed(seed), st));
+  HIPCHK(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (g_ctx.timing) collect_timings();
   return 0;
 }
 
@@ -366,11 +489,15 @@ int dg_verify_beacons_dev(const uint8_t* pk48_host, size_t n, const uint64_t* d_
   std::lock_guard<std::mutex> lk(g_mu);
   RET(require_ready());
   if (n == 0) return 0;
+  if (!pk48_host || !d_prev_round || !d_round || !d_prev_sigs || !d_prev_sig_off || !d_sigs96 || !d_status)
+    return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(n));
   hipStream_t st = stream ? (hipStream_t)stream : g_ctx.stream;
   uint8_t* d_msgs;
   RET(beacons_to_msgs(n, d_prev_round, d_round, d_prev_sigs, d_prev_sig_off, &d_msgs, st));
-  RET(verify_core(pk48_host, n, d_msgs, 32, d_sigs96, d_status, fresh_seed(seed), st));
+  RET(verify_single_key(pk48_host, (uint32_t)n, d_msgs, 32, d_sigs96, d_status, fresh_seed(seed), st));
   HIPCHK(hipStreamSynchronize(st));
+  if (g_ctx.timing) collect_timings();
   return 0;
 }
 
@@ -380,22 +507,21 @@ int dg_check_links(uint64_t cur_round, const uint8_t* cur_sig, size_t cur_sig_le
   std::lock_guard<std::mutex> lk(g_mu);
   RET(require_ready());
   if (n == 0) return 0;
+  if (!cur_sig || !prev_round || !round || !prev_sigs || !prev_sig_off || !sigs96 || !link_status)
+    return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(n));
   hipStream_t st = g_ctx.stream;
   uint64_t *d_pr, *d_r;
-  uint8_t *d_ps, *d_sigs, *d_cur;
+  uint8_t *d_ps, *d_sigs, *d_cur, *d_out;
   uint32_t* d_off;
   RET(upload(S_IN0, sigs96, n * 96, &d_sigs, st));
-  RET(upload(S_IN1, prev_round, n, &d_pr, st));
-  RET(upload(S_IN2, round, n, &d_r, st));
-  RET(upload(S_IN3, prev_sig_off, n + 1, &d_off, st));
-  RET(upload(S_IN4, prev_sigs, prev_sig_off[n], &d_ps, st));
+  RET(upload_beacons(n, prev_round, round, prev_sigs, prev_sig_off, st, &d_pr, &d_r, &d_ps, &d_off));
   RET(upload(S_DST, cur_sig, cur_sig_len, &d_cur, st));
-  void* p_out;
-  RET(ws(S_OUT0, n, &p_out));
+  RET(wsT(S_OUT0, n, &d_out));
   RET(launch("k_links", k_links, (uint32_t)n, 256, st, (uint32_t)n, cur_round, (const uint8_t*)d_cur,
              (uint32_t)cur_sig_len, (const uint64_t*)d_pr, (const uint64_t*)d_r, (const uint8_t*)d_ps,
-             (const uint32_t*)d_off, (const uint8_t*)d_sigs, (uint8_t*)p_out));
-  HIPCHK(hipMemcpyAsync(link_status, p_out, n, hipMemcpyDeviceToHost, st));
+             (const uint32_t*)d_off, (const uint8_t*)d_sigs, d_out));
+  HIPCHK(hipMemcpyAsync(link_status, d_out, n, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   return 0;
 }
@@ -405,14 +531,13 @@ int dg_beacon_messages(size_t n, const uint64_t* prev_round, const uint64_t* rou
   std::lock_guard<std::mutex> lk(g_mu);
   RET(require_ready());
   if (n == 0) return 0;
+  if (!prev_round || !round || !prev_sigs || !prev_sig_off || !out32) return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(n));
   hipStream_t st = g_ctx.stream;
   uint64_t *d_pr, *d_r;
   uint8_t *d_ps, *d_msgs;
   uint32_t* d_off;
-  RET(upload(S_IN1, prev_round, n, &d_pr, st));
-  RET(upload(S_IN2, round, n, &d_r, st));
-  RET(upload(S_IN3, prev_sig_off, n + 1, &d_off, st));
-  RET(upload(S_IN4, prev_sigs, prev_sig_off[n], &d_ps, st));
+  RET(upload_beacons(n, prev_round, round, prev_sigs, prev_sig_off, st, &d_pr, &d_r, &d_ps, &d_off));
   RET(beacons_to_msgs(n, d_pr, d_r, d_ps, d_off, &d_msgs, st));
   HIPCHK(hipMemcpyAsync(out32, d_msgs, 32 * n, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -423,14 +548,101 @@ int dg_randomness(size_t n, const uint8_t* sigs96, uint8_t* out32) {
   std::lock_guard<std::mutex> lk(g_mu);
   RET(require_ready());
   if (n == 0) return 0;
+  if (!sigs96 || !out32) return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(n));
   hipStream_t st = g_ctx.stream;
-  uint8_t* d_sigs;
+  uint8_t *d_sigs, *d_out;
   RET(upload(S_IN0, sigs96, n * 96, &d_sigs, st));
-  void* p_out;
-  RET(ws(S_OUT0, 32 * n, &p_out));
-  RET(launch("k_randomness", k_randomness, (uint32_t)n, 256, st, (uint32_t)n, (const uint8_t*)d_sigs, (uint8_t*)p_out));
-  HIPCHK(hipMemcpyAsync(out32, p_out, 32 * n, hipMemcpyDeviceToHost, st));
+  RET(wsT(S_OUT0, 32 * n, &d_out));
+  RET(launch("k_randomness", k_randomness, (uint32_t)n, 256, st, (uint32_t)n, (const uint8_t*)d_sigs, d_out));
+  HIPCHK(hipMemcpyAsync(out32, d_out, 32 * n, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+
+int dg_pubpoly_eval(const uint8_t* commits48, uint32_t t, size_t n, const uint32_t* index, uint8_t* out48) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  if (n == 0) return 0;
+  if (!commits48 || t == 0 || !index || !out48) return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(n));
+  hipStream_t st = g_ctx.stream;
+  uint8_t *d_c, *d_cst, *d_out, *d_kst;
+  uint32_t* d_idx;
+  G1AStore *cA, *keys;
+  RET(upload(S_IN0, commits48, (size_t)t * 48, &d_c, st));
+  RET(wsT(S_COMMITS, t, &cA));
+  RET(wsT(S_COMMITST, t, &d_cst));
+  RET(launch("k_decode_g1", k_decode_g1, t, 64, st, t, (const uint8_t*)d_c, cA, d_cst));
+  RET(upload(S_SLOTIDX, index, n, &d_idx, st));
+  RET(wsT(S_KEYS, n, &keys));
+  RET(wsT(S_KEYST, n, &d_kst));
+  RET(wsT(S_OUT0, 48 * n, &d_out));
+  RET(launch("k_pubpoly_eval", k_pubpoly_eval, (uint32_t)n, 64, st, (uint32_t)n, t, (const G1AStore*)cA,
+             (const uint8_t*)d_cst, (const uint32_t*)d_idx, keys, d_kst, d_out));
+  std::vector<uint8_t> kst(n);
+  HIPCHK(hipMemcpyAsync(out48, d_out, 48 * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(kst.data(), d_kst, n, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (g_ctx.timing) collect_timings();
+  if (kst[0] != DG_ST_OK) return fail(DG_E_ARG, "a commitment does not decode");
+  return 0;
+}
+
+int dg_verify_partials(const uint8_t* commits48, uint32_t t, size_t rounds, const uint8_t* msgs, size_t msg_len,
+                       uint32_t k, const uint8_t* partials98, uint8_t* status, uint64_t seed) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  if (rounds == 0 || k == 0) return 0;
+  if (!commits48 || t == 0 || !msgs || !partials98 || !status) return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(rounds * (size_t)k));
+  hipStream_t st = g_ctx.stream;
+  uint8_t *d_st, *d_p;
+  G2AStore* d_S;
+  RET(verify_partials_dev(commits48, t, (uint32_t)rounds, msgs, (uint32_t)msg_len, k, partials98, fresh_seed(seed), st,
+                          &d_st, &d_p, &d_S));
+  HIPCHK(hipMemcpyAsync(status, d_st, rounds * k, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (g_ctx.timing) collect_timings();
+  return 0;
+}
+
+int dg_recover(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t rounds, const uint8_t* msgs,
+               size_t msg_len, uint32_t k, const uint8_t* partials98, uint8_t* out_sig96, uint8_t* round_status,
+               uint8_t* share_status, uint64_t seed) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  (void)nshares;  // kyber passes n to RecoverCommit only as a capacity hint
+  if (rounds == 0) return 0;
+  if (!commits48 || t == 0 || k == 0 || !msgs || !partials98 || !out_sig96 || !round_status || !share_status)
+    return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(rounds * (size_t)(k > t ? k : t)));
+  hipStream_t st = g_ctx.stream;
+  const uint32_t R = (uint32_t)rounds;
+  uint8_t *d_st, *d_p, *d_rst, *d_sst, *d_out;
+  G2AStore* d_S;
+  RET(verify_partials_dev(commits48, t, R, msgs, (uint32_t)msg_len, k, partials98, fresh_seed(seed), st, &d_st, &d_p,
+                          &d_S));
+  uint32_t *d_sel, *d_selidx;
+  G2JStore *terms, *tmp;
+  RET(wsT(S_SEL, (size_t)R * t, &d_sel));
+  RET(wsT(S_SELIDX, (size_t)R * t, &d_selidx));
+  RET(wsT(S_RST, R, &d_rst));
+  RET(wsT(S_SST, (size_t)R * k, &d_sst));
+  RET(launch("k_recover_select", k_recover_select, R, 128, st, R, k, t, (const uint8_t*)d_p, (const uint8_t*)d_st,
+             d_sel, d_selidx, d_rst, d_sst));
+  RET(wsT(S_TERMS, (size_t)R * t, &terms));
+  RET(wsT(S_TMP, (size_t)R * t, &tmp));
+  RET(launch("k_recover_terms", k_recover_terms, R * t, 64, st, R, k, t, (const uint32_t*)d_sel,
+             (const uint32_t*)d_selidx, (const uint8_t*)d_rst, (const G2AStore*)d_S, terms));
+  RET(reduce_rows(terms, tmp, R, t, st));
+  RET(wsT(S_OUT0, (size_t)R * 96, &d_out));
+  RET(launch("k_compress_g2", k_compress_g2, R, 128, st, R, (const G2JStore*)terms, (const uint8_t*)d_rst, d_out));
+  HIPCHK(hipMemcpyAsync(out_sig96, d_out, (size_t)R * 96, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(round_status, d_rst, R, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(share_status, d_sst, (size_t)R * k, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (g_ctx.timing) collect_timings();
   return 0;
 }
 

@@ -40,10 +40,12 @@ struct Fp12 {
 
 #if defined(DG_OPCOUNT)
 // host-only instrumented build (tools/opcount): counts Montgomery multiplications (squarings included)
-extern thread_local uint64_t g_fp_mul_count;
+extern thread_local uint64_t g_fp_mul_count, g_fp_sqr_count;
 #define DG_COUNT_MUL() (++g_fp_mul_count)
+#define DG_COUNT_SQR() (++g_fp_sqr_count)
 #else
 #define DG_COUNT_MUL() ((void)0)
+#define DG_COUNT_SQR() ((void)0)
 #endif
 
 DGI uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
@@ -128,15 +130,8 @@ DGI Fp fp_neg(const Fp& a) {
   return fp_sel(fp_is_zero(a), d, a);
 }
 
-// Montgomery multiplication.  Device: product-scanning inline-asm block (tools/gen_fp_asm.py).
-// Host (tests/native only): CIOS without the extra carry word (valid since p[11] < 2^31 - 1).
-DGI Fp fp_mul(const Fp& a, const Fp& b) {
-  DG_COUNT_MUL();
-#if defined(DG_FP_ASM)
-  Fp r;
-  fp_mont_mul_asm(r.l, a.l, b.l, P_LIMBS, P_INV32);
-  return fp_reduce_once(r);
-#else
+// Host CIOS (tests/native and tools/opcount only): no extra carry word (valid since p[11] < 2^31 - 1).
+DGI Fp fp_mul_cios(const Fp& a, const Fp& b) {
   uint32_t t[12];
 #pragma unroll
   for (int j = 0; j < 12; ++j) t[j] = 0;
@@ -162,16 +157,29 @@ DGI Fp fp_mul(const Fp& a, const Fp& b) {
 #pragma unroll
   for (int j = 0; j < 12; ++j) r.l[j] = t[j];
   return fp_reduce_once(r);
+}
+
+// Montgomery multiplication / squaring.  Device: one product-scanning inline-asm block each
+// (tools/gen_fp_asm.py: 288 / 222 v_mad_u64_u32), kept out of line so the instruction stream of the
+// callers stays inside the instruction cache.
+DGN Fp fp_mul(const Fp& a, const Fp& b) {
+  DG_COUNT_MUL();
+#if defined(DG_FP_ASM)
+  Fp r;
+  fp_mont_mul_asm(r.l, a.l, b.l, P_LIMBS, P_INV32);
+  return fp_reduce_once(r);
+#else
+  return fp_mul_cios(a, b);
 #endif
 }
-DGI Fp fp_sqr(const Fp& a) {
+DGN Fp fp_sqr(const Fp& a) {
+  DG_COUNT_SQR();
 #if defined(DG_FP_ASM)
-  DG_COUNT_MUL();
   Fp r;
   fp_mont_sqr_asm(r.l, a.l, P_LIMBS, P_INV32);
   return fp_reduce_once(r);
 #else
-  return fp_mul(a, a);
+  return fp_mul_cios(a, a);
 #endif
 }
 
@@ -211,9 +219,9 @@ DGI Fp fp_pow_sched(const Fp& x, int first, const int8_t (&steps)[NSTEPS][2]) {
   }
   return acc;
 }
-DGI Fp fp_inv(const Fp& a) { return fp_pow_sched(a, EXP_PM2_FIRST, EXP_PM2_STEPS); }
+DGN Fp fp_inv(const Fp& a) { return fp_pow_sched(a, EXP_PM2_FIRST, EXP_PM2_STEPS); }
 // returns x^((p-3)/4)
-DGI Fp fp_pow_pm3d4(const Fp& a) { return fp_pow_sched(a, EXP_PM3D4_FIRST, EXP_PM3D4_STEPS); }
+DGN Fp fp_pow_pm3d4(const Fp& a) { return fp_pow_sched(a, EXP_PM3D4_FIRST, EXP_PM3D4_STEPS); }
 // sqrt(a) if a is a square (r^2 == a checked by the caller or via return)
 DGI bool fp_sqrt(Fp& r, const Fp& a) {
   Fp t = fp_pow_pm3d4(a);
@@ -289,13 +297,13 @@ DGI Fp2 fp2_sub(const Fp2& a, const Fp2& b) { return Fp2{fp_sub(a.c0, b.c0), fp_
 DGI Fp2 fp2_dbl(const Fp2& a) { return Fp2{fp_dbl(a.c0), fp_dbl(a.c1)}; }
 DGI Fp2 fp2_neg(const Fp2& a) { return Fp2{fp_neg(a.c0), fp_neg(a.c1)}; }
 DGI Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
-DGI Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
+DGN Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
   Fp t0 = fp_mul(a.c0, b.c0);
   Fp t1 = fp_mul(a.c1, b.c1);
   Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
   return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
-DGI Fp2 fp2_sqr(const Fp2& a) {
+DGN Fp2 fp2_sqr(const Fp2& a) {
   Fp m = fp_mul(a.c0, a.c1);
   return Fp2{fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(m)};
 }
@@ -367,7 +375,7 @@ DGI Fp6 fp6_add(const Fp6& a, const Fp6& b) { return Fp6{fp2_add(a.c0, b.c0), fp
 DGI Fp6 fp6_sub(const Fp6& a, const Fp6& b) { return Fp6{fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
 DGI Fp6 fp6_neg(const Fp6& a) { return Fp6{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
 DGI Fp6 fp6_mul_v(const Fp6& a) { return Fp6{fp2_mul_xi(a.c2), a.c0, a.c1}; }
-DGI Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
+DGN Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
   Fp2 v0 = fp2_mul(a.c0, b.c0);
   Fp2 v1 = fp2_mul(a.c1, b.c1);
   Fp2 v2 = fp2_mul(a.c2, b.c2);
@@ -376,7 +384,7 @@ DGI Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
   Fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), v0), v2), v1);
   return Fp6{c0, c1, c2};
 }
-DGI Fp6 fp6_sqr(const Fp6& a) {
+DGN Fp6 fp6_sqr(const Fp6& a) {
   // CH-SQR2
   Fp2 s0 = fp2_sqr(a.c0);
   Fp2 ab = fp2_mul(a.c0, a.c1);
@@ -399,7 +407,7 @@ DGN Fp6 fp6_inv(const Fp6& a) {
   return Fp6{fp2_mul(c0, t), fp2_mul(c1, t), fp2_mul(c2, t)};
 }
 // (a0 + a1 v + a2 v^2) * (b0 + b1 v)
-DGI Fp6 fp6_mul_01(const Fp6& a, const Fp2& b0, const Fp2& b1) {
+DGN Fp6 fp6_mul_01(const Fp6& a, const Fp2& b0, const Fp2& b1) {
   Fp2 v0 = fp2_mul(a.c0, b0);
   Fp2 v1 = fp2_mul(a.c1, b1);
   Fp2 c0 = fp2_add(fp2_mul_xi(fp2_mul(a.c2, b1)), v0);

@@ -4,6 +4,7 @@
 #pragma once
 #include "h2c.h"
 #include "pairing.h"
+#include "fr.h"
 
 namespace dg {
 
@@ -138,65 +139,191 @@ DG_KERNEL void __launch_bounds__(64) k_decode_g1(uint32_t n, const uint8_t* in48
   status[i] = ok ? DG_ST_OK_ : DG_ST_PK_DECODE_;
 }
 
-// RLC scaling: R_i = rho_i Q_i, T_i = rho_i S_i (O for items whose sigma did not decode)
-DG_KERNEL void __launch_bounds__(128) k_rlc_scale(uint32_t n, uint64_t seed, const G2JStore* Q, const G2AStore* S,
-                                                  const uint8_t* status, G2JStore* R, G2JStore* T) {
+// ------------------------------------------------------------------ batch verification engine
+// Items are (round r, key slot s) pairs laid out round-major, k items per round (k = 1 for chain
+// verification, k = partials per round for VerifyPartial / Recover).  Soundness of the batch:
+// the random linear combination uses coefficient alpha_r * beta_s for item (r, s), so the batch
+// equation is  prod_s e(beta_s X_s, h_eff(sum_{r in R_s} alpha_r Q_r)) * e(-g1, sum_r alpha_r sum_s beta_s S_rs) = 1,
+// a bilinear form alpha^T E beta in the per-item errors E_rs (Schwartz-Zippel bound 2 / 2^64).  An item
+// whose (r, s) cell is already taken (a second partial with the same index in one round) is checked
+// on its own instead.  With a single key slot beta = 1.
+DGI uint64_t rlc_alpha(uint64_t seed, uint64_t r) { return rlc_coeff(seed, r); }
+DGI uint64_t rlc_beta(uint64_t seed, uint64_t s) { return rlc_coeff(~seed, s); }
+
+// [k]P for a small scalar (< 2^nbits), MSB first
+template <class F>
+DGN Jac<F> jac_mul_small(const Jac<F>& p, uint32_t k) {
+  Jac<F> acc = jac_infinity<F>();
+  int top = 31;
+  while (top >= 0 && !((k >> top) & 1)) --top;
+  for (int b = top; b >= 0; --b) {
+    acc = jac_dbl(acc);
+    if ((k >> b) & 1) acc = jac_add(acc, p);
+  }
+  return acc;
+}
+
+DGI uint32_t be16(const uint8_t* p) { return (uint32_t)p[0] << 8 | p[1]; }
+
+// A12: PubPoly.Eval(idx) = sum_j C_j x^j at x = idx + 1 (Horner), affine (+ compressed when out48)
+DG_KERNEL void __launch_bounds__(64) k_pubpoly_eval(uint32_t n, uint32_t t, const G1AStore* commits,
+                                                    const uint8_t* commit_status, const uint32_t* idx,
+                                                    G1AStore* out, uint8_t* out_status, uint8_t* out48) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  if (status[i] != DG_ST_OK_) {
-    store_g2j(R[i], jac_infinity<Fp2>());
-    store_g2j(T[i], jac_infinity<Fp2>());
+  bool ok = true;
+  for (uint32_t j = 0; j < t; ++j) ok = ok && commit_status[j] == DG_ST_OK_;
+  G1A a{fp_zero(), fp_zero(), true};
+  if (ok) {
+    uint32_t x = idx[i] + 1;
+    G1J acc = jac_from_aff(load_g1a(commits[t - 1]));
+    for (int j = (int)t - 2; j >= 0; --j) acc = jac_add(jac_mul_small(acc, x), jac_from_aff(load_g1a(commits[j])));
+    a = g1_to_aff(acc);
+  }
+  store_g1a(out[i], a);
+  if (out_status) out_status[i] = ok ? DG_ST_OK_ : DG_ST_PK_DECODE_;
+  if (out48) g1_compress_aff(out48 + 48ull * i, a);
+}
+
+// decode sigma of every item (96 B at sigs + stride*i + offset) with the G2 subgroup check; claim the
+// item's (round, slot) cell -- a taken cell sends the item to the individual check (`isolate`)
+DG_KERNEL void __launch_bounds__(128) k_decode_items(uint32_t n, uint32_t k, uint32_t nslots, const uint8_t* sigs,
+                                                     uint32_t stride, uint32_t offset, const uint32_t* item_slot,
+                                                     const uint8_t* key_status, G2AStore* S, uint8_t* status,
+                                                     uint32_t* cell, uint8_t* isolate) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t slot = item_slot ? item_slot[i] : 0u;
+  isolate[i] = 0;
+  if (key_status[slot] != DG_ST_OK_) {
+    store_g2a(S[i], G2A{fp2_zero(), fp2_zero(), true});
+    status[i] = DG_ST_PK_DECODE_;
     return;
   }
-  uint64_t rho = rlc_coeff(seed, i);
-  store_g2j(R[i], jac_mul_u64(load_g2j(Q[i]), rho));
-  store_g2j(T[i], jac_mul_u64(jac_from_aff(load_g2a(S[i])), rho));
+  G2A a;
+  bool ok = g2_decompress(a, sigs + (size_t)stride * i + offset, true);
+  if (!ok) a = G2A{fp2_zero(), fp2_zero(), true};
+  store_g2a(S[i], a);
+  status[i] = ok ? DG_ST_OK_ : DG_ST_SIG_DECODE_;
+  if (ok) {
+    uint32_t old = atomicExch(&cell[(size_t)(i / k) * nslots + slot], 1u);
+    isolate[i] = old ? 1 : 0;
+  }
 }
 
-// out[j] = sum of in[j*chunk .. min(n, (j+1)*chunk))
-DG_KERNEL void __launch_bounds__(128) k_sum_points(uint32_t n, uint32_t chunk, const G2JStore* in, G2JStore* out) {
-  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t a = j * chunk;
-  if (a >= n) return;
-  uint32_t b = a + chunk < n ? a + chunk : n;
-  G2J acc = load_g2j(in[a]);
-  for (uint32_t k = a + 1; k < b; ++k) acc = jac_add(acc, load_g2j(in[k]));
-  store_g2j(out[j], acc);
+// U_i = beta_slot S_i for batch items, O otherwise
+DG_KERNEL void __launch_bounds__(128) k_scale_items(uint32_t n, uint32_t nslots, uint64_t seed,
+                                                    const uint32_t* item_slot, const G2AStore* S,
+                                                    const uint8_t* status, const uint8_t* isolate, G2JStore* U) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G2J u = jac_infinity<Fp2>();
+  if (status[i] == DG_ST_OK_ && !isolate[i]) {
+    u = jac_from_aff(load_g2a(S[i]));
+    if (nslots > 1) u = jac_mul_u64(u, rlc_beta(seed, item_slot ? item_slot[i] : 0u));
+  }
+  store_g2j(U[i], u);
 }
 
-// batch verdict: e(pk, h_eff * sumR) * e(-g1, sumT) == 1   -> *ok = 1/0
-DG_KERNEL void __launch_bounds__(64) k_rlc_final(const G1AStore* pk, const G2JStore* sumR, const G2JStore* sumT,
-                                                 uint32_t* ok) {
+// per round r: W_r = alpha_r sum_j U_{r,j};  A_r = alpha_r Q_r (O when the round has no batch item)
+DG_KERNEL void __launch_bounds__(128) k_round_combine(uint32_t R, uint32_t k, uint64_t seed, const G2JStore* U,
+                                                      const uint8_t* status, const uint8_t* isolate,
+                                                      const G2JStore* Q, G2JStore* W, G2JStore* A) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  bool any = false;
+  G2J v = jac_infinity<Fp2>();
+  for (uint32_t j = 0; j < k; ++j) {
+    size_t i = (size_t)r * k + j;
+    if (status[i] == DG_ST_OK_ && !isolate[i]) {
+      v = any ? jac_add(v, load_g2j(U[i])) : load_g2j(U[i]);
+      any = true;
+    }
+  }
+  if (!any) {
+    store_g2j(W[r], jac_infinity<Fp2>());
+    store_g2j(A[r], jac_infinity<Fp2>());
+    return;
+  }
+  uint64_t a = rlc_alpha(seed, r);
+  store_g2j(W[r], jac_mul_u64(v, a));
+  store_g2j(A[r], jac_mul_u64(load_g2j(Q[r]), a));
+}
+
+// Kp[s * nchunks + c] = sum of A_r over rounds r in chunk c whose (r, s) cell holds a batch item
+DG_KERNEL void __launch_bounds__(128) k_key_accum(uint32_t R, uint32_t nslots, uint32_t chunk, uint32_t nchunks,
+                                                  const uint32_t* cell, const G2JStore* A, G2JStore* Kp) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nslots * nchunks) return;
+  uint32_t s = g / nchunks, c = g % nchunks;
+  uint32_t a = c * chunk, b = a + chunk < R ? a + chunk : R;
+  G2J acc = jac_infinity<Fp2>();
+  for (uint32_t r = a; r < b; ++r)
+    if (cell[(size_t)r * nslots + s]) acc = jac_add(acc, load_g2j(A[r]));
+  store_g2j(Kp[g], acc);
+}
+
+// 2-D segmented sum: out[row * ocols + j] = sum_{c in [j*chunk, (j+1)*chunk) and < cols} in[row * cols + c]
+DG_KERNEL void __launch_bounds__(128) k_sum_rows(uint32_t rows, uint32_t cols, uint32_t chunk, const G2JStore* in,
+                                                 G2JStore* out) {
+  uint32_t ocols = (cols + chunk - 1) / chunk;
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= rows * ocols) return;
+  uint32_t row = g / ocols, j = g % ocols;
+  uint32_t a = j * chunk, b = a + chunk < cols ? a + chunk : cols;
+  const G2JStore* p = in + (size_t)row * cols;
+  G2J acc = load_g2j(p[a]);
+  for (uint32_t c = a + 1; c < b; ++c) acc = jac_add(acc, load_g2j(p[c]));
+  store_g2j(out[g], acc);
+}
+
+// Miller loop of pair s: (beta_s X_s, h_eff(K_s)) for s < nslots, (-g1, T) for s == nslots; f = 1 if a
+// side is the identity
+DG_KERNEL void __launch_bounds__(64) k_pair_miller(uint32_t nslots, uint64_t seed, const G1AStore* keys,
+                                                   const G2JStore* K, const G2JStore* T, Fp12* f) {
+  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > nslots) return;
+  G1A P[1];
+  G2A Q[1];
+  if (s < nslots) {
+    G1A x = load_g1a(keys[s]);
+    G1J bx = jac_from_aff(x);
+    if (nslots > 1) bx = jac_mul_u64(bx, rlc_beta(seed, s));
+    P[0] = g1_to_aff(bx);
+    Q[0] = g2_to_aff(g2_clear_cofactor(load_g2j(K[s])));
+  } else {
+    P[0] = G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false};
+    Q[0] = g2_to_aff(load_g2j(T[0]));
+  }
+  f[s] = (P[0].inf || Q[0].inf) ? fp12_one() : miller_loop<1>(P, Q, 1);
+}
+
+// product of the npairs Miller values, one final exponentiation, verdict
+DG_KERNEL void __launch_bounds__(64) k_final_check(uint32_t npairs, const Fp12* f, uint32_t* ok) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  G1A P[2];
-  G2A Q[2];
-  int np = 0;
-  G1A key = load_g1a(pk[0]);
-  G2A a = g2_to_aff(g2_clear_cofactor(load_g2j(sumR[0])));
-  G2A b = g2_to_aff(load_g2j(sumT[0]));
-  if (!key.inf && !a.inf) {
-    P[np] = key;
-    Q[np] = a;
-    ++np;
-  }
-  if (!b.inf) {
-    P[np] = G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false};
-    Q[np] = b;
-    ++np;
-  }
-  bool good = np == 0 ? true : fp12_is_one(final_exp_cubed(miller_loop<2>(P, Q, np)));
-  *ok = good ? 1u : 0u;
+  Fp12 acc = f[0];
+  for (uint32_t s = 1; s < npairs; ++s) acc = fp12_mul(acc, f[s]);
+  *ok = fp12_is_one(final_exp_cubed(acc)) ? 1u : 0u;
 }
 
-// per-item bls.Verify with precomputed uncleared hash Q_i and decoded S_i; pk index per item (or 0)
-DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, const G1AStore* pks, const uint32_t* pk_idx,
-                                                    const G2JStore* Q, const uint32_t* q_idx, const G2AStore* S,
-                                                    uint8_t* status) {
+// H_r = h_eff(Q_r), affine (individual checks)
+DG_KERNEL void __launch_bounds__(128) k_clear_rounds(uint32_t R, const G2JStore* Q, G2AStore* H) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  store_g2a(H[r], g2_to_aff(g2_clear_cofactor(load_g2j(Q[r]))));
+}
+
+// individual bls.Verify of item i: e(X_slot, H_{i/k}) == e(g1, S_i).  all = 1: every decoded item
+// (after a failed batch); all = 0: only the isolated ones.
+DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, uint32_t all, const G1AStore* keys,
+                                                    const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
+                                                    const uint8_t* isolate, uint8_t* status) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (status[i] != DG_ST_OK_) return;
-  G1A key = load_g1a(pks[pk_idx ? pk_idx[i] : 0]);
-  G2A h = g2_to_aff(g2_clear_cofactor(load_g2j(Q[q_idx ? q_idx[i] : i])));
+  if (!all && !isolate[i]) return;
+  G1A key = load_g1a(keys[item_slot ? item_slot[i] : 0u]);
+  G2A h = load_g2a(H[i / k]);
   G2A s = load_g2a(S[i]);
   G1A P[2];
   G2A Qa[2];
@@ -213,6 +340,105 @@ DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, const G1AStore* 
   }
   bool good = np == 0 ? true : fp12_is_one(final_exp_cubed(miller_loop<2>(P, Qa, np)));
   status[i] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
+}
+
+// *flag |= 1 if any byte of v[0..n) is non-zero
+DG_KERNEL void __launch_bounds__(256) k_any(uint32_t n, const uint8_t* v, uint32_t* flag) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && v[i]) atomicOr(flag, 1u);
+}
+
+// ------------------------------------------------------------------ Recover (A6)
+// per round: the first t items (input order) that passed VerifyPartial, sorted by index, duplicates
+// collapsed (kyber xyCommit); round_status NOT_ENOUGH if fewer than t distinct remain.  share_status
+// = the verify status of every item examined, NOT_EXAMINED after the t-th collected one.
+DG_KERNEL void __launch_bounds__(128) k_recover_select(uint32_t R, uint32_t k, uint32_t t, const uint8_t* partials,
+                                                       const uint8_t* status, uint32_t* sel, uint32_t* selidx,
+                                                       uint8_t* round_status, uint8_t* share_status) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  uint32_t* ps = sel + (size_t)r * t;
+  uint32_t* pi = selidx + (size_t)r * t;
+  uint32_t got = 0;
+  for (uint32_t j = 0; j < k; ++j) {
+    size_t i = (size_t)r * k + j;
+    if (got >= t) {
+      share_status[i] = DG_ST_NOT_EXAMINED_;
+      continue;
+    }
+    uint8_t st = status[i];
+    share_status[i] = st;
+    if (st != DG_ST_OK_) continue;
+    uint32_t idx = be16(partials + 98 * i);
+    // insertion by index (stable: the earlier of two equal indices stays first)
+    uint32_t m = got;
+    while (m > 0 && pi[m - 1] > idx) {
+      pi[m] = pi[m - 1];
+      ps[m] = ps[m - 1];
+      --m;
+    }
+    pi[m] = idx;
+    ps[m] = j;
+    ++got;
+  }
+  uint32_t distinct = 0;
+  for (uint32_t m = 0; m < got; ++m) {
+    if (m > 0 && pi[m] == pi[m - 1]) continue;
+    pi[distinct] = pi[m];
+    ps[distinct] = ps[m];
+    ++distinct;
+  }
+  round_status[r] = distinct >= t ? DG_ST_OK_ : DG_ST_NOT_ENOUGH_;
+}
+
+// thread (r, m): lambda_m * S_{r, sel[m]}  (lambda over the round's t selected indices)
+DG_KERNEL void __launch_bounds__(64) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
+                                                     const uint32_t* selidx, const uint8_t* round_status,
+                                                     const G2AStore* S, G2JStore* terms) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= R * t) return;
+  uint32_t r = g / t, m = g % t;
+  if (round_status[r] != DG_ST_OK_) {
+    store_g2j(terms[g], jac_infinity<Fp2>());
+    return;
+  }
+  Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, m);
+  G2J p = jac_from_aff(load_g2a(S[(size_t)r * k + sel[g]]));
+  store_g2j(terms[g], jac_mul_u256(p, lam.l));
+}
+
+// compress points (zeros where status != OK)
+DG_KERNEL void __launch_bounds__(128) k_compress_g2(uint32_t n, const G2JStore* P, const uint8_t* st, uint8_t* out96) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (st && st[i] != DG_ST_OK_) {
+    for (int b = 0; b < 96; ++b) out96[96ull * i + b] = 0;
+    return;
+  }
+  g2_compress_aff(out96 + 96ull * i, g2_to_aff(load_g2j(P[i])));
+}
+
+// A7: bls.Sign / tbls.Sign -- x * H(m); scalars are 32 B big-endian (< r)
+DG_KERNEL void __launch_bounds__(128) k_sign(uint32_t n, const uint8_t* sc32, const uint16_t* index, const uint8_t* msgs,
+                                             uint32_t msg_len, const uint8_t* dst, uint32_t dst_len, uint8_t* out) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t kl[8];
+  const uint8_t* s = sc32 + 32ull * i;
+  for (int w = 0; w < 8; ++w) {
+    const uint8_t* q = s + 28 - 4 * w;
+    kl[w] = (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | q[3];
+  }
+  G2J h = hash_to_g2(msgs + (size_t)msg_len * i, msg_len, dst, dst_len);
+  G2A sig = g2_to_aff(jac_mul_u256(h, kl));
+  uint32_t rec = index ? 98u : 96u;
+  uint8_t* o = out + (size_t)rec * i;
+  if (index) {
+    o[0] = (uint8_t)(index[i] >> 8);
+    o[1] = (uint8_t)index[i];
+    o += 2;
+  }
+  g2_compress_aff(o, sig);
 }
 #endif
 

@@ -1,0 +1,68 @@
+"""Multi-GPU layout of the verify path: one process per GPU, one contiguous round range
+per rank, no data-path collective; the only exchange is the all-gather of per-round verdict bitmaps
+(RCCL over xGMI on the GPU node, gloo in the CPU tests)."""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PROBE = os.path.join(os.path.dirname(_HERE), "tools", "microbench", "libdrandprobe.so")
+
+
+def round_range(total, world, rank):
+    """[a, b) of `total` rounds for `rank`: contiguous, sizes differ by at most one."""
+    base, extra = divmod(total, world)
+    a = rank * base + min(rank, extra)
+    return a, a + base + (1 if rank < extra else 0)
+
+
+def pack_bits(status):
+    """uint8 status per round (torch tensor) -> verdict bitmap (1 = rejected), little-endian bit order."""
+    import torch
+
+    bad = (status != 0).to(torch.uint8)
+    pad = (-bad.numel()) % 8
+    if pad:
+        bad = torch.cat([bad, torch.zeros(pad, dtype=torch.uint8, device=bad.device)])
+    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=bad.device)
+    return (bad.view(-1, 8) * w).sum(dim=1).to(torch.uint8)
+
+
+def allgather_verdicts(status, world, group=None):
+    """All-gather every rank's packed verdict bitmap (equal-size shards padded to the largest)."""
+    import torch
+    import torch.distributed as dist
+
+    bits = pack_bits(status)
+    if world == 1:
+        return bits
+    n = torch.tensor([bits.numel()], device=bits.device, dtype=torch.int64)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+    m = int(n.item())
+    if bits.numel() < m:
+        bits = torch.cat([bits, torch.zeros(m - bits.numel(), dtype=torch.uint8, device=bits.device)])
+    out = torch.empty(world * m, dtype=torch.uint8, device=bits.device)
+    dist.all_gather_into_tensor(out, bits, group=group)
+    return out
+
+
+def unpack_bits(bitmap, sizes):
+    """Inverse of the padded all-gather: per-rank bitmaps -> one flat verdict array (numpy)."""
+    b = np.unpackbits(np.asarray(bitmap, dtype=np.uint8), bitorder="little")
+    m = len(b) // len(sizes)
+    return np.concatenate([b[r * m:r * m + s] for r, s in enumerate(sizes)])
+
+
+def mad_peak(device=0):
+    """Measured v_mad_u64_u32 lane-MAC rate (the integer-VALU roofline denominator)."""
+    lib = ctypes.CDLL(PROBE)
+    rate = ctypes.c_double()
+    cus = ctypes.c_int()
+    clk = ctypes.c_int()
+    rc = lib.probe_mad_rate(device, ctypes.byref(rate), ctypes.byref(cus), ctypes.byref(clk))
+    if rc != 0:
+        raise RuntimeError("probe_mad_rate failed")
+    return {"tmac_s": rate.value / 1e12, "cus": cus.value, "clock_khz": clk.value,
+            "source": "measured: dependency-free v_mad_u64_u32 streams (tools/microbench/probe.hip), "
+                      "%d CUs" % cus.value}

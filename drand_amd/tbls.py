@@ -140,6 +140,56 @@ def recover_batch(pub: PubPoly, msgs, partials, t, n, seed=0):
     return out, rs, ss
 
 
+def _beacon_arrays(prev_rounds, rounds, prev_sigs):
+    pr = np.ascontiguousarray(prev_rounds, dtype=np.uint64)
+    rr = np.ascontiguousarray(rounds, dtype=np.uint64)
+    ps = [bytes(x) for x in prev_sigs]
+    off = np.zeros(len(ps) + 1, dtype=np.uint32)
+    off[1:] = np.cumsum([len(x) for x in ps])
+    psb = L.u8(ps) if ps else np.zeros(0, np.uint8)
+    return pr, rr, psb, off
+
+
+def verify_beacons(public: bytes, prev_rounds, rounds, prev_sigs, sigs, seed=0):
+    """beacon.VerifyBeacon (beacon/chain.go:65-71) over a batch: statuses (DG_ST_*) per beacon."""
+    pr, rr, psb, off = _beacon_arrays(prev_rounds, rounds, prev_sigs)
+    n = len(rr)
+    s = L.u8(sigs, (n, 96))
+    st = np.zeros(n, dtype=np.uint8)
+    L.check(L.lib().dg_verify_beacons(L.ptr(bytes(public)), n, L.ptr(pr), L.ptr(rr), L.ptr(psb), L.ptr(off), L.ptr(s),
+                                      L.ptr(st), seed))
+    return st
+
+
+def beacon_messages(prev_rounds, rounds, prev_sigs):
+    """beacon.Message (beacon/chain.go:86-94) batch -> (n, 32)."""
+    pr, rr, psb, off = _beacon_arrays(prev_rounds, rounds, prev_sigs)
+    out = np.zeros((len(rr), 32), dtype=np.uint8)
+    L.check(L.lib().dg_beacon_messages(len(rr), L.ptr(pr), L.ptr(rr), L.ptr(psb), L.ptr(off), L.ptr(out)))
+    return out
+
+
+def randomness(sigs):
+    """beacon.RandomnessFromSignature (beacon/chain.go:52-55) batch -> (n, 32)."""
+    s = L.u8(sigs)
+    s = s.reshape(-1, 96)
+    out = np.zeros((s.shape[0], 32), dtype=np.uint8)
+    L.check(L.lib().dg_randomness(s.shape[0], L.ptr(s), L.ptr(out)))
+    return out
+
+
+def check_links(cur_round, cur_sig, prev_rounds, rounds, prev_sigs, sigs):
+    """syncFrom's link check (beacon/beacon.go:561-573): 0 linked / 1 broken per beacon."""
+    pr, rr, psb, off = _beacon_arrays(prev_rounds, rounds, prev_sigs)
+    n = len(rr)
+    s = L.u8(sigs, (n, 96))
+    out = np.zeros(n, dtype=np.uint8)
+    cs = bytes(cur_sig)
+    L.check(L.lib().dg_check_links(int(cur_round), L.ptr(cs), len(cs), n, L.ptr(pr), L.ptr(rr), L.ptr(psb), L.ptr(off),
+                                   L.ptr(s), L.ptr(out)))
+    return out
+
+
 class ThresholdScheme:
     """`tbls.NewThresholdSchemeOnG2(bls12381)`: keys on G1, signatures on G2 (key/curve.go:21-30)."""
 

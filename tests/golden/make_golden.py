@@ -197,10 +197,11 @@ def adversarial(coeffs, commits, shares, rounds):
     # duplicates collapse: [p0, p0, p1, p2] with t=3 -> 3 collected, 2 distinct -> error
     dup = [parts[3], parts[3], parts[4], parts[0]]
     sig, rs, ss = twin.recover(commits, msg, dup, t, n)
-    psig, prs, pss = T.recover(commits, msg, dup, t, n, statuses=[0, 0, 0, 1])
+    dst = [twin.verify_partial(commits, msg, p) for p in dup]
+    psig, prs, pss = T.recover(commits, msg, dup, t, n, statuses=dst)
     assert rs == prs == T.ST_NOT_ENOUGH
     cases.append({"round": rd["round"], "msg": rd["msg"], "modes": ["duplicate"], "partials": [h(p) for p in dup],
-                  "verify_status": [0, 0, 0, 1], "recover_status": rs, "recover_sig": None, "share_status": ss})
+                  "verify_status": dst, "recover_status": rs, "recover_sig": None, "share_status": ss})
     # out-of-order valid partials recover the same signature
     order = [parts[4], parts[2], parts[3]]
     sig, rs, ss = twin.recover(commits, msg, order, t, n)

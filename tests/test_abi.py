@@ -1,0 +1,63 @@
+"""The C-ABI boundary (CPU): libdrandgpu.so loads, exports every function include/drand_gpu.h declares
+with the argument count the ctypes binding uses, and refuses compute without a gfx950 device (no CPU
+fallback exists)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from drand_amd import _lib as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "drand_gpu.h")
+
+
+def declared():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(?:int|void|const char\*)\s+(dg_\w+)\s*\(([^)]*)\)\s*;", txt):
+        args = m.group(2).strip()
+        n = 0 if args in ("", "void") else args.count(",") + 1
+        out[m.group(1)] = n
+    return out
+
+
+def test_header_declares_the_survey_boundary():
+    d = declared()
+    for name in ("dg_init", "dg_shutdown", "dg_verify", "dg_verify_beacons", "dg_verify_partials", "dg_recover",
+                 "dg_hash_to_g2", "dg_sign", "dg_pubpoly_eval", "dg_check_links", "dg_beacon_messages",
+                 "dg_randomness"):
+        assert name in d, name
+
+
+def test_library_exports_every_declared_symbol():
+    lib = L.load()
+    nm = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (dg_\w+)", nm))
+    d = declared()
+    assert set(d) <= exported, set(d) - exported
+    for name, nargs in d.items():
+        assert hasattr(lib, name)
+        assert name in L.SIGNATURES, name
+        assert len(L.SIGNATURES[name][0]) == nargs, name
+
+
+def test_no_device_means_no_compute():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    lib = L.load()
+    assert lib.dg_device_ready() == 0
+    out = np.zeros(96, np.uint8)
+    msg = np.zeros(32, np.uint8)
+    rc = lib.dg_hash_to_g2(1, L.ptr(msg), 32, L.ptr(L.DST_NUL), len(L.DST_NUL), L.ptr(out))
+    assert rc == -1  # DG_E_NODEV: there is no CPU fallback
+    assert b"gfx950" in lib.dg_last_error()
+    with pytest.raises(L.DrandGpuError):
+        from drand_amd import tbls
+
+        tbls.hash_to_g2([bytes(32)])

@@ -22,6 +22,15 @@ def main():
     os.makedirs(os.path.dirname(out), exist_ok=True)
     tmp = out + ".partial"
     done = 0
+    if not os.path.exists(tmp):
+        # every chain file is a prefix of the longer ones: start from the longest shorter one
+        d = os.path.dirname(out)
+        have = sorted((int(f.split("_")[-1].split(".")[0]), f) for f in os.listdir(d)
+                      if f.startswith("chain_v1_") and f.endswith(".bin"))
+        have = [(m, f) for m, f in have if m < n]
+        if have:
+            import shutil
+            shutil.copyfile(os.path.join(d, have[-1][1]), tmp)
     if os.path.exists(tmp):
         done = os.path.getsize(tmp) // 96
     x = S.master_secret()

@@ -1,0 +1,113 @@
+// Instrumented HOST build of the kernels' device arithmetic (drand_amd/csrc/*.h compiled with g++ and
+// -DDG_OPCOUNT): counts the Montgomery multiplications and squarings each kernel's per-unit body
+// executes, so bench.py can turn kernel time into algorithmic multiply-adds/s.
+// Tooling only -- never linked into the product library.
+#include <string.h>
+
+#include "../../drand_amd/csrc/kernels.h"
+
+namespace dg {
+thread_local uint64_t g_fp_mul_count = 0, g_fp_sqr_count = 0;
+}
+using namespace dg;
+
+static void reset() { g_fp_mul_count = g_fp_sqr_count = 0; }
+static void take(uint64_t* out) {
+  out[0] = g_fp_mul_count;
+  out[1] = g_fp_sqr_count;
+}
+
+extern "C" {
+// out[0..1] = (mul, sqr) of hash_to_g2_uncleared(msg) -- k_h2c_uncleared per round
+void oc_h2c_uncleared(const uint8_t* msg, uint32_t len, const uint8_t* dst, uint32_t dl, uint64_t* out) {
+  reset();
+  G2J q = hash_to_g2_uncleared(msg, len, dst, dl);
+  (void)q;
+  take(out);
+}
+// g2_decompress + subgroup check -- k_decode_items per item; returns decode ok
+int oc_decode_g2(const uint8_t* sig96, uint64_t* out) {
+  reset();
+  G2A a;
+  bool ok = g2_decompress(a, sig96, true);
+  take(out);
+  return ok;
+}
+// k_round_combine per round (k = 1): W = alpha sigma, A = alpha Q (Q = uncleared hash of msg)
+void oc_round_combine(const uint8_t* msg, uint32_t len, const uint8_t* dst, uint32_t dl, const uint8_t* sig96,
+                      uint64_t alpha, uint64_t* out) {
+  G2J q = hash_to_g2_uncleared(msg, len, dst, dl);
+  G2A s;
+  g2_decompress(s, sig96, true);
+  reset();
+  G2J w = jac_mul_u64(jac_from_aff(s), alpha);
+  G2J a = jac_mul_u64(q, alpha);
+  (void)w;
+  (void)a;
+  take(out);
+}
+// one Jacobian G2 addition of two generic points (k_sum_rows / k_key_accum per point)
+void oc_g2_add(const uint8_t* sig_a, const uint8_t* sig_b, uint64_t* out) {
+  G2A a, b;
+  g2_decompress(a, sig_a, false);
+  g2_decompress(b, sig_b, false);
+  G2J ja = jac_dbl(jac_from_aff(a)), jb = jac_dbl(jac_from_aff(b));  // generic Z != 1
+  reset();
+  G2J c = jac_add(ja, jb);
+  (void)c;
+  take(out);
+}
+// k_pair_miller (key pair) + k_final_check for a batch of one key
+void oc_batch_final(const uint8_t* pk48, const uint8_t* sig_a, const uint8_t* sig_b, uint64_t* out) {
+  G1A pk;
+  g1_decompress(pk, pk48, false);
+  G2A a, b;
+  g2_decompress(a, sig_a, false);
+  g2_decompress(b, sig_b, false);
+  G2J K = jac_dbl(jac_from_aff(a)), T = jac_dbl(jac_from_aff(b));
+  reset();
+  G1A P[1] = {pk};
+  G2A Q[1] = {g2_to_aff(g2_clear_cofactor(K))};
+  Fp12 f0 = miller_loop<1>(P, Q, 1);
+  P[0] = G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false};
+  Q[0] = g2_to_aff(T);
+  Fp12 f1 = miller_loop<1>(P, Q, 1);
+  bool ok = fp12_is_one(final_exp_cubed(fp12_mul(f0, f1)));
+  (void)ok;
+  take(out);
+}
+// k_verify_items per item (individual check) given uncleared hash msg and sigma
+void oc_verify_item(const uint8_t* pk48, const uint8_t* msg, uint32_t len, const uint8_t* dst, uint32_t dl,
+                    const uint8_t* sig96, uint64_t* out) {
+  G1A pk;
+  g1_decompress(pk, pk48, false);
+  G2J q = hash_to_g2_uncleared(msg, len, dst, dl);
+  G2A s;
+  g2_decompress(s, sig96, false);
+  reset();
+  G2A h = g2_to_aff(g2_clear_cofactor(q));
+  G1A P[2] = {pk, G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false}};
+  G2A Q[2] = {h, s};
+  bool ok = fp12_is_one(final_exp_cubed(miller_loop<2>(P, Q, 2)));
+  (void)ok;
+  take(out);
+}
+// k_scale_items per item with nslots > 1: beta * sigma
+void oc_scale_item(const uint8_t* sig96, uint64_t beta, uint64_t* out) {
+  G2A s;
+  g2_decompress(s, sig96, false);
+  reset();
+  G2J u = jac_mul_u64(jac_from_aff(s), beta);
+  (void)u;
+  take(out);
+}
+// k_recover_terms per (round, share): lambda_m * S (lambda = 32 B little-endian limbs)
+void oc_recover_term(const uint8_t* sig96, const uint32_t* lam8, uint64_t* out) {
+  G2A s;
+  g2_decompress(s, sig96, false);
+  reset();
+  G2J u = jac_mul_u256(jac_from_aff(s), lam8);
+  (void)u;
+  take(out);
+}
+}

@@ -1,0 +1,71 @@
+"""Per-unit Montgomery multiplication/squaring counts of each verify-path kernel, from the instrumented
+host build of the device arithmetic (liboc.so), averaged over the committed 64-round chain fixture.
+Writes profiles/opcounts.json, which bench.py reads to convert kernel time into multiply-adds/s.
+MACs: one fp_mul = 288 v_mad_u64_u32, one fp_sqr = 222 (counted in drand_amd/csrc/fp_asm.h)."""
+import ctypes
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+MAC_MUL, MAC_SQR = 288, 222
+DST = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"
+
+
+def main():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    L = ctypes.CDLL(os.path.join(HERE, "liboc.so"))
+    c = json.load(open(os.path.join(ROOT, "tests", "golden", "chain_t3n5.json")))
+    rounds = c["rounds"]
+    pk = bytes.fromhex(c["pk"])
+    o = (ctypes.c_uint64 * 2)()
+    acc = {}
+
+    def add(name, n=1):
+        m, s = o[0], o[1]
+        a = acc.setdefault(name, [0, 0, 0])
+        a[0] += m
+        a[1] += s
+        a[2] += n
+
+    for i, r in enumerate(rounds):
+        msg = bytes.fromhex(r["msg"])
+        sig = bytes.fromhex(r["sig"])
+        alpha = int.from_bytes(hashlib.sha256(b"a%d" % i).digest()[:8], "big") | 1
+        L.oc_h2c_uncleared(msg, 32, DST, len(DST), o)
+        add("k_h2c_uncleared")
+        assert L.oc_decode_g2(sig, o) == 1
+        add("k_decode_items")
+        L.oc_round_combine(msg, 32, DST, len(DST), sig, ctypes.c_uint64(alpha), o)
+        add("k_round_combine")
+        L.oc_scale_item(sig, ctypes.c_uint64(alpha), o)
+        add("k_scale_items[nslots>1]")
+        nxt = bytes.fromhex(rounds[(i + 1) % len(rounds)]["sig"])
+        L.oc_g2_add(sig, nxt, o)
+        add("k_sum_rows")
+        lam = (ctypes.c_uint32 * 8)(*[int.from_bytes(hashlib.sha256(b"l%d%d" % (i, w)).digest()[:4], "little")
+                                      for w in range(7)] + [0x3fffffff])
+        L.oc_recover_term(sig, lam, o)
+        add("k_recover_terms")
+        if i < 8:
+            L.oc_verify_item(pk, msg, 32, DST, len(DST), sig, o)
+            add("k_verify_items")
+            L.oc_batch_final(pk, sig, nxt, o)
+            add("k_pair_miller+k_final_check")
+    out = {"mac_per_mul": MAC_MUL, "mac_per_sqr": MAC_SQR, "sample": "tests/golden/chain_t3n5.json (64 rounds)",
+           "per_unit": {}}
+    for k, (m, s, n) in acc.items():
+        out["per_unit"][k] = {"mul": m / n, "sqr": s / n, "M": (m + s) / n, "macs": (m * MAC_MUL + s * MAC_SQR) / n}
+    out["per_unit"]["k_key_accum"] = out["per_unit"]["k_sum_rows"]
+    with open(os.path.join(ROOT, "profiles", "opcounts.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    for k, v in sorted(out["per_unit"].items()):
+        print("%-28s M=%9.1f  MACs=%12.0f" % (k, v["M"], v["macs"]))
+
+
+if __name__ == "__main__":
+    main()

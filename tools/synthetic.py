@@ -43,3 +43,8 @@ def share_value(coeffs, i):
 def chain_path(n):
     import os
     return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "chain_v1_%d.bin" % n)
+
+
+# x * g1 for x = master_secret(): the group key C_0 of every synthetic group (= chain_t3n5.json "pk";
+# pinned by tests/test_oracle.py::test_group_pk_constant)
+GROUP_PK = bytes.fromhex("a48a078a2548dcc710aa9925a1c0cf951be802bdce52febb5f1b75af1a01c22760724cd295bdc4fe7e5ab0f6cead0564")
