@@ -110,7 +110,14 @@ def u8(a, shape=None):
     elif isinstance(a, (bytes, bytearray)):
         arr = np.frombuffer(bytes(a), dtype=np.uint8).copy()
     else:
-        arr = np.frombuffer(b"".join(bytes(x) for x in a), dtype=np.uint8).copy()
+        def flat(x):
+            if isinstance(x, (bytes, bytearray, memoryview)):
+                return bytes(x)
+            if isinstance(x, np.ndarray):
+                return np.ascontiguousarray(x, dtype=np.uint8).tobytes()
+            return b"".join(flat(y) for y in x)
+
+        arr = np.frombuffer(flat(a), dtype=np.uint8).copy()
     if shape is not None:
         arr = arr.reshape(shape)
     return arr

@@ -8,6 +8,7 @@ import pytest
 from drand_amd import _lib as L
 from drand_amd import tbls
 from oracle import twin
+from oracle.pyref import tbls as T
 from tests.fixtures import chain, chain_arrays, group, hx, load
 from tools import corrupt as C
 from tools import synthetic as S
@@ -55,7 +56,9 @@ def test_beacon_messages_randomness_links_golden():
     rr2 = list(rr)
     rr2[20] = rr2[19]
     links = tbls.check_links(0, hx(c["genesis_seed"]), pr, rr2, ps2, sigs)
-    assert np.nonzero(links)[0].tolist() == [10, 20]
+    want = T.check_links(0, hx(c["genesis_seed"]), pr, rr2, ps2, [bytes(s) for s in sigs])
+    assert links.tolist() == want
+    assert np.nonzero(links)[0].tolist() == [10, 20, 21]  # 21: its prev_round no longer matches round 20
 
 
 def test_verify_beacons_golden_chain():
