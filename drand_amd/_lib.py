@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdrandgpu.so")
+LIB_PATH = os.environ.get("DRAND_GPU_LIB", os.path.join(_HERE, "libdrandgpu.so"))
 
 # status codes (include/drand_gpu.h)
 ST_OK = 0

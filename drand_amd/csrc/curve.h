@@ -68,7 +68,7 @@ DGI Jac<F> jac_neg(const Jac<F>& p) {
 
 // dbl-2009-l (a = 0): 2M + 5S
 template <class F>
-DGN Jac<F> jac_dbl(const Jac<F>& p) {
+DGH Jac<F> jac_dbl(const Jac<F>& p) {
   F A = f_sqr(p.x);
   F B = f_sqr(p.y);
   F C = f_sqr(B);
@@ -84,7 +84,7 @@ DGN Jac<F> jac_dbl(const Jac<F>& p) {
 
 // add-2007-bl with the exceptional cases handled
 template <class F>
-DGN Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
+DGH Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
   F Z1Z1 = f_sqr(p.z);
@@ -110,7 +110,7 @@ DGN Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
 
 // madd-2007-bl: q affine (not infinity)
 template <class F>
-DGN Jac<F> jac_add_aff(const Jac<F>& p, const F& qx, const F& qy) {
+DGH Jac<F> jac_add_aff(const Jac<F>& p, const F& qx, const F& qy) {
   if (jac_is_inf(p)) return Jac<F>{qx, qy, f_one_of(F{})};
   F Z1Z1 = f_sqr(p.z);
   F U2 = f_mul(qx, Z1Z1);
@@ -132,7 +132,7 @@ DGN Jac<F> jac_add_aff(const Jac<F>& p, const F& qx, const F& qy) {
 }
 
 template <class F>
-DGN bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
+DGH bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
   bool pi = jac_is_inf(p), qi = jac_is_inf(q);
   if (pi || qi) return pi && qi;
   F Z1Z1 = f_sqr(p.z);
@@ -143,7 +143,7 @@ DGN bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
 
 // [k]P for a 64-bit scalar (double-and-add, MSB first)
 template <class F>
-DGN Jac<F> jac_mul_u64(const Jac<F>& p, uint64_t k) {
+DGH Jac<F> jac_mul_u64(const Jac<F>& p, uint64_t k) {
   Jac<F> acc = jac_infinity<F>();
   for (int b = 63; b >= 0; --b) {
     acc = jac_dbl(acc);
@@ -153,7 +153,7 @@ DGN Jac<F> jac_mul_u64(const Jac<F>& p, uint64_t k) {
 }
 // [k]P for a 256-bit scalar given as 8 little-endian 32-bit limbs (plain integer)
 template <class F>
-DGN Jac<F> jac_mul_u256(const Jac<F>& p, const uint32_t* k) {
+DGH Jac<F> jac_mul_u256(const Jac<F>& p, const uint32_t* k) {
   Jac<F> acc = jac_infinity<F>();
   // fixed 4-bit window with a 16-entry table would need 16 points in registers; keep double-and-add
   for (int w = 7; w >= 0; --w) {
@@ -171,25 +171,25 @@ DGI Aff<F> jac_to_aff_with_inv(const Jac<F>& p, const F& zinv) {
   F zi2 = f_sqr(zinv);
   return Aff<F>{f_mul(p.x, zi2), f_mul(p.y, f_mul(zi2, zinv)), false};
 }
-DGN G1A g1_to_aff(const G1J& p) {
+DGH G1A g1_to_aff(const G1J& p) {
   if (jac_is_inf(p)) return G1A{fp_zero(), fp_zero(), true};
   return jac_to_aff_with_inv(p, fp_inv(p.z));
 }
-DGN G2A g2_to_aff(const G2J& p) {
+DGH G2A g2_to_aff(const G2J& p) {
   if (jac_is_inf(p)) return G2A{fp2_zero(), fp2_zero(), true};
   return jac_to_aff_with_inv(p, fp2_inv(p.z));
 }
 
 // ---- G2 endomorphism psi = untwist o Frobenius o twist, subgroup check, cofactor clearing
-DGN G2J g2_psi(const G2J& p) {
+DGH G2J g2_psi(const G2J& p) {
   return G2J{fp2_mul(fp2_conj(p.x), fp2_const(PSI_CX)), fp2_mul(fp2_conj(p.y), fp2_const(PSI_CY)), fp2_conj(p.z)};
 }
 // [z]P with z = -Z_ABS
 DGI G2J g2_mul_z(const G2J& p) { return jac_neg(jac_mul_u64(p, Z_ABS)); }
 // P in G2  <=>  psi(P) == [z]P   (Scott, "A note on group membership tests for G1, G2 and GT")
-DGN bool g2_in_subgroup(const G2J& p) { return jac_eq(g2_psi(p), g2_mul_z(p)); }
+DGH bool g2_in_subgroup(const G2J& p) { return jac_eq(g2_psi(p), g2_mul_z(p)); }
 // RFC 9380 Appendix G.3 (Budroni-Pintore): h_eff * P = [z^2 - z - 1]P + [z - 1]psi(P) + psi^2(2P)
-DGN G2J g2_clear_cofactor(const G2J& p) {
+DGH G2J g2_clear_cofactor(const G2J& p) {
   G2J t1 = g2_mul_z(p);
   G2J t2 = g2_psi(p);
   G2J t3 = g2_psi(g2_psi(jac_dbl(p)));
@@ -201,13 +201,13 @@ DGN G2J g2_clear_cofactor(const G2J& p) {
   return jac_add(t3, jac_neg(p));
 }
 // G1 subgroup check by [r]P == O (keys and commits only: a handful per batch)
-DGN bool g1_in_subgroup(const G1J& p) {
+DGH bool g1_in_subgroup(const G1J& p) {
   // r as 8 little-endian limbs
   return jac_is_inf(jac_mul_u256(p, R_LIMBS));
 }
 
 // ---- ZCash decoding.  Status: 0 ok, 1 = decode error.
-DGN bool g1_decompress(G1A& out, const uint8_t* in, bool subgroup_check) {
+DGH bool g1_decompress(G1A& out, const uint8_t* in, bool subgroup_check) {
   uint8_t f = in[0];
   if (!(f & 0x80)) return false;
   if (f & 0x40) {
@@ -232,7 +232,7 @@ DGN bool g1_decompress(G1A& out, const uint8_t* in, bool subgroup_check) {
   if (subgroup_check && !g1_in_subgroup(jac_from_aff(out))) return false;
   return true;
 }
-DGN bool g2_decompress(G2A& out, const uint8_t* in, bool subgroup_check) {
+DGH bool g2_decompress(G2A& out, const uint8_t* in, bool subgroup_check) {
   uint8_t f = in[0];
   if (!(f & 0x80)) return false;
   if (f & 0x40) {

@@ -19,6 +19,17 @@
 #define DGI static inline
 #define DGN static
 #endif
+// Code-size policy (DESIGN.md §code generation).  DGH marks the mid-level routines (Fp2/Fp6 products,
+// exponentiations, curve formulas): out of line by default (DG_FLAT=0), inlined into their kernels with
+// DG_FLAT=1.  DGN routines (Fp12 / pairing level) are always out of line.
+#ifndef DG_FLAT
+#define DG_FLAT 0
+#endif
+#if DG_FLAT
+#define DGH DGI
+#else
+#define DGH DGN
+#endif
 
 #include "bls_constants.h"
 #include "fp_asm.h"
@@ -160,9 +171,40 @@ DGI Fp fp_mul_cios(const Fp& a, const Fp& b) {
 }
 
 // Montgomery multiplication / squaring.  Device: one product-scanning inline-asm block each
-// (tools/gen_fp_asm.py: 288 / 222 v_mad_u64_u32), kept out of line so the instruction stream of the
-// callers stays inside the instruction cache.
-DGN Fp fp_mul(const Fp& a, const Fp& b) {
+// (tools/gen_fp_asm.py: 288 / 222 v_mad_u64_u32).  DG_FP_CALL selects how callers reach it:
+//   0  out-of-line, operands by reference (through the stack)
+//   1  out-of-line, the 24 operand limbs passed as scalar arguments (VGPRs), result returned in VGPRs
+//   2  inlined at every call site
+#ifndef DG_FP_CALL
+#define DG_FP_CALL 1
+#endif
+#if defined(DG_FP_ASM) && DG_FP_CALL == 1
+#define DG_L12(p) p##0, p##1, p##2, p##3, p##4, p##5, p##6, p##7, p##8, p##9, p##10, p##11
+#define DG_P12(p)                                                                                      \
+  uint32_t p##0, uint32_t p##1, uint32_t p##2, uint32_t p##3, uint32_t p##4, uint32_t p##5, uint32_t p##6, \
+      uint32_t p##7, uint32_t p##8, uint32_t p##9, uint32_t p##10, uint32_t p##11
+#define DG_A12(x) x.l[0], x.l[1], x.l[2], x.l[3], x.l[4], x.l[5], x.l[6], x.l[7], x.l[8], x.l[9], x.l[10], x.l[11]
+__device__ __noinline__ Fp fp_mul_r(DG_P12(a), DG_P12(b)) {
+  const uint32_t a[12] = {DG_L12(a)}, b[12] = {DG_L12(b)};
+  Fp r;
+  fp_mont_mul_asm(r.l, a, b, P_LIMBS, P_INV32);
+  return fp_reduce_once(r);
+}
+__device__ __noinline__ Fp fp_sqr_r(DG_P12(a)) {
+  const uint32_t a[12] = {DG_L12(a)};
+  Fp r;
+  fp_mont_sqr_asm(r.l, a, P_LIMBS, P_INV32);
+  return fp_reduce_once(r);
+}
+DGI Fp fp_mul(const Fp& a, const Fp& b) { return fp_mul_r(DG_A12(a), DG_A12(b)); }
+DGI Fp fp_sqr(const Fp& a) { return fp_sqr_r(DG_A12(a)); }
+#else
+#if defined(DG_FP_ASM) && DG_FP_CALL == 2
+#define DGF DGI
+#else
+#define DGF DGN
+#endif
+DGF Fp fp_mul(const Fp& a, const Fp& b) {
   DG_COUNT_MUL();
 #if defined(DG_FP_ASM)
   Fp r;
@@ -172,7 +214,7 @@ DGN Fp fp_mul(const Fp& a, const Fp& b) {
   return fp_mul_cios(a, b);
 #endif
 }
-DGN Fp fp_sqr(const Fp& a) {
+DGF Fp fp_sqr(const Fp& a) {
   DG_COUNT_SQR();
 #if defined(DG_FP_ASM)
   Fp r;
@@ -182,6 +224,7 @@ DGN Fp fp_sqr(const Fp& a) {
   return fp_mul_cios(a, a);
 #endif
 }
+#endif
 
 // plain integer (little-endian limbs) -> Montgomery
 DGI Fp fp_to_mont(const Fp& a) { return fp_mul(a, fp_const(FP_R2)); }
@@ -219,9 +262,9 @@ DGI Fp fp_pow_sched(const Fp& x, int first, const int8_t (&steps)[NSTEPS][2]) {
   }
   return acc;
 }
-DGN Fp fp_inv(const Fp& a) { return fp_pow_sched(a, EXP_PM2_FIRST, EXP_PM2_STEPS); }
+DGH Fp fp_inv(const Fp& a) { return fp_pow_sched(a, EXP_PM2_FIRST, EXP_PM2_STEPS); }
 // returns x^((p-3)/4)
-DGN Fp fp_pow_pm3d4(const Fp& a) { return fp_pow_sched(a, EXP_PM3D4_FIRST, EXP_PM3D4_STEPS); }
+DGH Fp fp_pow_pm3d4(const Fp& a) { return fp_pow_sched(a, EXP_PM3D4_FIRST, EXP_PM3D4_STEPS); }
 // sqrt(a) if a is a square (r^2 == a checked by the caller or via return)
 DGI bool fp_sqrt(Fp& r, const Fp& a) {
   Fp t = fp_pow_pm3d4(a);
@@ -297,13 +340,13 @@ DGI Fp2 fp2_sub(const Fp2& a, const Fp2& b) { return Fp2{fp_sub(a.c0, b.c0), fp_
 DGI Fp2 fp2_dbl(const Fp2& a) { return Fp2{fp_dbl(a.c0), fp_dbl(a.c1)}; }
 DGI Fp2 fp2_neg(const Fp2& a) { return Fp2{fp_neg(a.c0), fp_neg(a.c1)}; }
 DGI Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
-DGN Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
+DGH Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
   Fp t0 = fp_mul(a.c0, b.c0);
   Fp t1 = fp_mul(a.c1, b.c1);
   Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
   return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
-DGN Fp2 fp2_sqr(const Fp2& a) {
+DGH Fp2 fp2_sqr(const Fp2& a) {
   Fp m = fp_mul(a.c0, a.c1);
   return Fp2{fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(m)};
 }
@@ -375,7 +418,7 @@ DGI Fp6 fp6_add(const Fp6& a, const Fp6& b) { return Fp6{fp2_add(a.c0, b.c0), fp
 DGI Fp6 fp6_sub(const Fp6& a, const Fp6& b) { return Fp6{fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
 DGI Fp6 fp6_neg(const Fp6& a) { return Fp6{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
 DGI Fp6 fp6_mul_v(const Fp6& a) { return Fp6{fp2_mul_xi(a.c2), a.c0, a.c1}; }
-DGN Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
+DGH Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
   Fp2 v0 = fp2_mul(a.c0, b.c0);
   Fp2 v1 = fp2_mul(a.c1, b.c1);
   Fp2 v2 = fp2_mul(a.c2, b.c2);
@@ -384,7 +427,7 @@ DGN Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
   Fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), v0), v2), v1);
   return Fp6{c0, c1, c2};
 }
-DGN Fp6 fp6_sqr(const Fp6& a) {
+DGH Fp6 fp6_sqr(const Fp6& a) {
   // CH-SQR2
   Fp2 s0 = fp2_sqr(a.c0);
   Fp2 ab = fp2_mul(a.c0, a.c1);
@@ -407,7 +450,7 @@ DGN Fp6 fp6_inv(const Fp6& a) {
   return Fp6{fp2_mul(c0, t), fp2_mul(c1, t), fp2_mul(c2, t)};
 }
 // (a0 + a1 v + a2 v^2) * (b0 + b1 v)
-DGN Fp6 fp6_mul_01(const Fp6& a, const Fp2& b0, const Fp2& b1) {
+DGH Fp6 fp6_mul_01(const Fp6& a, const Fp2& b0, const Fp2& b1) {
   Fp2 v0 = fp2_mul(a.c0, b0);
   Fp2 v1 = fp2_mul(a.c1, b1);
   Fp2 c0 = fp2_add(fp2_mul_xi(fp2_mul(a.c2, b1)), v0);

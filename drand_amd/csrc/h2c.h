@@ -17,7 +17,7 @@ struct Sha256 {
 
 DGI uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
-DGN void sha256_compress(uint32_t h[8], const uint32_t* win) {
+DGH void sha256_compress(uint32_t h[8], const uint32_t* win) {
   const uint32_t K[64] = {
       0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5, 0xd807aa98,
       0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786,
@@ -113,7 +113,7 @@ DGI void beacon_message(uint8_t out[32], const uint8_t* prev_sig, uint32_t prev_
 }
 
 // RFC 9380 §5.3.1 expand_message_xmd(msg, DST, 256) -> hash_to_field (count 2, m 2, L 64).
-DGN void hash_to_field_fp2x2(Fp2 u[2], const uint8_t* msg, uint32_t msg_len, const uint8_t* dst, uint32_t dst_len) {
+DGH void hash_to_field_fp2x2(Fp2 u[2], const uint8_t* msg, uint32_t msg_len, const uint8_t* dst, uint32_t dst_len) {
   uint8_t b0[32], bi[32];
   Sha256 s;
   sha256_init(s);
@@ -154,7 +154,7 @@ DGN void hash_to_field_fp2x2(Fp2 u[2], const uint8_t* msg, uint32_t msg_len, con
 // RFC 9380 §6.6.2 simplified SWU onto E2': y^2 = x^3 + A'x + B', A' = 240u, B' = 1012(1+u), Z = -(2+u).
 // One Fp inversion, one Fp sqrt of the norm and one (p-3)/4 exponentiation; the gx2 branch reuses the
 // first norm root through sqrt(norm(gx2)) = norm(u)^3 * 5 * sqrt(-5) * sqrt(-norm(gx1)).
-DGN void sswu_g2(Fp2& ox, Fp2& oy, const Fp2& u, const Fp& den_inv_norm_hint, bool use_hint) {
+DGH void sswu_g2(Fp2& ox, Fp2& oy, const Fp2& u, const Fp& den_inv_norm_hint, bool use_hint) {
   (void)den_inv_norm_hint;
   (void)use_hint;
   Fp2 A = fp2_const(SSWU_A), B = fp2_const(SSWU_B), Z = fp2_const(SSWU_Z);
@@ -204,7 +204,7 @@ DGI Fp2 poly_eval_const(const uint32_t (*c)[2][12], int n, const Fp2& x) {
 }
 
 // 3-isogeny E2' -> E2 (RFC 9380 Appendix E.3), output in Jacobian coordinates without inversion
-DGN G2J iso_map_g2(const Fp2& x, const Fp2& y) {
+DGH G2J iso_map_g2(const Fp2& x, const Fp2& y) {
   Fp2 xn = poly_eval_const(ISO_XNUM, 4, x);
   Fp2 xd = poly_eval_const(ISO_XDEN, 3, x);
   Fp2 yn = poly_eval_const(ISO_YNUM, 4, x);
