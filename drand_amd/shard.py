@@ -42,9 +42,13 @@ def allgather_verdicts(status, world, group=None):
     m = int(n.item())
     if bits.numel() < m:
         bits = torch.cat([bits, torch.zeros(m - bits.numel(), dtype=torch.uint8, device=bits.device)])
-    out = torch.empty(world * m, dtype=torch.uint8, device=bits.device)
-    dist.all_gather_into_tensor(out, bits, group=group)
-    return out
+    if dist.get_backend(group) == "nccl":  # RCCL on ROCm
+        out = torch.empty(world * m, dtype=torch.uint8, device=bits.device)
+        dist.all_gather_into_tensor(out, bits, group=group)
+        return out
+    parts = [torch.empty(m, dtype=torch.uint8, device=bits.device) for _ in range(world)]
+    dist.all_gather(parts, bits, group=group)  # gloo (CPU tests)
+    return torch.cat(parts)
 
 
 def unpack_bits(bitmap, sizes):
