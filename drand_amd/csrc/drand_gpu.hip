@@ -234,9 +234,9 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   RET(launch("k_key_accum", k_key_accum, b.nslots * nchunks, 128, st, b.R, b.nslots, chunk, nchunks,
              (const uint32_t*)cell, (const G2JStore*)A, Kp));
   RET(reduce_rows(Kp, tmp, b.nslots, nchunks, st));  // K_s = Kp[s]
-  RET(launch("k_pair_miller", k_pair_miller, b.nslots + 1, 64, st, b.nslots, seed, b.keys, (const G2JStore*)Kp,
-             (const G2JStore*)W, f));
-  RET(launch("k_final_check", k_final_check, 1, 64, st, b.nslots + 1, (const Fp12*)f, flag));
+  RET(launch("k_pair_miller_coop", k_pair_miller_coop, 128 * (b.nslots + 1), 128, st, b.nslots, seed, b.keys,
+             (const G2JStore*)Kp, (const G2JStore*)W, f));
+  RET(launch("k_final_coop", k_final_coop, 128, 128, st, b.nslots + 1, (const Fp12*)f, flag));
   // isolated items present?
   HIPCHK(hipMemsetAsync(flag + 1, 0, 4, st));
   RET(launch("k_any", k_any, N, 256, st, N, (const uint8_t*)iso, flag + 1));

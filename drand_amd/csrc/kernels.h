@@ -5,6 +5,7 @@
 #include "h2c.h"
 #include "pairing.h"
 #include "fr.h"
+#include "coop.h"
 
 namespace dg {
 
@@ -304,6 +305,57 @@ DG_KERNEL void __launch_bounds__(64) k_final_check(uint32_t npairs, const Fp12* 
   Fp12 acc = f[0];
   for (uint32_t s = 1; s < npairs; ++s) acc = fp12_mul(acc, f[s]);
   *ok = fp12_is_one(final_exp_cubed(acc)) ? 1u : 0u;
+}
+
+// Pair s on one 128-lane workgroup: setup on lane 0, then the multi-lane Miller loop (coop.h).
+// Pairs as k_pair_miller; f[s] = 1 when a side is the identity.
+DG_KERNEL void __launch_bounds__(128) k_pair_miller_coop(uint32_t nslots, uint64_t seed, const G1AStore* keys,
+                                                        const G2JStore* K, const G2JStore* T, Fp12* f) {
+  __shared__ Fp12W F, L;
+  __shared__ Fp2 prod[36];
+  __shared__ G1A sP;
+  __shared__ G2A sQ;
+  const uint32_t s = blockIdx.x;
+  if (threadIdx.x == 0) {
+    if (s < nslots) {
+      G1J bx = jac_from_aff(load_g1a(keys[s]));
+      if (nslots > 1) bx = jac_mul_u64(bx, rlc_beta(seed, s));
+      sP = g1_to_aff(bx);
+      sQ = g2_to_aff(g2_clear_cofactor(load_g2j(K[s])));
+    } else {
+      sP = G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false};
+      sQ = g2_to_aff(load_g2j(T[0]));
+    }
+  }
+  __syncthreads();
+  G1A P = sP;
+  G2A Q = sQ;
+  if (P.inf || Q.inf) {
+    if (threadIdx.x == 0) f[s] = fp12_one();
+    return;
+  }
+  co_miller_loop(&F, &L, prod, P, Q);
+  if (threadIdx.x < 6) ((Fp2*)&f[s])[(threadIdx.x & 1) * 3 + threadIdx.x / 2] = F.e[threadIdx.x];
+}
+
+// product of the npairs Miller values and one final exponentiation on one 128-lane workgroup
+DG_KERNEL void __launch_bounds__(128) k_final_coop(uint32_t npairs, const Fp12* f, uint32_t* ok) {
+  __shared__ Fp12W F, G, S[7];
+  __shared__ Fp2 prod[36];
+  const int t = threadIdx.x;
+  if (t < 6) F.e[t] = ((const Fp2*)&f[0])[(t & 1) * 3 + t / 2];
+  __syncthreads();
+  for (uint32_t s = 1; s < npairs; ++s) {
+    if (t < 6) G.e[t] = ((const Fp2*)&f[s])[(t & 1) * 3 + t / 2];
+    __syncthreads();
+    co_mul(&F, &F, &G, prod);
+  }
+  co_final_exp_cubed(&F, S, prod);
+  if (t == 0) {
+    bool one = fp2_eq(F.e[0], fp2_one());
+    for (int k = 1; k < 6; ++k) one = one && fp2_is_zero(F.e[k]);
+    *ok = one ? 1u : 0u;
+  }
 }
 
 // H_r = h_eff(Q_r), affine (individual checks)
