@@ -60,7 +60,8 @@ int fail(int code, const std::string& msg) {
 enum Slot {
   S_MSGS, S_DST, S_Q, S_S, S_U, S_STATUS, S_ISO, S_CELL, S_W, S_A, S_TMP, S_KP, S_F, S_H, S_FLAG, S_KEYS, S_KEYST,
   S_COMMITS, S_COMMITST, S_SLOTIDX, S_ITEMSLOT, S_SEL, S_SELIDX, S_RST, S_SST, S_TERMS, S_IN0, S_IN1, S_IN2, S_IN3,
-  S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_COUNT
+  S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
+  S_MSM_OUT, S_COUNT
 };
 
 int ws(Slot s, size_t bytes, void** out) {
@@ -202,40 +203,77 @@ struct Batch {
   uint8_t* status;
 };
 
+// Pippenger MSM (msm.h): out[0] = sum_r alpha_r PA_r, out[1] = sum_r alpha_r PB_r (PB may be null),
+// over the rounds with active[r] != 0.
+int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA, const G2JStore* PB, G2JStore** out,
+            hipStream_t st) {
+  const uint32_t nsides = PB ? 2 : 1;
+  uint32_t *cnt, *list;
+  G2JStore *chunks, *B, *G;
+  RET(wsT(S_MSM_CNT, 4 * MSM_NBK + 1, &cnt));
+  uint32_t *offset = cnt + MSM_NBK, *cursor = offset + MSM_NBK, *chunk_off = cursor + MSM_NBK;
+  RET(wsT(S_MSM_LIST, (size_t)MSM_WIN * R + 1, &list));
+  const uint32_t max_chunks = (MSM_WIN * R) / MSM_CHUNK + MSM_NBK;
+  RET(wsT(S_MSM_CHUNKS, (size_t)max_chunks * nsides, &chunks));
+  RET(wsT(S_MSM_B, (size_t)MSM_NBK * nsides, &B));
+  RET(wsT(S_MSM_G, (size_t)MSM_WIN * MSM_NGROUP * nsides, &G));
+  RET(wsT(S_MSM_OUT, 2, out));
+  HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * MSM_NBK, st));
+  RET(launch("k_msm_count", k_msm_count, R, 256, st, R, seed, active, cnt));
+  RET(launch("k_msm_scan", k_msm_scan, 256, 256, st, (const uint32_t*)cnt, offset, cursor, chunk_off));
+  RET(launch("k_msm_scatter", k_msm_scatter, R, 256, st, R, seed, active, cursor, list));
+  RET(launch("k_msm_chunks", k_msm_chunks, max_chunks * nsides, 128, st, max_chunks, nsides, (const uint32_t*)cnt,
+             (const uint32_t*)offset, (const uint32_t*)chunk_off, (const uint32_t*)list, PA, PB, chunks));
+  RET(launch("k_msm_buckets", k_msm_buckets, MSM_NBK * nsides, 128, st, max_chunks, nsides, (const uint32_t*)chunk_off,
+             (const G2JStore*)chunks, B));
+  RET(launch("k_msm_groups", k_msm_groups, MSM_WIN * MSM_NGROUP * nsides, 64, st, nsides, (const G2JStore*)B, G));
+  RET(launch("k_msm_windows", k_msm_windows, 64, 64, st, nsides, (const G2JStore*)G, *out));
+  return 0;
+}
+
 int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   const uint32_t N = b.R * b.k;
-  uint8_t* iso;
+  uint8_t *iso, *active;
   uint32_t *cell, *flag;
-  G2JStore *U, *W, *A, *tmp, *Kp;
+  G2JStore *U, *V, *A = nullptr, *tmp, *Kp, *msm;
   Fp12* f;
   RET(wsT(S_ISO, N, &iso));
+  RET(wsT(S_ACTIVE, b.R, &active));
   RET(wsT(S_CELL, (size_t)b.R * b.nslots, &cell));
   RET(wsT(S_FLAG, 4, &flag));
   RET(wsT(S_U, N, &U));
-  RET(wsT(S_W, b.R, &W));
-  RET(wsT(S_A, b.R, &A));
-  uint32_t nchunks = 16384 / b.nslots;
-  if (nchunks < 1) nchunks = 1;
-  if (nchunks > b.R) nchunks = b.R;
-  uint32_t chunk = (b.R + nchunks - 1) / nchunks;
-  nchunks = (b.R + chunk - 1) / chunk;
-  RET(wsT(S_KP, (size_t)b.nslots * nchunks, &Kp));
-  size_t ntmp = (size_t)b.nslots * nchunks > b.R ? (size_t)b.nslots * nchunks : b.R;
-  RET(wsT(S_TMP, ntmp, &tmp));
+  RET(wsT(S_W, b.R, &V));
+  if (b.nslots > 1) RET(wsT(S_A, b.R, &A));
   RET(wsT(S_F, b.nslots + 1, &f));
   HIPCHK(hipMemsetAsync(cell, 0, sizeof(uint32_t) * (size_t)b.R * b.nslots, st));
   RET(launch("k_decode_items", k_decode_items, N, 128, st, N, b.k, b.nslots, b.sigs, b.stride, b.offset, b.item_slot,
              b.key_status, b.S, b.status, cell, iso));
   RET(launch("k_scale_items", k_scale_items, N, 128, st, N, b.nslots, seed, b.item_slot, (const G2AStore*)b.S,
              (const uint8_t*)b.status, (const uint8_t*)iso, U));
-  RET(launch("k_round_combine", k_round_combine, b.R, 128, st, b.R, b.k, seed, (const G2JStore*)U,
-             (const uint8_t*)b.status, (const uint8_t*)iso, b.Q, W, A));
-  RET(reduce_rows(W, tmp, 1, b.R, st));  // T = W[0]
-  RET(launch("k_key_accum", k_key_accum, b.nslots * nchunks, 128, st, b.R, b.nslots, chunk, nchunks,
-             (const uint32_t*)cell, (const G2JStore*)A, Kp));
-  RET(reduce_rows(Kp, tmp, b.nslots, nchunks, st));  // K_s = Kp[s]
-  RET(launch("k_pair_miller_coop", k_pair_miller_coop, 128 * (b.nslots + 1), 128, st, b.nslots, seed, b.keys,
-             (const G2JStore*)Kp, (const G2JStore*)W, f));
+  RET(launch("k_round_combine", k_round_combine, b.R, 128, st, b.R, b.k, b.nslots, seed, (const G2JStore*)U,
+             (const uint8_t*)b.status, (const uint8_t*)iso, b.Q, V, A, active));
+  const G2JStore *T, *K;
+  if (b.nslots == 1) {
+    // T = sum alpha_r V_r and K = sum alpha_r Q_r in one MSM (shared bucket sort)
+    RET(msm_run(b.R, seed, active, V, b.Q, &msm, st));
+    T = msm;
+    K = msm + 1;
+  } else {
+    RET(msm_run(b.R, seed, active, V, nullptr, &msm, st));
+    T = msm;
+    uint32_t nchunks = 16384 / b.nslots;
+    if (nchunks < 1) nchunks = 1;
+    if (nchunks > b.R) nchunks = b.R;
+    uint32_t chunk = (b.R + nchunks - 1) / nchunks;
+    nchunks = (b.R + chunk - 1) / chunk;
+    RET(wsT(S_KP, (size_t)b.nslots * nchunks, &Kp));
+    RET(wsT(S_TMP, (size_t)b.nslots * nchunks, &tmp));
+    RET(launch("k_key_accum", k_key_accum, b.nslots * nchunks, 128, st, b.R, b.nslots, chunk, nchunks,
+               (const uint32_t*)cell, (const G2JStore*)A, Kp));
+    RET(reduce_rows(Kp, tmp, b.nslots, nchunks, st));  // K_s = Kp[s]
+    K = Kp;
+  }
+  RET(launch("k_pair_miller_coop", k_pair_miller_coop, 128 * (b.nslots + 1), 128, st, b.nslots, seed, b.keys, K, T, f));
   RET(launch("k_final_coop", k_final_coop, 128, 128, st, b.nslots + 1, (const Fp12*)f, flag));
   // isolated items present?
   HIPCHK(hipMemsetAsync(flag + 1, 0, 4, st));
@@ -254,8 +292,6 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   return 0;
 }
 
-// The group key of the single-key paths, decoded once per distinct key (kyber keeps it as a decoded
-// Point too): decompression + [r]P subgroup check is a ~1.5k-Fp-multiplication single-lane job.
 int decode_key(const uint8_t* pk48_host, hipStream_t st, G1AStore** keys, uint8_t** key_status) {
   Ctx& c = g_ctx;
   RET(wsT(S_PK1, 1, keys));

@@ -226,10 +226,13 @@ DG_KERNEL void __launch_bounds__(128) k_scale_items(uint32_t n, uint32_t nslots,
   store_g2j(U[i], u);
 }
 
-// per round r: W_r = alpha_r sum_j U_{r,j};  A_r = alpha_r Q_r (O when the round has no batch item)
-DG_KERNEL void __launch_bounds__(128) k_round_combine(uint32_t R, uint32_t k, uint64_t seed, const G2JStore* U,
-                                                      const uint8_t* status, const uint8_t* isolate,
-                                                      const G2JStore* Q, G2JStore* W, G2JStore* A) {
+// per round r: V_r = sum_j U_{r,j} over its batch items, active[r] = (any batch item); with several
+// key slots also A_r = alpha_r Q_r (the per-key hash sums are masked by the cell map, so they are not a
+// single MSM); the alpha_r-weighted sums of V (and of Q with one key) are Pippenger MSMs (msm.h)
+DG_KERNEL void __launch_bounds__(128) k_round_combine(uint32_t R, uint32_t k, uint32_t nslots, uint64_t seed,
+                                                      const G2JStore* U, const uint8_t* status,
+                                                      const uint8_t* isolate, const G2JStore* Q, G2JStore* V,
+                                                      G2JStore* A, uint8_t* active) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   bool any = false;
@@ -241,14 +244,9 @@ DG_KERNEL void __launch_bounds__(128) k_round_combine(uint32_t R, uint32_t k, ui
       any = true;
     }
   }
-  if (!any) {
-    store_g2j(W[r], jac_infinity<Fp2>());
-    store_g2j(A[r], jac_infinity<Fp2>());
-    return;
-  }
-  uint64_t a = rlc_alpha(seed, r);
-  store_g2j(W[r], jac_mul_u64(v, a));
-  store_g2j(A[r], jac_mul_u64(load_g2j(Q[r]), a));
+  store_g2j(V[r], v);
+  active[r] = any ? 1 : 0;
+  if (nslots > 1) store_g2j(A[r], any ? jac_mul_u64(load_g2j(Q[r]), rlc_alpha(seed, r)) : jac_infinity<Fp2>());
 }
 
 // Kp[s * nchunks + c] = sum of A_r over rounds r in chunk c whose (r, s) cell holds a batch item
@@ -495,3 +493,5 @@ DG_KERNEL void __launch_bounds__(128) k_sign(uint32_t n, const uint8_t* sc32, co
 #endif
 
 }  // namespace dg
+
+#include "msm.h"
