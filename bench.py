@@ -81,6 +81,37 @@ def cpu_baseline(pk, msgs, sigs, seconds=10.0, threads=16):
                       "bls.Verify: 2 Miller loops + final exp per round), %d threads, %.1f s" % (n, threads, dt)}
 
 
+def recover_bench(L, tbls, chain_sigs, first_round, R, t, n, steps):
+    """BASELINE configs[2]: VerifyPartial on every share + Lagrange Recover for an (n, t) group
+    over R rounds of the chain, through dg_recover (host-buffer API: the 98 B partials cross PCIe inside the
+    timed region).  Partials are produced on the GPU by dg_sign (untimed); every recovered signature must
+    equal the chain's signature byte for byte."""
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "groups.json")))["t%d" % t]
+    pub = tbls.PubPoly([bytes.fromhex(c) for c in g])
+    coeffs = S.poly_coeffs(t)
+    shares = [S.share_value(coeffs, i) for i in range(n)]
+    rounds = np.arange(first_round, first_round + R, dtype=np.uint64)
+    prev = [bytes(chain_sigs[r - 2]) if r >= 2 else S.GENESIS_SEED for r in rounds.tolist()]
+    msgs = tbls.beacon_messages(rounds - 1, rounds, prev)
+    sc = [shares[i] for _ in range(R) for i in range(n)]
+    idx = [i for _ in range(R) for i in range(n)]
+    t0 = time.perf_counter()
+    parts = tbls.sign_batch(sc, np.repeat(msgs, n, axis=0), idx).reshape(R, n, 98)
+    gen_s = time.perf_counter() - t0
+    sigs, rs, ss = tbls.recover_batch(pub, msgs, parts, t, n, seed=5)  # warmup + check
+    want = chain_sigs[first_round - 1:first_round - 1 + R]
+    assert not rs.any() and np.array_equal(sigs, want), "recovered signatures differ from the chain"
+    t0 = time.perf_counter()
+    for s in range(steps):
+        tbls.recover_batch(pub, msgs, parts, t, n, seed=6 + s)
+    dt = (time.perf_counter() - t0) / steps
+    return {"metric": "Recover/s at n=%d t=%d (all %d shares VerifyPartial'd, first t valid interpolated)" % (n, t, n),
+            "value": R / dt, "unit": "recovers/s", "rounds": R, "partials_per_round": n, "s_per_step": dt,
+            "partials_verified_per_s": R * n / dt, "partials_generated_s": gen_s,
+            "note": "host-buffer C-ABI (dg_recover): PCIe transfer of %d MB of partials inside the timed region; "
+                    "recovered signatures equal the chain's" % (R * n * 98 // 10**6)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,6 +120,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=100000, help="rounds per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--recover-rounds", type=int, default=20000, help="0 disables the Recover line")
     args = ap.parse_args()
 
     import torch
@@ -181,6 +213,9 @@ def main():
                     "kernel_avg_us": us, "units_per_launch": per_launch_units, "macs_per_unit": macs,
                     "peak_source": peak["source"]}
         share = {k: round(v[0] * v[1] / (dt * 1e6 / 1.0), 4) for k, v in kt.items()}
+        rec = None
+        if args.recover_rounds and chain is not None:
+            rec = recover_bench(L, tbls, chain, 1, min(args.recover_rounds, len(chain)), 33, 64, 1)
         cpu = None
         if not args.no_cpu_baseline:
             m = tbls.beacon_messages(rounds[:4096] - 1, rounds[:4096], prev_sigs[:4096])
@@ -191,7 +226,7 @@ def main():
                "config": {"workload": "batch bls.Verify / beacon.VerifyBeacon of %d linked chain rounds per GPU, one "
                                       "shared group key (BASELINE configs[1]; configs[3] at N>1)" % n,
                           "rounds_per_gpu": n, "global_rounds": world * n, "parallelism": "rounds sharded dp%d" % world},
-               "roofline": roof, "cpu_baseline": cpu,
+               "roofline": roof, "cpu_baseline": cpu, "recover": rec,
                "kernel_time_share": share,
                "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()}}
         print(json.dumps(out), flush=True)

@@ -161,3 +161,15 @@ def test_chain_file_prefix_matches_fixture():
     mm = np.memmap(files[0], dtype=np.uint8, mode="r")
     for k, r in enumerate(c["rounds"]):
         assert bytes(mm[96 * k:96 * k + 96]).hex() == r["sig"]
+
+
+def test_group_commits_fixture():
+    from tools import synthetic as S
+
+    g = load("groups.json")
+    for t in (3, 33, 129):
+        coeffs = S.poly_coeffs(t)
+        assert g["t%d" % t][0] == S.GROUP_PK.hex()
+        for j in (1, t - 1):
+            assert twin.g1_mul_gen(coeffs[j]).hex() == g["t%d" % t][j]
+    assert g["t3"] == chain()["commits"]
