@@ -1,10 +1,17 @@
-// Wave-cooperative GT (Fp12) arithmetic for the single-batch tail of the verify path: the product of
-// the per-key Miller values and the one final exponentiation per RLC batch (A11).  A lone lane doing
-// this is latency-bound (~30k dependent Fp multiplications); here one 64-lane wave splits every Fp12
-// product into its 36 independent Fp2 products, one per lane, staged through LDS, so the critical path
-// of a GT multiplication is one Fp2 product plus a 6-term sum.
+// Workgroup-cooperative arithmetic for the latency-bound tail of a verification batch: the Miller
+// loops (with the cofactor clearing of the per-key hash sums), the product of the Miller values and the
+// one final exponentiation (A11).  One lane doing this is bound by the latency of ~30k dependent Fp
+// multiplications (~1.3 us each on gfx950).  Here a 128-lane workgroup (two waves) evaluates every
+// formula as a short sequence of PHASES; a phase is a set of independent Fp multiplications, one per
+// lane, whose operands and results live in LDS:
+//   - an Fp2 x Fp2 product takes 3 lanes (Karatsuba: a0 b0, a1 b1, (a0+a1)(b0+b1)),
+//   - an Fp2 x Fp product takes 2 lanes,
+// and the linear glue between phases (additions, doubling, halving, multiplication by small constants)
+// runs on lane 0.  The critical path of a GT multiplication becomes one Fp product plus two short
+// combination steps; a G2 doubling becomes three Fp products deep, an addition six, a Miller doubling
+// step (line, f^2, f * line) four.
 //
-// Representation: Fp12 = Fp2[w]/(w^6 - xi), xi = 1 + u, f = sum_k e_k w^k.  With v = w^2 this is the
+// GT representation: Fp12 = Fp2[w]/(w^6 - xi), xi = 1 + u, f = sum_k e_k w^k.  With v = w^2 this is the
 // tower of field.h: (a0 + a1 v + a2 v^2) + (b0 + b1 v + b2 v^2) w = [a0, b0, a1, b1, a2, b2].
 #pragma once
 #include "pairing.h"
@@ -25,152 +32,503 @@ DGI Fp12W fp12_to_w(const Fp12& a) {
   w.e[5] = a.c1.c2;
   return w;
 }
-DGI Fp12 fp12_from_w(const Fp12W& w) {
-  return Fp12{Fp6{w.e[0], w.e[2], w.e[4]}, Fp6{w.e[1], w.e[3], w.e[5]}};
+DGI Fp12 fp12_from_w(const Fp12W& w) { return Fp12{Fp6{w.e[0], w.e[2], w.e[4]}, Fp6{w.e[1], w.e[3], w.e[5]}}; }
+
+// x / 2 (Montgomery form is linear, so halving the representative halves the value)
+DGI Fp fp_half(const Fp& a) {
+  uint32_t mask = 0u - (a.l[0] & 1u);
+  Fp s;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) s.l[i] = addc32(a.l[i], P_LIMBS[i] & mask, c, &c);
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < 11; ++i) r.l[i] = (s.l[i] >> 1) | (s.l[i + 1] << 31);
+  r.l[11] = (s.l[11] >> 1) | (c << 31);
+  return r;
+}
+DGI Fp2 fp2_half(const Fp2& a) { return Fp2{fp_half(a.c0), fp_half(a.c1)}; }
+DGI Fp2 fp2_triple(const Fp2& a) { return fp2_add(fp2_dbl(a), a); }
+// 3 b' c with b' = 4 (1 + u): 12 (1 + u) c
+DGI Fp2 fp2_mul_b3(const Fp2& c) {
+  Fp2 x = fp2_mul_xi(c);
+  Fp2 x4 = fp2_dbl(fp2_dbl(x));
+  return fp2_add(fp2_dbl(x4), x4);
 }
 
 #if defined(__HIP__)
-// All co_* functions are called by every lane of a 128-lane (two-wave) workgroup; buffers live in LDS.
-// `prod` is a 36-entry Fp2 LDS scratch.  dst may alias a or b.
-// Products run on lanes [CO_BASE, CO_BASE + 36) -- the second wave of a 128-lane workgroup -- so the
-// first wave is free for concurrent work (the Miller loop computes its next line on lane 0 while the
-// square of f is in flight: different waves, so truly concurrent, not divergent lanes of one wave).
-constexpr int CO_BASE = 64;
-__device__ __forceinline__ void co_mul_products(const Fp12W* a, const Fp12W* b, Fp2* prod) {
-  const int t = (int)threadIdx.x - CO_BASE;
-  if (t >= 0 && t < 36) prod[t] = fp2_mul(a->e[t / 6], b->e[t % 6]);
+constexpr int CO_THREADS = 128;
+
+// product jobs: o = a * b
+struct CoM2 {
+  const Fp2* a;
+  const Fp2* b;
+  Fp2* o;
+};
+struct CoM1 {
+  const Fp2* a;
+  const Fp* b;
+  Fp2* o;
+};
+
+template <int N>
+__device__ __forceinline__ CoM2 co_pick(const CoM2 (&j)[N], int q) {
+  CoM2 r = j[0];
+#pragma unroll
+  for (int k = 1; k < N; ++k)
+    if (q == k) r = j[k];
+  return r;
 }
-__device__ __forceinline__ void co_mul_sums(Fp12W* dst, const Fp2* prod) {
-  const int t = (int)threadIdx.x - CO_BASE;
-  if (t >= 0 && t < 6) {
+template <int N>
+__device__ __forceinline__ CoM1 co_pick(const CoM1 (&j)[N], int q) {
+  CoM1 r = j[0];
+#pragma unroll
+  for (int k = 1; k < N; ++k)
+    if (q == k) r = j[k];
+  return r;
+}
+__device__ __forceinline__ Fp co_kara_operand(const Fp2& a, int m) {
+  return m == 0 ? a.c0 : (m == 1 ? a.c1 : fp_add(a.c0, a.c1));
+}
+__device__ __forceinline__ Fp2 co_kara_combine(const Fp* t) {
+  return Fp2{fp_sub(t[0], t[1]), fp_sub(fp_sub(t[2], t[0]), t[1])};
+}
+
+// one phase of N2 Fp2 x Fp2 and N1 Fp2 x Fp products (3 N2 + 2 N1 <= 128); tmp: 128 Fp in LDS
+template <int N2, int N1>
+__device__ __forceinline__ void co_phase(const CoM2 (&j2)[N2], const CoM1 (&j1)[N1], Fp* tmp) {
+  static_assert(3 * N2 + 2 * N1 <= CO_THREADS, "phase too wide");
+  const int t = threadIdx.x;
+  if (t < 3 * N2) {
+    int q = t / 3, m = t - 3 * q;
+    CoM2 j = co_pick(j2, q);
+    tmp[t] = fp_mul(co_kara_operand(*j.a, m), co_kara_operand(*j.b, m));
+  } else if (t < 3 * N2 + 2 * N1) {
+    int u = t - 3 * N2, q = u / 2, m = u - 2 * q;
+    CoM1 j = co_pick(j1, q);
+    tmp[t] = fp_mul(m ? j.a->c1 : j.a->c0, *j.b);
+  }
+  __syncthreads();
+  if (t < N2) {
+    CoM2 j = co_pick(j2, t);
+    *j.o = co_kara_combine(tmp + 3 * t);
+  } else if (t < N2 + N1) {
+    int u = t - N2;
+    CoM1 j = co_pick(j1, u);
+    *j.o = Fp2{tmp[3 * N2 + 2 * u], tmp[3 * N2 + 2 * u + 1]};
+  }
+  __syncthreads();
+}
+template <int N2>
+__device__ __forceinline__ void co_phase(const CoM2 (&j2)[N2], Fp* tmp) {
+  static_assert(3 * N2 <= CO_THREADS, "phase too wide");
+  const int t = threadIdx.x;
+  if (t < 3 * N2) {
+    int q = t / 3, m = t - 3 * q;
+    CoM2 j = co_pick(j2, q);
+    tmp[t] = fp_mul(co_kara_operand(*j.a, m), co_kara_operand(*j.b, m));
+  }
+  __syncthreads();
+  if (t < N2) {
+    CoM2 j = co_pick(j2, t);
+    *j.o = co_kara_combine(tmp + 3 * t);
+  }
+  __syncthreads();
+}
+// lane-0 glue; everyone waits
+#define CO_SERIAL(...)      \
+  do {                      \
+    if (threadIdx.x == 0) { \
+      __VA_ARGS__;          \
+    }                       \
+    __syncthreads();        \
+  } while (0)
+
+// ---------------------------------------------------------------- GT arithmetic
+struct CoGT {
+  Fp2 prod[36];  // products a_i b_j
+  Fp tmp[CO_THREADS];
+  Fp2 gamma[6];  // Frobenius constants xi^(k (p-1) / 6)
+};
+
+// dst = a * b in GT (dst may alias a or b): 36 Fp2 products (108 lanes), then the 6 convolution sums
+__device__ __forceinline__ void co_fp12_mul(Fp12W* dst, const Fp12W* a, const Fp12W* b, CoGT* s) {
+  const int t = threadIdx.x;
+  if (t < 108) {
+    int q = t / 3, m = t - 3 * q;
+    s->tmp[t] = fp_mul(co_kara_operand(a->e[q / 6], m), co_kara_operand(b->e[q % 6], m));
+  }
+  __syncthreads();
+  if (t < 36) s->prod[t] = co_kara_combine(s->tmp + 3 * t);
+  __syncthreads();
+  if (t < 6) {
     Fp2 lo = fp2_zero(), hi = fp2_zero();
     for (int i = 0; i < 6; ++i) {
       int j = t - i;
       if (j >= 0)
-        lo = fp2_add(lo, prod[i * 6 + j]);
+        lo = fp2_add(lo, s->prod[i * 6 + j]);
       else
-        hi = fp2_add(hi, prod[i * 6 + j + 6]);
+        hi = fp2_add(hi, s->prod[i * 6 + j + 6]);
     }
     dst->e[t] = fp2_add(lo, fp2_mul_xi(hi));
   }
-}
-__device__ __forceinline__ void co_mul(Fp12W* dst, const Fp12W* a, const Fp12W* b, Fp2* prod) {
-  co_mul_products(a, b, prod);
-  __syncthreads();
-  co_mul_sums(dst, prod);
   __syncthreads();
 }
-__device__ __forceinline__ void co_copy(Fp12W* dst, const Fp12W* a) {
+// dst = a * l for a line l = l0 + l2 w^2 + l3 w^3 (nonzero coefficients in L->e[0], e[2], e[3])
+__device__ __forceinline__ void co_fp12_mul_line(Fp12W* dst, const Fp12W* a, const Fp12W* L, CoGT* s) {
   const int t = threadIdx.x;
-  if (t < 6) dst->e[t] = a->e[t];
+  if (t < 54) {
+    int q = t / 3, m = t - 3 * q;  // q = 3 i + jj, line slot {0, 2, 3}[jj]
+    int i = q / 3, jj = q - 3 * i;
+    s->tmp[t] = fp_mul(co_kara_operand(a->e[i], m), co_kara_operand(L->e[jj == 0 ? 0 : jj + 1], m));
+  }
+  __syncthreads();
+  if (t < 18) s->prod[t] = co_kara_combine(s->tmp + 3 * t);
+  __syncthreads();
+  if (t < 6) {
+    // c_k = a_k l0 + a_{k-2} l2 + a_{k-3} l3 (indices mod 6, wrapped terms times xi)
+    Fp2 lo = fp2_zero(), hi = fp2_zero();
+    for (int jj = 0; jj < 3; ++jj) {
+      int i = t - (jj == 0 ? 0 : jj + 1);
+      if (i >= 0)
+        lo = fp2_add(lo, s->prod[i * 3 + jj]);
+      else
+        hi = fp2_add(hi, s->prod[(i + 6) * 3 + jj]);
+    }
+    dst->e[t] = fp2_add(lo, fp2_mul_xi(hi));
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ void co_fp12_copy(Fp12W* dst, const Fp12W* a) {
+  if (threadIdx.x < 6) dst->e[threadIdx.x] = a->e[threadIdx.x];
   __syncthreads();
 }
 // f^(p^6): negate the odd w-coefficients
-__device__ __forceinline__ void co_conj(Fp12W* dst, const Fp12W* a) {
+__device__ __forceinline__ void co_fp12_conj(Fp12W* dst, const Fp12W* a) {
   const int t = threadIdx.x;
   if (t < 6) dst->e[t] = (t & 1) ? fp2_neg(a->e[t]) : a->e[t];
   __syncthreads();
 }
-// f^p: e_k -> conj(e_k) * xi^(k (p-1) / 6)
-__device__ __forceinline__ void co_frob(Fp12W* dst, const Fp12W* a) {
+// f^p: e_k -> conj(e_k) * gamma_k
+__device__ __forceinline__ void co_fp12_frob(Fp12W* dst, const Fp12W* a, CoGT* s) {
   const int t = threadIdx.x;
-  if (t < 6) {
-    Fp2 g = fp2_one();
-    Fp2 d = fp2_const(FROB_D);
-    if (t == 1) g = d;
-    if (t == 2) g = fp2_const(FROB_G1);
-    if (t == 3) g = fp2_mul(d, fp2_const(FROB_G1));
-    if (t == 4) g = fp2_const(FROB_G2);
-    if (t == 5) g = fp2_mul(d, fp2_const(FROB_G2));
-    dst->e[t] = fp2_mul(fp2_conj(a->e[t]), g);
+  if (t < 18) {
+    int q = t / 3, m = t - 3 * q;
+    s->tmp[t] = fp_mul(co_kara_operand(fp2_conj(a->e[q]), m), co_kara_operand(s->gamma[q], m));
   }
   __syncthreads();
+  if (t < 6) dst->e[t] = co_kara_combine(s->tmp + 3 * t);
+  __syncthreads();
+}
+__device__ __forceinline__ void co_gt_init(CoGT* s) {
+  CO_SERIAL({
+    Fp2 d = fp2_const(FROB_D), g1 = fp2_const(FROB_G1), g2 = fp2_const(FROB_G2);
+    s->gamma[0] = fp2_one();
+    s->gamma[1] = d;
+    s->gamma[2] = g1;
+    s->gamma[3] = fp2_mul(d, g1);
+    s->gamma[4] = g2;
+    s->gamma[5] = fp2_mul(d, g2);
+  });
 }
 // inversion on one lane (once per batch)
-__device__ __forceinline__ void co_inv(Fp12W* dst, const Fp12W* a) {
-  if (threadIdx.x == 0) *dst = fp12_to_w(fp12_inv(fp12_from_w(*a)));
-  __syncthreads();
+__device__ __forceinline__ void co_fp12_inv(Fp12W* dst, const Fp12W* a) {
+  CO_SERIAL(*dst = fp12_to_w(fp12_inv(fp12_from_w(*a))));
 }
 // a^z, z = -Z_ABS (a in the cyclotomic subgroup, so a^-1 = conj(a))
-__device__ __forceinline__ void co_exp_z(Fp12W* dst, const Fp12W* a, Fp12W* tmp, Fp2* prod) {
-  co_copy(tmp, a);
+__device__ __forceinline__ void co_fp12_exp_z(Fp12W* dst, const Fp12W* a, Fp12W* acc, CoGT* s) {
+  co_fp12_copy(acc, a);
   for (int b = 62; b >= 0; --b) {
-    co_mul(tmp, tmp, tmp, prod);
-    if ((Z_ABS >> b) & 1) co_mul(tmp, tmp, a, prod);
+    co_fp12_mul(acc, acc, acc, s);
+    if ((Z_ABS >> b) & 1) co_fp12_mul(acc, acc, a, s);
   }
-  co_conj(dst, tmp);
+  co_fp12_conj(dst, acc);
 }
 
-// f^(3 (p^12 - 1) / r), same chain as final_exp_cubed (pairing.h); result in *f.  scratch: 7 Fp12W.
-__device__ void co_final_exp_cubed(Fp12W* f, Fp12W* s, Fp2* prod) {
-  Fp12W *f1 = &s[0], *f2 = &s[1], *t0 = &s[2], *t1 = &s[3], *x = &s[4], *y = &s[5], *tmp = &s[6];
-  co_inv(f1, f);
-  co_conj(f2, f);
-  co_mul(f1, f2, f1, prod);  // f^(p^6 - 1)
-  co_frob(f2, f1);
-  co_frob(f2, f2);
-  co_mul(f2, f2, f1, prod);  // ^(p^2 + 1)
-  co_exp_z(t0, f2, tmp, prod);
-  co_conj(x, f2);
-  co_mul(t0, t0, x, prod);  // f2^(z-1)
-  co_exp_z(t1, t0, tmp, prod);
-  co_conj(x, t0);
-  co_mul(t1, t1, x, prod);  // f2^((z-1)^2)
-  co_exp_z(x, t1, tmp, prod);
-  co_frob(y, t1);
-  co_mul(x, x, y, prod);  // a = t1^(z+p)
-  co_exp_z(y, x, tmp, prod);
-  co_exp_z(y, y, tmp, prod);
-  co_frob(t0, x);
-  co_frob(t0, t0);
-  co_mul(y, y, t0, prod);
-  co_conj(t0, x);
-  co_mul(y, y, t0, prod);  // b = a^(z^2 + p^2 - 1)
-  co_mul(t0, f2, f2, prod);
-  co_mul(t0, t0, f2, prod);  // c = f2^3
-  co_mul(f, y, t0, prod);
+// f <- f^(3 (p^12 - 1) / r), the chain of final_exp_cubed (pairing.h).  scratch: 7 Fp12W.
+__device__ void co_final_exp_cubed(Fp12W* f, Fp12W* sc, CoGT* s) {
+  Fp12W *f1 = &sc[0], *f2 = &sc[1], *t0 = &sc[2], *t1 = &sc[3], *x = &sc[4], *y = &sc[5], *acc = &sc[6];
+  co_fp12_inv(f1, f);
+  co_fp12_conj(f2, f);
+  co_fp12_mul(f1, f2, f1, s);  // f^(p^6 - 1)
+  co_fp12_frob(f2, f1, s);
+  co_fp12_frob(f2, f2, s);
+  co_fp12_mul(f2, f2, f1, s);  // ^(p^2 + 1)
+  co_fp12_exp_z(t0, f2, acc, s);
+  co_fp12_conj(x, f2);
+  co_fp12_mul(t0, t0, x, s);  // f2^(z-1)
+  co_fp12_exp_z(t1, t0, acc, s);
+  co_fp12_conj(x, t0);
+  co_fp12_mul(t1, t1, x, s);  // f2^((z-1)^2)
+  co_fp12_exp_z(x, t1, acc, s);
+  co_fp12_frob(y, t1, s);
+  co_fp12_mul(x, x, y, s);  // a = t1^(z+p)
+  co_fp12_exp_z(y, x, acc, s);
+  co_fp12_exp_z(y, y, acc, s);
+  co_fp12_frob(t0, x, s);
+  co_fp12_frob(t0, t0, s);
+  co_fp12_mul(y, y, t0, s);
+  co_fp12_conj(t0, x);
+  co_fp12_mul(y, y, t0, s);  // b = a^(z^2 + p^2 - 1)
+  co_fp12_mul(t0, f2, f2, s);
+  co_fp12_mul(t0, t0, f2, s);  // c = f2^3
+  co_fp12_mul(f, y, t0, s);
 }
 
-// Multi-lane Miller loop of one pair (P affine G1, Q affine G2, neither at infinity), z < 0: lane 0
-// computes the line functions (the G2 doubling/addition steps), lanes CO_BASE.. fold them into f.
-// Result (tower layout) written by the caller from *f.
-__device__ void co_miller_loop(Fp12W* f, Fp12W* L, Fp2* prod, const G1A& P, const G2A& Q) {
+// ---------------------------------------------------------------- G2 (Jacobian) arithmetic
+struct CoG2 {
+  Fp2 x, y, z;
+};
+struct CoG2Tmp {
+  Fp2 v[16];
+  Fp tmp[CO_THREADS];
+  uint32_t flag;
+};
+
+// P <- 2P (dbl-2009-l, a = 0): three product phases
+__device__ void co_g2_dbl(CoG2* P, CoG2Tmp* s) {
+  Fp2 *A = &s->v[0], *B = &s->v[1], *YZ = &s->v[2], *E = &s->v[3], *XB = &s->v[4], *C = &s->v[5], *D0 = &s->v[6],
+      *F = &s->v[7], *DX = &s->v[8], *Y3 = &s->v[9];
+  {
+    const CoM2 j[3] = {{&P->x, &P->x, A}, {&P->y, &P->y, B}, {&P->y, &P->z, YZ}};
+    co_phase(j, s->tmp);
+  }
+  CO_SERIAL({
+    *E = fp2_triple(*A);
+    *XB = fp2_add(P->x, *B);
+  });
+  {
+    const CoM2 j[3] = {{B, B, C}, {XB, XB, D0}, {E, E, F}};
+    co_phase(j, s->tmp);
+  }
+  CO_SERIAL({
+    Fp2 D = fp2_dbl(fp2_sub(fp2_sub(*D0, *A), *C));
+    Fp2 X3 = fp2_sub(*F, fp2_dbl(D));
+    *DX = fp2_sub(D, X3);
+    P->x = X3;
+    P->z = fp2_dbl(*YZ);
+  });
+  {
+    const CoM2 j[1] = {{E, DX, Y3}};
+    co_phase(j, s->tmp);
+  }
+  CO_SERIAL(P->y = fp2_sub(*Y3, fp2_dbl(fp2_dbl(fp2_dbl(*C)))));
+}
+
+// O <- P + Q (add-2007-bl); exceptional cases (an input at infinity, P = +-Q) are resolved on lane 0.
+// O may alias P or Q.
+__device__ void co_g2_add(CoG2* O, const CoG2* P, const CoG2* Q, CoG2Tmp* s) {
+  Fp2 *Z1Z1 = &s->v[0], *Z2Z2 = &s->v[1], *ZZ = &s->v[2], *Z12 = &s->v[3], *U1 = &s->v[4], *U2 = &s->v[5],
+      *S1a = &s->v[6], *S2a = &s->v[7], *S1 = &s->v[8], *S2 = &s->v[9], *H = &s->v[10], *R = &s->v[11],
+      *I = &s->v[12], *R2 = &s->v[13], *J = &s->v[14], *V = &s->v[15];
+  CO_SERIAL({
+    bool pi = fp2_is_zero(P->z), qi = fp2_is_zero(Q->z);
+    s->flag = pi ? 1u : (qi ? 2u : 0u);
+    if (pi)
+      *O = *Q;
+    else if (qi)
+      *O = *P;
+    *Z12 = fp2_add(P->z, Q->z);
+  });
+  if (s->flag) return;
+  {
+    const CoM2 j[3] = {{&P->z, &P->z, Z1Z1}, {&Q->z, &Q->z, Z2Z2}, {Z12, Z12, ZZ}};
+    co_phase(j, s->tmp);
+  }
+  {
+    const CoM2 j[4] = {{&P->x, Z2Z2, U1}, {&Q->x, Z1Z1, U2}, {&P->y, &Q->z, S1a}, {&Q->y, &P->z, S2a}};
+    co_phase(j, s->tmp);
+  }
+  {
+    const CoM2 j[2] = {{S1a, Z2Z2, S1}, {S2a, Z1Z1, S2}};
+    co_phase(j, s->tmp);
+  }
+  CO_SERIAL({
+    *H = fp2_sub(*U2, *U1);
+    *R = fp2_dbl(fp2_sub(*S2, *S1));
+    s->flag = 0;
+    if (fp2_is_zero(*H)) {
+      // P = Q: double on this lane (practically never); P = -Q: infinity
+      if (fp2_is_zero(*R)) {
+        G2J d = jac_dbl(G2J{P->x, P->y, P->z});
+        *O = CoG2{d.x, d.y, d.z};
+      } else {
+        *O = CoG2{fp2_zero(), fp2_zero(), fp2_zero()};
+      }
+      s->flag = 1;
+    }
+    *Z12 = fp2_dbl(*H);  // I0 = 2H
+  });
+  if (s->flag) return;
+  {
+    const CoM2 j[2] = {{Z12, Z12, I}, {R, R, R2}};
+    co_phase(j, s->tmp);
+  }
+  {
+    const CoM2 j[2] = {{H, I, J}, {U1, I, V}};
+    co_phase(j, s->tmp);
+  }
+  CO_SERIAL({
+    Fp2 X3 = fp2_sub(fp2_sub(*R2, *J), fp2_dbl(*V));
+    *V = fp2_sub(*V, X3);                       // V - X3
+    *ZZ = fp2_sub(fp2_sub(*ZZ, *Z1Z1), *Z2Z2);  // 2 Z1 Z2
+    *I = X3;
+  });
+  {
+    // U1 <- r (V - X3), U2 <- S1 J, Z1Z1 <- Z3 = 2 Z1 Z2 H
+    const CoM2 j[3] = {{R, V, U1}, {S1, J, U2}, {ZZ, H, Z1Z1}};
+    co_phase(j, s->tmp);
+  }
+  CO_SERIAL({
+    O->x = *I;
+    O->y = fp2_sub(*U1, fp2_dbl(*U2));
+    O->z = *Z1Z1;
+  });
+}
+
+// psi(P) = (conj(x) cx, conj(y) cy, conj(z)) -- one phase; O may alias P
+__device__ void co_g2_psi(CoG2* O, const CoG2* P, CoG2Tmp* s) {
+  Fp2 *cx = &s->v[0], *cy = &s->v[1], *a = &s->v[2], *b = &s->v[3], *ox = &s->v[4], *oy = &s->v[5];
+  CO_SERIAL({
+    *cx = fp2_const(PSI_CX);
+    *cy = fp2_const(PSI_CY);
+    *a = fp2_conj(P->x);
+    *b = fp2_conj(P->y);
+  });
+  {
+    const CoM2 j[2] = {{a, cx, ox}, {b, cy, oy}};
+    co_phase(j, s->tmp);
+  }
+  CO_SERIAL({ *O = CoG2{*ox, *oy, fp2_conj(P->z)}; });
+}
+// O = [z] P (z = -Z_ABS); O must not alias P
+__device__ void co_g2_mul_z(CoG2* O, const CoG2* P, CoG2Tmp* s) {
+  CO_SERIAL(*O = *P);
+  for (int b = 62; b >= 0; --b) {
+    co_g2_dbl(O, s);
+    if ((Z_ABS >> b) & 1) co_g2_add(O, O, P, s);
+  }
+  CO_SERIAL(O->y = fp2_neg(O->y));
+}
+// P <- h_eff P = [z^2 - z - 1]P + [z - 1]psi(P) + psi^2(2P)  (as g2_clear_cofactor, curve.h); t: 4 CoG2
+__device__ void co_g2_clear_cofactor(CoG2* P, CoG2* t, CoG2Tmp* s) {
+  CoG2 *t1 = &t[0], *t2 = &t[1], *t3 = &t[2], *p0 = &t[3];
+  CO_SERIAL(*p0 = *P);
+  co_g2_mul_z(t1, p0, s);  // t1 = [z]P
+  co_g2_psi(t2, p0, s);    // t2 = psi(P)
+  CO_SERIAL(*t3 = *p0);
+  co_g2_dbl(t3, s);
+  co_g2_psi(t3, t3, s);
+  co_g2_psi(t3, t3, s);  // t3 = psi^2(2P)
+  CO_SERIAL(t2->y = fp2_neg(t2->y));
+  co_g2_add(t3, t3, t2, s);  // t3 = psi^2(2P) - psi(P)
+  CO_SERIAL(t2->y = fp2_neg(t2->y));
+  co_g2_add(t2, t1, t2, s);  // t2 = [z]P + psi(P)
+  co_g2_mul_z(P, t2, s);     // P = [z]([z]P + psi(P))
+  co_g2_add(t3, t3, P, s);
+  CO_SERIAL(t1->y = fp2_neg(t1->y));
+  co_g2_add(t3, t3, t1, s);
+  CO_SERIAL(p0->y = fp2_neg(p0->y));
+  co_g2_add(P, t3, p0, s);
+}
+
+// ---------------------------------------------------------------- Miller loop
+// Line functions of pairing.h (homogeneous projective T, M-twist), split into product phases; the line
+// l = c0 + c1 w^2 + c4 w^3 goes to L->e[0], e[2], e[3].
+struct CoML {
+  CoG2 T;      // projective (X, Y, Z)
+  Fp2 qx, qy;  // Q affine
+  Fp px, py;   // P affine
+  Fp2 v[16];
+  Fp tmp[CO_THREADS];
+};
+
+__device__ void co_line_dbl(CoML* m, Fp12W* L) {
+  Fp2 *xy = &m->v[0], *b = &m->v[1], *c = &m->v[2], *j = &m->v[3], *yz2 = &m->v[4], *yz = &m->v[5], *a = &m->v[6],
+      *e = &m->v[7], *g = &m->v[8], *h = &m->v[9], *j3 = &m->v[10], *nh = &m->v[11], *bf = &m->v[12],
+      *e2 = &m->v[13], *g2 = &m->v[14];
+  CoG2* T = &m->T;
+  CO_SERIAL(*yz = fp2_add(T->y, T->z));
+  {
+    const CoM2 jb[5] = {{&T->x, &T->y, xy}, {&T->y, &T->y, b}, {&T->z, &T->z, c}, {&T->x, &T->x, j}, {yz, yz, yz2}};
+    co_phase(jb, m->tmp);
+  }
+  CO_SERIAL({
+    *a = fp2_half(*xy);
+    *e = fp2_mul_b3(*c);
+    Fp2 f = fp2_triple(*e);
+    *g = fp2_half(fp2_add(*b, f));
+    *h = fp2_sub(fp2_sub(*yz2, *b), *c);
+    L->e[0] = fp2_sub(*e, *b);
+    *j3 = fp2_triple(*j);
+    *nh = fp2_neg(*h);
+    *bf = fp2_sub(*b, f);
+  });
+  {
+    const CoM2 jb[4] = {{e, e, e2}, {a, bf, &T->x}, {g, g, g2}, {b, h, &T->z}};
+    const CoM1 j1[2] = {{j3, &m->px, &L->e[2]}, {nh, &m->py, &L->e[3]}};
+    co_phase(jb, j1, m->tmp);
+  }
+  CO_SERIAL(T->y = fp2_sub(*g2, fp2_triple(*e2)));
+}
+
+__device__ void co_line_add(CoML* m, Fp12W* L) {
+  Fp2 *qyz = &m->v[0], *qxz = &m->v[1], *th = &m->v[2], *la = &m->v[3], *nth = &m->v[4], *c = &m->v[5],
+      *d = &m->v[6], *tq = &m->v[7], *lq = &m->v[8], *e = &m->v[9], *f = &m->v[10], *g = &m->v[11], *h = &m->v[12],
+      *gh = &m->v[13], *y1 = &m->v[14], *y2 = &m->v[15];
+  CoG2* T = &m->T;
+  {
+    const CoM2 jb[2] = {{&m->qy, &T->z, qyz}, {&m->qx, &T->z, qxz}};
+    co_phase(jb, m->tmp);
+  }
+  CO_SERIAL({
+    *th = fp2_sub(T->y, *qyz);
+    *la = fp2_sub(T->x, *qxz);
+    *nth = fp2_neg(*th);
+  });
+  {
+    const CoM2 jb[4] = {{th, th, c}, {la, la, d}, {th, &m->qx, tq}, {la, &m->qy, lq}};
+    const CoM1 j1[2] = {{nth, &m->px, &L->e[2]}, {la, &m->py, &L->e[3]}};
+    co_phase(jb, j1, m->tmp);
+  }
+  CO_SERIAL(L->e[0] = fp2_sub(*tq, *lq));
+  {
+    const CoM2 jb[3] = {{la, d, e}, {&T->z, c, f}, {&T->x, d, g}};
+    co_phase(jb, m->tmp);
+  }
+  CO_SERIAL({
+    *h = fp2_sub(fp2_add(*e, *f), fp2_dbl(*g));
+    *gh = fp2_sub(*g, *h);
+  });
+  {
+    const CoM2 jb[4] = {{la, h, &T->x}, {th, gh, y1}, {e, &T->y, y2}, {&T->z, e, qyz}};
+    co_phase(jb, m->tmp);
+  }
+  CO_SERIAL({
+    T->y = fp2_sub(*y1, *y2);
+    T->z = *qyz;
+  });
+}
+
+// f = Miller loop of (P, Q), P = (m->px, m->py) and Q = (m->qx, m->qy) affine, neither at infinity
+// (z < 0: conjugated at the end).  L: line scratch.
+__device__ void co_miller_loop(Fp12W* f, Fp12W* L, CoML* m, CoGT* s) {
   const int t = threadIdx.x;
-  G2Proj T{Q.x, Q.y, fp2_one()};
   if (t < 6) {
     f->e[t] = t == 0 ? fp2_one() : fp2_zero();
     L->e[t] = fp2_zero();
   }
-  __syncthreads();
-  Fp2 c0, c1, c4;
+  CO_SERIAL(m->T = CoG2{m->qx, m->qy, fp2_one()});
   for (int b = 62; b >= 0; --b) {
-    co_mul_products(f, f, prod);  // f^2 on lanes CO_BASE..
-    if (t == 0) line_dbl(T, c0, c1, c4, P.x, P.y);
-    __syncthreads();
-    co_mul_sums(f, prod);
-    if (t == 0) {
-      L->e[0] = c0;
-      L->e[2] = c1;
-      L->e[3] = c4;
-    }
-    __syncthreads();
-    co_mul_products(f, L, prod);
-    bool add = (Z_ABS >> b) & 1;
-    if (t == 0 && add) line_add(T, Q.x, Q.y, c0, c1, c4, P.x, P.y);
-    __syncthreads();
-    co_mul_sums(f, prod);
-    __syncthreads();
-    if (add) {
-      if (t == 0) {
-        L->e[0] = c0;
-        L->e[2] = c1;
-        L->e[3] = c4;
-      }
-      __syncthreads();
-      co_mul(f, f, L, prod);
+    co_line_dbl(m, L);
+    co_fp12_mul(f, f, f, s);
+    co_fp12_mul_line(f, f, L, s);
+    if ((Z_ABS >> b) & 1) {
+      co_line_add(m, L);
+      co_fp12_mul_line(f, f, L, s);
     }
   }
-  co_conj(f, f);
+  co_fp12_conj(f, f);
 }
 #endif
 

@@ -61,7 +61,7 @@ enum Slot {
   S_MSGS, S_DST, S_Q, S_S, S_U, S_STATUS, S_ISO, S_CELL, S_W, S_A, S_TMP, S_KP, S_F, S_H, S_FLAG, S_KEYS, S_KEYST,
   S_COMMITS, S_COMMITST, S_SLOTIDX, S_ITEMSLOT, S_SEL, S_SELIDX, S_RST, S_SST, S_TERMS, S_IN0, S_IN1, S_IN2, S_IN3,
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
-  S_MSM_OUT, S_COUNT
+  S_MSM_P1, S_MSM_W, S_MSM_OUT, S_COUNT
 };
 
 int ws(Slot s, size_t bytes, void** out) {
@@ -174,11 +174,11 @@ int wsT(Slot s, size_t count, T** out) {
 }
 
 // Collapse each of `rows` rows of `cols` Jacobian points (row-major in buf) to its sum, left in buf[row].
-int reduce_rows(G2JStore* buf, G2JStore* tmp, uint32_t rows, uint32_t cols, hipStream_t st) {
+int reduce_rows(G2JStore* buf, G2JStore* tmp, uint32_t rows, uint32_t cols, hipStream_t st, uint32_t max_chunk = 32) {
   G2JStore* src = buf;
   G2JStore* dst = tmp;
   while (cols > 1) {
-    uint32_t chunk = cols < 32 ? cols : 32;
+    uint32_t chunk = cols < max_chunk ? cols : max_chunk;
     uint32_t ocols = (cols + chunk - 1) / chunk;
     RET(launch("k_sum_rows", k_sum_rows, rows * ocols, 128, st, rows, cols, chunk, (const G2JStore*)src, dst));
     cols = ocols;
@@ -209,14 +209,16 @@ int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA
             hipStream_t st) {
   const uint32_t nsides = PB ? 2 : 1;
   uint32_t *cnt, *list;
-  G2JStore *chunks, *B, *G;
+  G2JStore *chunks, *BP, *tmp, *P1, *W;
   RET(wsT(S_MSM_CNT, 4 * MSM_NBK + 1, &cnt));
   uint32_t *offset = cnt + MSM_NBK, *cursor = offset + MSM_NBK, *chunk_off = cursor + MSM_NBK;
   RET(wsT(S_MSM_LIST, (size_t)MSM_WIN * R + 1, &list));
   const uint32_t max_chunks = (MSM_WIN * R) / MSM_CHUNK + MSM_NBK;
   RET(wsT(S_MSM_CHUNKS, (size_t)max_chunks * nsides, &chunks));
-  RET(wsT(S_MSM_B, (size_t)MSM_NBK * nsides, &B));
-  RET(wsT(S_MSM_G, (size_t)MSM_WIN * MSM_NGROUP * nsides, &G));
+  RET(wsT(S_MSM_B, (size_t)MSM_NBK * MSM_BSPLIT * nsides, &BP));
+  RET(wsT(S_MSM_G, (size_t)MSM_NBK * MSM_BSPLIT * nsides, &tmp));
+  RET(wsT(S_MSM_P1, (size_t)MSM_WIN * MSM_C * 16 * nsides, &P1));
+  RET(wsT(S_MSM_W, (size_t)MSM_WIN * nsides, &W));
   RET(wsT(S_MSM_OUT, 2, out));
   HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * MSM_NBK, st));
   RET(launch("k_msm_count", k_msm_count, R, 256, st, R, seed, active, cnt));
@@ -224,10 +226,13 @@ int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA
   RET(launch("k_msm_scatter", k_msm_scatter, R, 256, st, R, seed, active, cursor, list));
   RET(launch("k_msm_chunks", k_msm_chunks, max_chunks * nsides, 128, st, max_chunks, nsides, (const uint32_t*)cnt,
              (const uint32_t*)offset, (const uint32_t*)chunk_off, (const uint32_t*)list, PA, PB, chunks));
-  RET(launch("k_msm_buckets", k_msm_buckets, MSM_NBK * nsides, 128, st, max_chunks, nsides, (const uint32_t*)chunk_off,
-             (const G2JStore*)chunks, B));
-  RET(launch("k_msm_groups", k_msm_groups, MSM_WIN * MSM_NGROUP * nsides, 64, st, nsides, (const G2JStore*)B, G));
-  RET(launch("k_msm_windows", k_msm_windows, 64, 64, st, nsides, (const G2JStore*)G, *out));
+  RET(launch("k_msm_buckets", k_msm_buckets, MSM_NBK * MSM_BSPLIT * nsides, 128, st, max_chunks, nsides,
+             (const uint32_t*)chunk_off, (const G2JStore*)chunks, BP));
+  RET(reduce_rows(BP, tmp, MSM_NBK * nsides, MSM_BSPLIT, st));  // B[side][b] = BP[side * NBK + b]
+  RET(launch("k_msm_slices", k_msm_slices, nsides * MSM_WIN * MSM_C * 16, 128, st, nsides, (const G2JStore*)BP, P1));
+  RET(reduce_rows(P1, tmp, nsides * MSM_WIN * MSM_C, 16, st, 4));  // S[side][w][k] = P1[...]
+  RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * MSM_WIN * nsides, 128, st, (const G2JStore*)P1, W));
+  RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsides, 128, st, (const G2JStore*)W, *out));
   return 0;
 }
 

@@ -276,79 +276,69 @@ DG_KERNEL void __launch_bounds__(128) k_sum_rows(uint32_t rows, uint32_t cols, u
   store_g2j(out[g], acc);
 }
 
-// Miller loop of pair s: (beta_s X_s, h_eff(K_s)) for s < nslots, (-g1, T) for s == nslots; f = 1 if a
-// side is the identity
-DG_KERNEL void __launch_bounds__(64) k_pair_miller(uint32_t nslots, uint64_t seed, const G1AStore* keys,
-                                                   const G2JStore* K, const G2JStore* T, Fp12* f) {
-  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s > nslots) return;
-  G1A P[1];
-  G2A Q[1];
-  if (s < nslots) {
-    G1A x = load_g1a(keys[s]);
-    G1J bx = jac_from_aff(x);
-    if (nslots > 1) bx = jac_mul_u64(bx, rlc_beta(seed, s));
-    P[0] = g1_to_aff(bx);
-    Q[0] = g2_to_aff(g2_clear_cofactor(load_g2j(K[s])));
-  } else {
-    P[0] = G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false};
-    Q[0] = g2_to_aff(load_g2j(T[0]));
-  }
-  f[s] = (P[0].inf || Q[0].inf) ? fp12_one() : miller_loop<1>(P, Q, 1);
-}
-
-// product of the npairs Miller values, one final exponentiation, verdict
-DG_KERNEL void __launch_bounds__(64) k_final_check(uint32_t npairs, const Fp12* f, uint32_t* ok) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  Fp12 acc = f[0];
-  for (uint32_t s = 1; s < npairs; ++s) acc = fp12_mul(acc, f[s]);
-  *ok = fp12_is_one(final_exp_cubed(acc)) ? 1u : 0u;
-}
-
-// Pair s on one 128-lane workgroup: setup on lane 0, then the multi-lane Miller loop (coop.h).
-// Pairs as k_pair_miller; f[s] = 1 when a side is the identity.
+// Pair s on one 128-lane workgroup (coop.h): P side and Q side prepared cooperatively (for key pairs the
+// hash-side sum is cofactor-cleared here, once per key and batch), then the cooperative Miller loop.
+// Pairs: (beta_s X_s, h_eff K_s) for s < nslots, (-g1, T) for s == nslots; f[s] = 1
+// when a side is the identity.
 DG_KERNEL void __launch_bounds__(128) k_pair_miller_coop(uint32_t nslots, uint64_t seed, const G1AStore* keys,
-                                                        const G2JStore* K, const G2JStore* T, Fp12* f) {
+                                                         const G2JStore* K, const G2JStore* T, Fp12* f) {
+  __shared__ CoGT gt;
+  __shared__ CoML ml;
+  __shared__ CoG2Tmp g2t;
+  __shared__ CoG2 Kp, tp[4];
   __shared__ Fp12W F, L;
-  __shared__ Fp2 prod[36];
-  __shared__ G1A sP;
-  __shared__ G2A sQ;
+  __shared__ uint32_t skip;
   const uint32_t s = blockIdx.x;
-  if (threadIdx.x == 0) {
-    if (s < nslots) {
+  if (s < nslots) {
+    CO_SERIAL({
       G1J bx = jac_from_aff(load_g1a(keys[s]));
       if (nslots > 1) bx = jac_mul_u64(bx, rlc_beta(seed, s));
-      sP = g1_to_aff(bx);
-      sQ = g2_to_aff(g2_clear_cofactor(load_g2j(K[s])));
-    } else {
-      sP = G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false};
-      sQ = g2_to_aff(load_g2j(T[0]));
-    }
+      G1A pa = g1_to_aff(bx);
+      ml.px = pa.x;
+      ml.py = pa.y;
+      skip = pa.inf ? 1u : 0u;
+      G2J k = load_g2j(K[s]);
+      Kp = CoG2{k.x, k.y, k.z};
+    });
+    co_g2_clear_cofactor(&Kp, tp, &g2t);
+    CO_SERIAL({
+      G2A qa = g2_to_aff(G2J{Kp.x, Kp.y, Kp.z});
+      ml.qx = qa.x;
+      ml.qy = qa.y;
+      skip |= qa.inf ? 1u : 0u;
+    });
+  } else {
+    CO_SERIAL({
+      ml.px = fp_const(G1_GEN_X);
+      ml.py = fp_const(G1_GEN_NEG_Y);
+      G2A qa = g2_to_aff(load_g2j(T[0]));
+      ml.qx = qa.x;
+      ml.qy = qa.y;
+      skip = qa.inf ? 1u : 0u;
+    });
   }
-  __syncthreads();
-  G1A P = sP;
-  G2A Q = sQ;
-  if (P.inf || Q.inf) {
+  if (skip) {
     if (threadIdx.x == 0) f[s] = fp12_one();
     return;
   }
-  co_miller_loop(&F, &L, prod, P, Q);
+  co_miller_loop(&F, &L, &ml, &gt);
   if (threadIdx.x < 6) ((Fp2*)&f[s])[(threadIdx.x & 1) * 3 + threadIdx.x / 2] = F.e[threadIdx.x];
 }
 
 // product of the npairs Miller values and one final exponentiation on one 128-lane workgroup
 DG_KERNEL void __launch_bounds__(128) k_final_coop(uint32_t npairs, const Fp12* f, uint32_t* ok) {
+  __shared__ CoGT gt;
   __shared__ Fp12W F, G, S[7];
-  __shared__ Fp2 prod[36];
   const int t = threadIdx.x;
+  co_gt_init(&gt);
   if (t < 6) F.e[t] = ((const Fp2*)&f[0])[(t & 1) * 3 + t / 2];
   __syncthreads();
   for (uint32_t s = 1; s < npairs; ++s) {
     if (t < 6) G.e[t] = ((const Fp2*)&f[s])[(t & 1) * 3 + t / 2];
     __syncthreads();
-    co_mul(&F, &F, &G, prod);
+    co_fp12_mul(&F, &F, &G, &gt);
   }
-  co_final_exp_cubed(&F, S, prod);
+  co_final_exp_cubed(&F, S, &gt);
   if (t == 0) {
     bool one = fp2_eq(F.e[0], fp2_one());
     for (int k = 1; k < 6; ++k) one = one && fp2_is_zero(F.e[k]);

@@ -19,8 +19,8 @@
 namespace dg {
 
 constexpr uint32_t MSM_C = 8, MSM_WIN = 8, MSM_NB = 256, MSM_NBK = MSM_WIN * MSM_NB;  // 2048 bucket slots
-constexpr uint32_t MSM_CHUNK = 16;
-constexpr uint32_t MSM_GROUP = 17, MSM_NGROUP = 15;  // 255 = 15 * 17 buckets per window
+constexpr uint32_t MSM_CHUNK = 8;   // points per first-level lane
+constexpr uint32_t MSM_BSPLIT = 8;  // lanes per bucket at the second level
 
 #if defined(__HIP__)
 DG_KERNEL void __launch_bounds__(256) k_msm_count(uint32_t R, uint64_t seed, const uint8_t* active, uint32_t* count) {
@@ -111,55 +111,78 @@ DG_KERNEL void __launch_bounds__(128) k_msm_chunks(uint32_t max_chunks, uint32_t
   store_g2j(out[side * max_chunks + c], acc);
 }
 
-// lane g: side = g / NBK, bucket b: B[side][b] = sum of its chunks
+// lane g: side, bucket b, lane-in-bucket q < MSM_BSPLIT: strided partial sum of the bucket's chunks,
+// BP[(side * NBK + b) * MSM_BSPLIT + q]; the MSM_BSPLIT partials are then row-summed into B[side][b]
 DG_KERNEL void __launch_bounds__(128) k_msm_buckets(uint32_t max_chunks, uint32_t nsides, const uint32_t* chunk_off,
-                                                    const G2JStore* chunks, G2JStore* B) {
+                                                    const G2JStore* chunks, G2JStore* BP) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= MSM_NBK * nsides) return;
-  uint32_t side = g / MSM_NBK, b = g % MSM_NBK;
+  if (g >= MSM_NBK * MSM_BSPLIT * nsides) return;
+  uint32_t q = g % MSM_BSPLIT, sb = g / MSM_BSPLIT;
+  uint32_t side = sb / MSM_NBK, b = sb % MSM_NBK;
   uint32_t c0 = chunk_off[b], c1 = chunk_off[b + 1];
   G2J acc = jac_infinity<Fp2>();
-  for (uint32_t c = c0; c < c1; ++c) acc = jac_add(acc, load_g2j(chunks[side * max_chunks + c]));
-  store_g2j(B[g], acc);
+  for (uint32_t c = c0 + q; c < c1; c += MSM_BSPLIT) acc = jac_add(acc, load_g2j(chunks[side * max_chunks + c]));
+  store_g2j(BP[g], acc);
 }
 
-// lane g: side, window w, group q over buckets lo..hi (1-based digits):
-//   G = sum_{b=lo..hi} (b - lo + 1) B_b + (lo - 1) sum_{b=lo..hi} B_b = sum_b b B_b
-DG_KERNEL void __launch_bounds__(64) k_msm_groups(uint32_t nsides, const G2JStore* B, G2JStore* G) {
+// Bucket aggregation by bit slices: sum_b b B_b = sum_k 2^k S_k with S_k = sum of the buckets whose
+// digit b has bit k set (128 of the 255).  Level 1: lane (side, w, k, c < 16) sums 8 of those buckets.
+DG_KERNEL void __launch_bounds__(128) k_msm_slices(uint32_t nsides, const G2JStore* B, G2JStore* P1) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t per_side = MSM_WIN * MSM_NGROUP;
-  if (g >= per_side * nsides) return;
-  uint32_t side = g / per_side, w = (g % per_side) / MSM_NGROUP, q = g % MSM_NGROUP;
-  uint32_t lo = 1 + q * MSM_GROUP, hi = lo + MSM_GROUP - 1;
+  if (g >= nsides * MSM_WIN * MSM_C * 16) return;
+  uint32_t c = g % 16, k = (g / 16) % MSM_C, w = (g / (16 * MSM_C)) % MSM_WIN, side = g / (16 * MSM_C * MSM_WIN);
   const G2JStore* Bw = B + side * MSM_NBK + w * MSM_NB;
-  G2J run = jac_infinity<Fp2>(), acc = jac_infinity<Fp2>();
-  for (uint32_t b = hi; b >= lo; --b) {
-    run = jac_add(run, load_g2j(Bw[b]));
-    acc = jac_add(acc, run);
+  G2J acc = jac_infinity<Fp2>();
+  for (uint32_t i = 8 * c; i < 8 * c + 8; ++i) {
+    // i-th digit in 0..255 with bit k set: insert a 1 at bit k of i
+    uint32_t b = ((i >> k) << (k + 1)) | (1u << k) | (i & ((1u << k) - 1));
+    acc = jac_add(acc, load_g2j(Bw[b]));
   }
-  if (lo > 1) acc = jac_add(acc, jac_mul_small(run, lo - 1));
-  store_g2j(G[g], acc);
+  store_g2j(P1[g], acc);
 }
 
-// lane g: side, window w: S_w = 2^(8w) * sum_q G[side][w][q]; then lane (side, 0) sums the 8 windows
-DG_KERNEL void __launch_bounds__(64) k_msm_windows(uint32_t nsides, const G2JStore* G, G2JStore* out) {
-  __shared__ G2JStore S[2 * MSM_WIN];
-  uint32_t g = threadIdx.x;
-  if (g < MSM_WIN * nsides) {
-    uint32_t side = g / MSM_WIN, w = g % MSM_WIN;
-    const G2JStore* Gw = G + side * MSM_WIN * MSM_NGROUP + w * MSM_NGROUP;
-    G2J acc = load_g2j(Gw[0]);
-    for (uint32_t q = 1; q < MSM_NGROUP; ++q) acc = jac_add(acc, load_g2j(Gw[q]));
-    for (uint32_t k = 0; k < MSM_C * w; ++k) acc = jac_dbl(acc);
-    store_g2j(S[g], acc);
+// one 128-lane workgroup per (side, window): W_w = sum_k 2^k S_{w,k} (Horner with cooperative doublings
+// and additions, coop.h), then 2^(8w) W_w
+DG_KERNEL void __launch_bounds__(128) k_msm_horner_coop(const G2JStore* S, G2JStore* Wout) {
+  __shared__ CoG2Tmp tmp;
+  __shared__ CoG2 acc, nxt;
+  const uint32_t sw = blockIdx.x, w = sw % MSM_WIN;
+  const G2JStore* Sw = S + sw * MSM_C;
+  CO_SERIAL({
+    G2J a = load_g2j(Sw[MSM_C - 1]);
+    acc = CoG2{a.x, a.y, a.z};
+  });
+  for (int k = MSM_C - 2; k >= 0; --k) {
+    co_g2_dbl(&acc, &tmp);
+    CO_SERIAL({
+      G2J a = load_g2j(Sw[k]);
+      nxt = CoG2{a.x, a.y, a.z};
+    });
+    co_g2_add(&acc, &acc, &nxt, &tmp);
   }
-  __syncthreads();
-  if (g < nsides) {
-    G2J acc = load_g2j(S[g * MSM_WIN]);
-    for (uint32_t w = 1; w < MSM_WIN; ++w) acc = jac_add(acc, load_g2j(S[g * MSM_WIN + w]));
-    store_g2j(out[g], acc);
-  }
+  for (uint32_t d = 0; d < MSM_C * w; ++d) co_g2_dbl(&acc, &tmp);
+  CO_SERIAL(store_g2j(Wout[sw], G2J{acc.x, acc.y, acc.z}));
 }
+
+// one 128-lane workgroup per side: out[side] = sum_w W[side][w]
+DG_KERNEL void __launch_bounds__(128) k_msm_final_coop(const G2JStore* W, G2JStore* out) {
+  __shared__ CoG2Tmp tmp;
+  __shared__ CoG2 acc, nxt;
+  const uint32_t side = blockIdx.x;
+  CO_SERIAL({
+    G2J a = load_g2j(W[side * MSM_WIN]);
+    acc = CoG2{a.x, a.y, a.z};
+  });
+  for (uint32_t w = 1; w < MSM_WIN; ++w) {
+    CO_SERIAL({
+      G2J a = load_g2j(W[side * MSM_WIN + w]);
+      nxt = CoG2{a.x, a.y, a.z};
+    });
+    co_g2_add(&acc, &acc, &nxt, &tmp);
+  }
+  CO_SERIAL(store_g2j(out[side], G2J{acc.x, acc.y, acc.z}));
+}
+
 #endif
 
 }  // namespace dg
