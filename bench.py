@@ -120,6 +120,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=100000, help="rounds per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--async", dest="use_async", action="store_true",
+                    help="enqueue the steps through dg_verify_beacons_dev_async (batches may overlap)")
     ap.add_argument("--recover-rounds", type=int, default=20000, help="0 disables the Recover line")
     args = ap.parse_args()
 
@@ -163,20 +165,48 @@ def main():
     d_ps = torch.from_numpy(psb).to(dev)
     d_off = torch.from_numpy(off.astype(np.int32)).to(dev)
     d_sig = torch.from_numpy(np.ascontiguousarray(sigs)).to(dev)
-    d_st = torch.full((n,), 99, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # one status buffer per in-flight batch (the library rotates over 3 workspace sets)
+    nbuf = 3
+    d_sts = [torch.full((n,), 99, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+    gathered = [None] * nbuf
+    side = torch.cuda.Stream(dev)
     pkb = ctypes.c_char_p(pk)
+    counter = [0]
 
     def step(seed):
-        L.check(lib.dg_verify_beacons_dev(pkb, n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off), L.ptr(d_sig),
-                                          L.ptr(d_st), seed, ctypes.c_void_p(stream.cuda_stream)))
-        return shard.allgather_verdicts(d_st, world)
+        """Enqueue one batch (asynchronously: consecutive batches overlap) and the all-gather of its verdict
+        bitmap on a side stream that waits for the batch; returns the gathered bitmap tensor."""
+        i = counter[0] % nbuf
+        counter[0] += 1
+        if gathered[i] is not None:
+            gathered[i][1].synchronize()  # the all-gather that read this status buffer has finished
+        d_st = d_sts[i]
+        if not args.use_async:
+            L.check(lib.dg_verify_beacons_dev(pkb, n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off),
+                                              L.ptr(d_sig), L.ptr(d_st), seed, None))
+            side.wait_stream(torch.cuda.current_stream(dev))
+        else:
+            L.check(lib.dg_verify_beacons_dev_async(pkb, n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off),
+                                                    L.ptr(d_sig), L.ptr(d_st), seed, None,
+                                                    ctypes.c_void_p(side.cuda_stream)))
+        with torch.cuda.stream(side):
+            bits = shard.allgather_verdicts(d_st, world)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        gathered[i] = (bits, ev)
+        return bits
+
+    def drain():
+        L.check(lib.dg_wait_all())
+        torch.cuda.synchronize()
 
     for w in range(args.warmup):
         step(1000 + w)
-    torch.cuda.synchronize()
+    drain()
     bitmap = step(7)
-    assert int(d_st.max().item()) == 0, "valid chain rounds rejected"
+    drain()
+    used = min(counter[0], nbuf)
+    assert all(int(d.max().item()) == 0 for d in d_sts[:used]), "valid chain rounds rejected"
     assert bitmap.sum().item() == 0
     if world > 1:
         dist.barrier()
@@ -185,12 +215,13 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        step(17 + s)
-    torch.cuda.synchronize()
+    bits = [step(17 + s) for s in range(args.steps)]
+    drain()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    used = min(counter[0], nbuf)
+    assert all(int(b.sum().item()) == 0 for b in bits) and all(int(d.max().item()) == 0 for d in d_sts[:used])
     kt = L.timings()
     L.check(lib.dg_set_timing(0))
     t = torch.tensor([dt], dtype=torch.float64, device=dev)

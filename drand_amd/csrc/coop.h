@@ -102,11 +102,11 @@ __device__ __forceinline__ void co_phase(const CoM2 (&j2)[N2], const CoM1 (&j1)[
   if (t < 3 * N2) {
     int q = t / 3, m = t - 3 * q;
     CoM2 j = co_pick(j2, q);
-    tmp[t] = fp_mul(co_kara_operand(*j.a, m), co_kara_operand(*j.b, m));
+    tmp[t] = fp_mul_inl(co_kara_operand(*j.a, m), co_kara_operand(*j.b, m));
   } else if (t < 3 * N2 + 2 * N1) {
     int u = t - 3 * N2, q = u / 2, m = u - 2 * q;
     CoM1 j = co_pick(j1, q);
-    tmp[t] = fp_mul(m ? j.a->c1 : j.a->c0, *j.b);
+    tmp[t] = fp_mul_inl(m ? j.a->c1 : j.a->c0, *j.b);
   }
   __syncthreads();
   if (t < N2) {
@@ -126,7 +126,7 @@ __device__ __forceinline__ void co_phase(const CoM2 (&j2)[N2], Fp* tmp) {
   if (t < 3 * N2) {
     int q = t / 3, m = t - 3 * q;
     CoM2 j = co_pick(j2, q);
-    tmp[t] = fp_mul(co_kara_operand(*j.a, m), co_kara_operand(*j.b, m));
+    tmp[t] = fp_mul_inl(co_kara_operand(*j.a, m), co_kara_operand(*j.b, m));
   }
   __syncthreads();
   if (t < N2) {
@@ -156,7 +156,7 @@ __device__ __forceinline__ void co_fp12_mul(Fp12W* dst, const Fp12W* a, const Fp
   const int t = threadIdx.x;
   if (t < 108) {
     int q = t / 3, m = t - 3 * q;
-    s->tmp[t] = fp_mul(co_kara_operand(a->e[q / 6], m), co_kara_operand(b->e[q % 6], m));
+    s->tmp[t] = fp_mul_inl(co_kara_operand(a->e[q / 6], m), co_kara_operand(b->e[q % 6], m));
   }
   __syncthreads();
   if (t < 36) s->prod[t] = co_kara_combine(s->tmp + 3 * t);
@@ -180,7 +180,7 @@ __device__ __forceinline__ void co_fp12_mul_line(Fp12W* dst, const Fp12W* a, con
   if (t < 54) {
     int q = t / 3, m = t - 3 * q;  // q = 3 i + jj, line slot {0, 2, 3}[jj]
     int i = q / 3, jj = q - 3 * i;
-    s->tmp[t] = fp_mul(co_kara_operand(a->e[i], m), co_kara_operand(L->e[jj == 0 ? 0 : jj + 1], m));
+    s->tmp[t] = fp_mul_inl(co_kara_operand(a->e[i], m), co_kara_operand(L->e[jj == 0 ? 0 : jj + 1], m));
   }
   __syncthreads();
   if (t < 18) s->prod[t] = co_kara_combine(s->tmp + 3 * t);
@@ -214,7 +214,7 @@ __device__ __forceinline__ void co_fp12_frob(Fp12W* dst, const Fp12W* a, CoGT* s
   const int t = threadIdx.x;
   if (t < 18) {
     int q = t / 3, m = t - 3 * q;
-    s->tmp[t] = fp_mul(co_kara_operand(fp2_conj(a->e[q]), m), co_kara_operand(s->gamma[q], m));
+    s->tmp[t] = fp_mul_inl(co_kara_operand(fp2_conj(a->e[q]), m), co_kara_operand(s->gamma[q], m));
   }
   __syncthreads();
   if (t < 6) dst->e[t] = co_kara_combine(s->tmp + 3 * t);

@@ -26,19 +26,30 @@ struct Timing {
   int launches;
 };
 
+// A workspace set: its own stream, grow-only device buffers and completion event.  Batches enqueued
+// through the asynchronous entry point rotate over kSets sets, so the latency-bound tail of one batch
+// (Miller loops, final exponentiation: a few workgroups) overlaps the throughput-bound head of the next.
+constexpr int kSets = 3;
+struct Set {
+  hipStream_t stream = nullptr;
+  std::vector<void*> pool;  // indexed by Slot
+  std::vector<size_t> pool_size;
+  hipEvent_t done = nullptr;
+  bool busy = false;
+  uint8_t pk_bytes[48];
+  bool pk_valid = false;
+};
+
 struct Ctx {
   int device = -1;
   bool ready = false;
-  hipStream_t stream = nullptr;
-  std::vector<void*> pool;  // grow-only device allocations, indexed by slot
-  std::vector<size_t> pool_size;
+  Set sets[kSets];
+  int cur = 0, next = 0;
   bool timing = false;
   std::vector<Timing> timings;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
   std::vector<const char*> pending_names;
   std::vector<hipEvent_t> free_events;
-  uint8_t pk_bytes[48];
-  bool pk_valid = false;
 };
 
 std::mutex g_mu;
@@ -64,8 +75,10 @@ enum Slot {
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_COUNT
 };
 
+Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
+
 int ws(Slot s, size_t bytes, void** out) {
-  Ctx& c = g_ctx;
+  Set& c = cur_set();
   if (c.pool.size() < S_COUNT) {
     c.pool.assign(S_COUNT, nullptr);
     c.pool_size.assign(S_COUNT, 0);
@@ -80,6 +93,21 @@ int ws(Slot s, size_t bytes, void** out) {
     c.pool_size[s] = sz;
   }
   *out = c.pool[s];
+  return 0;
+}
+
+// Take the next workspace set (waiting for the batch still using it) and make it current.
+int acquire_set(hipStream_t* st) {
+  Ctx& c = g_ctx;
+  int i = c.next;
+  c.next = (c.next + 1) % kSets;
+  Set& s = c.sets[i];
+  if (s.busy) {
+    HIPCHK(hipEventSynchronize(s.done));
+    s.busy = false;
+  }
+  c.cur = i;
+  *st = s.stream;
   return 0;
 }
 
@@ -280,25 +308,20 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   }
   RET(launch("k_pair_miller_coop", k_pair_miller_coop, 128 * (b.nslots + 1), 128, st, b.nslots, seed, b.keys, K, T, f));
   RET(launch("k_final_coop", k_final_coop, 128, 128, st, b.nslots + 1, (const Fp12*)f, flag));
-  // isolated items present?
+  // isolated items present?  The per-item pass decides on the device (no host round trip), so a batch
+  // is one stream-ordered sequence of launches.
   HIPCHK(hipMemsetAsync(flag + 1, 0, 4, st));
   RET(launch("k_any", k_any, N, 256, st, N, (const uint8_t*)iso, flag + 1));
-  uint32_t h_flag[2] = {0, 0};
-  HIPCHK(hipMemcpyAsync(h_flag, flag, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  bool batch_ok = h_flag[0] != 0, any_iso = h_flag[1] != 0;
-  if (!batch_ok || any_iso) {
-    G2AStore* H;
-    RET(wsT(S_H, b.R, &H));
-    RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, b.Q, H));
-    RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, batch_ok ? 0u : 1u, b.keys, b.item_slot,
-               (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status));
-  }
+  G2AStore* H;
+  RET(wsT(S_H, b.R, &H));
+  RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, (const uint32_t*)flag, b.Q, H));
+  RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
+             (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status));
   return 0;
 }
 
 int decode_key(const uint8_t* pk48_host, hipStream_t st, G1AStore** keys, uint8_t** key_status) {
-  Ctx& c = g_ctx;
+  Set& c = cur_set();
   RET(wsT(S_PK1, 1, keys));
   RET(wsT(S_PK1ST, 1, key_status));
   if (c.pk_valid && memcmp(c.pk_bytes, pk48_host, 48) == 0) return 0;
@@ -392,7 +415,10 @@ int dg_init(int device) {
   if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
     return fail(DG_E_NODEV, std::string("not a gfx950 device: ") + prop.gcnArchName);
   HIPCHK(hipSetDevice(device));
-  if (!g_ctx.stream) HIPCHK(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking));
+  for (Set& x : g_ctx.sets) {
+    if (!x.stream) HIPCHK(hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking));
+    if (!x.done) HIPCHK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
+  }
   g_ctx.device = device;
   g_ctx.ready = true;
   return 0;
@@ -401,13 +427,19 @@ int dg_init(int device) {
 void dg_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!g_ctx.ready) return;
-  for (void* p : g_ctx.pool)
-    if (p) hipFree(p);
-  g_ctx.pool.clear();
-  g_ctx.pool_size.clear();
-  g_ctx.pk_valid = false;
-  if (g_ctx.stream) hipStreamDestroy(g_ctx.stream);
-  g_ctx.stream = nullptr;
+  for (Set& x : g_ctx.sets) {
+    if (x.stream) (void)hipStreamSynchronize(x.stream);
+    for (void* p : x.pool)
+      if (p) (void)hipFree(p);
+    x.pool.clear();
+    x.pool_size.clear();
+    x.pk_valid = false;
+    x.busy = false;
+    if (x.stream) (void)hipStreamDestroy(x.stream);
+    if (x.done) (void)hipEventDestroy(x.done);
+    x.stream = nullptr;
+    x.done = nullptr;
+  }
   g_ctx.ready = false;
 }
 
@@ -440,7 +472,8 @@ int dg_hash_to_g2(size_t n, const uint8_t* msgs, size_t msg_len, const uint8_t* 
   RET(require_ready());
   if (n == 0) return 0;
   if (!msgs || !dst || !out96 || dst_len > 255 || n > 0xffffffffu) return fail(DG_E_ARG, "bad arguments");
-  hipStream_t st = g_ctx.stream;
+  hipStream_t st;
+  RET(acquire_set(&st));
   const uint8_t *d_msgs, *d_dst;
   RET(upload(S_MSGS, msgs, n * msg_len, (uint8_t**)&d_msgs, st));
   RET(upload(S_DST, dst, dst_len, (uint8_t**)&d_dst, st));
@@ -461,7 +494,8 @@ int dg_sign(size_t n, const uint8_t* scalars32, const uint16_t* index, const uin
   if (n == 0) return 0;
   if (!scalars32 || !msgs || !out) return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(n));
-  hipStream_t st = g_ctx.stream;
+  hipStream_t st;
+  RET(acquire_set(&st));
   uint8_t *d_sc, *d_m, *d_dst, *d_out;
   uint16_t* d_idx = nullptr;
   RET(upload(S_IN0, scalars32, n * 32, &d_sc, st));
@@ -485,7 +519,8 @@ int dg_verify(const uint8_t pk48[48], size_t n, const uint8_t* msgs, size_t msg_
   if (n == 0) return 0;
   if (!pk48 || !msgs || !sigs96 || !status) return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(n));
-  hipStream_t st = g_ctx.stream;
+  hipStream_t st;
+  RET(acquire_set(&st));
   uint8_t *d_msgs, *d_sigs, *d_st;
   RET(upload(S_MSGS, msgs, n * msg_len, &d_msgs, st));
   RET(upload(S_IN0, sigs96, n * 96, &d_sigs, st));
@@ -513,6 +548,36 @@ static int upload_beacons(size_t n, const uint64_t* prev_round, const uint64_t* 
   return 0;
 }
 
+// Enqueue one device-resident beacon batch on the next workspace set without waiting for it.
+static int enqueue_beacons_dev(const uint8_t* pk48_host, size_t n, const uint64_t* d_pr, const uint64_t* d_r,
+                               const uint8_t* d_ps, const uint32_t* d_off, const uint8_t* d_sigs, uint8_t* d_status,
+                               uint64_t seed, hipStream_t in_stream, hipStream_t done_stream) {
+  hipStream_t st;
+  RET(acquire_set(&st));
+  Set& set = cur_set();
+  if (in_stream) {
+    HIPCHK(hipEventRecord(set.done, in_stream));  // inputs ready
+    HIPCHK(hipStreamWaitEvent(st, set.done, 0));
+  }
+  uint8_t* d_msgs;
+  RET(beacons_to_msgs(n, d_pr, d_r, d_ps, d_off, &d_msgs, st));
+  RET(verify_single_key(pk48_host, (uint32_t)n, d_msgs, 32, d_sigs, d_status, fresh_seed(seed), st));
+  HIPCHK(hipEventRecord(set.done, st));
+  set.busy = true;
+  if (done_stream) HIPCHK(hipStreamWaitEvent(done_stream, set.done, 0));
+  return 0;
+}
+
+static int wait_all() {
+  for (Set& x : g_ctx.sets)
+    if (x.busy) {
+      HIPCHK(hipEventSynchronize(x.done));
+      x.busy = false;
+    }
+  if (g_ctx.timing) collect_timings();
+  return 0;
+}
+
 int dg_verify_beacons(const uint8_t pk48[48], size_t n, const uint64_t* prev_round, const uint64_t* round,
                       const uint8_t* prev_sigs, const uint32_t* prev_sig_off, const uint8_t* sigs96, uint8_t* status,
                       uint64_t seed) {
@@ -522,7 +587,8 @@ int dg_verify_beacons(const uint8_t pk48[48], size_t n, const uint64_t* prev_rou
   if (!pk48 || !prev_round || !round || !prev_sigs || !prev_sig_off || !sigs96 || !status)
     return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(n));
-  hipStream_t st = g_ctx.stream;
+  hipStream_t st;
+  RET(acquire_set(&st));
   uint64_t *d_pr, *d_r;
   uint8_t *d_ps, *d_sigs, *d_msgs, *d_st;
   uint32_t* d_off;
@@ -546,13 +612,30 @@ int dg_verify_beacons_dev(const uint8_t* pk48_host, size_t n, const uint64_t* d_
   if (!pk48_host || !d_prev_round || !d_round || !d_prev_sigs || !d_prev_sig_off || !d_sigs96 || !d_status)
     return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(n));
-  hipStream_t st = stream ? (hipStream_t)stream : g_ctx.stream;
-  uint8_t* d_msgs;
-  RET(beacons_to_msgs(n, d_prev_round, d_round, d_prev_sigs, d_prev_sig_off, &d_msgs, st));
-  RET(verify_single_key(pk48_host, (uint32_t)n, d_msgs, 32, d_sigs96, d_status, fresh_seed(seed), st));
-  HIPCHK(hipStreamSynchronize(st));
-  if (g_ctx.timing) collect_timings();
+  RET(enqueue_beacons_dev(pk48_host, n, d_prev_round, d_round, d_prev_sigs, d_prev_sig_off, d_sigs96, d_status, seed,
+                          (hipStream_t)stream, nullptr));
+  RET(wait_all());
   return 0;
+}
+
+int dg_verify_beacons_dev_async(const uint8_t* pk48_host, size_t n, const uint64_t* d_prev_round,
+                                const uint64_t* d_round, const uint8_t* d_prev_sigs, const uint32_t* d_prev_sig_off,
+                                const uint8_t* d_sigs96, uint8_t* d_status, uint64_t seed, void* in_stream,
+                                void* done_stream) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  if (n == 0) return 0;
+  if (!pk48_host || !d_prev_round || !d_round || !d_prev_sigs || !d_prev_sig_off || !d_sigs96 || !d_status)
+    return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(n));
+  return enqueue_beacons_dev(pk48_host, n, d_prev_round, d_round, d_prev_sigs, d_prev_sig_off, d_sigs96, d_status, seed,
+                             (hipStream_t)in_stream, (hipStream_t)done_stream);
+}
+
+int dg_wait_all(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  return wait_all();
 }
 
 int dg_check_links(uint64_t cur_round, const uint8_t* cur_sig, size_t cur_sig_len, size_t n, const uint64_t* prev_round,
@@ -564,7 +647,8 @@ int dg_check_links(uint64_t cur_round, const uint8_t* cur_sig, size_t cur_sig_le
   if (!cur_sig || !prev_round || !round || !prev_sigs || !prev_sig_off || !sigs96 || !link_status)
     return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(n));
-  hipStream_t st = g_ctx.stream;
+  hipStream_t st;
+  RET(acquire_set(&st));
   uint64_t *d_pr, *d_r;
   uint8_t *d_ps, *d_sigs, *d_cur, *d_out;
   uint32_t* d_off;
@@ -587,7 +671,8 @@ int dg_beacon_messages(size_t n, const uint64_t* prev_round, const uint64_t* rou
   if (n == 0) return 0;
   if (!prev_round || !round || !prev_sigs || !prev_sig_off || !out32) return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(n));
-  hipStream_t st = g_ctx.stream;
+  hipStream_t st;
+  RET(acquire_set(&st));
   uint64_t *d_pr, *d_r;
   uint8_t *d_ps, *d_msgs;
   uint32_t* d_off;
@@ -604,7 +689,8 @@ int dg_randomness(size_t n, const uint8_t* sigs96, uint8_t* out32) {
   if (n == 0) return 0;
   if (!sigs96 || !out32) return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(n));
-  hipStream_t st = g_ctx.stream;
+  hipStream_t st;
+  RET(acquire_set(&st));
   uint8_t *d_sigs, *d_out;
   RET(upload(S_IN0, sigs96, n * 96, &d_sigs, st));
   RET(wsT(S_OUT0, 32 * n, &d_out));
@@ -620,7 +706,8 @@ int dg_pubpoly_eval(const uint8_t* commits48, uint32_t t, size_t n, const uint32
   if (n == 0) return 0;
   if (!commits48 || t == 0 || !index || !out48) return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(n));
-  hipStream_t st = g_ctx.stream;
+  hipStream_t st;
+  RET(acquire_set(&st));
   uint8_t *d_c, *d_cst, *d_out, *d_kst;
   uint32_t* d_idx;
   G1AStore *cA, *keys;
@@ -650,7 +737,8 @@ int dg_verify_partials(const uint8_t* commits48, uint32_t t, size_t rounds, cons
   if (rounds == 0 || k == 0) return 0;
   if (!commits48 || t == 0 || !msgs || !partials98 || !status) return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(rounds * (size_t)k));
-  hipStream_t st = g_ctx.stream;
+  hipStream_t st;
+  RET(acquire_set(&st));
   uint8_t *d_st, *d_p;
   G2AStore* d_S;
   RET(verify_partials_dev(commits48, t, (uint32_t)rounds, msgs, (uint32_t)msg_len, k, partials98, fresh_seed(seed), st,
@@ -671,7 +759,8 @@ int dg_recover(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t ro
   if (!commits48 || t == 0 || k == 0 || !msgs || !partials98 || !out_sig96 || !round_status || !share_status)
     return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(rounds * (size_t)(k > t ? k : t)));
-  hipStream_t st = g_ctx.stream;
+  hipStream_t st;
+  RET(acquire_set(&st));
   const uint32_t R = (uint32_t)rounds;
   uint8_t *d_st, *d_p, *d_rst, *d_sst, *d_out;
   G2AStore* d_S;

@@ -226,6 +226,24 @@ DGF Fp fp_sqr(const Fp& a) {
 }
 #endif
 
+// Inlined variants for the innermost loops (exponentiation chains, the per-lane products of the
+// cooperative phases in coop.h): no call, operands stay in registers.
+#if defined(DG_FP_ASM)
+__device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) {
+  Fp r;
+  fp_mont_mul_asm(r.l, a.l, b.l, P_LIMBS, P_INV32);
+  return fp_reduce_once(r);
+}
+__device__ __forceinline__ Fp fp_sqr_inl(const Fp& a) {
+  Fp r;
+  fp_mont_sqr_asm(r.l, a.l, P_LIMBS, P_INV32);
+  return fp_reduce_once(r);
+}
+#else
+DGI Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_mul(a, b); }
+DGI Fp fp_sqr_inl(const Fp& a) { return fp_sqr(a); }
+#endif
+
 // plain integer (little-endian limbs) -> Montgomery
 DGI Fp fp_to_mont(const Fp& a) { return fp_mul(a, fp_const(FP_R2)); }
 DGI Fp fp_from_mont(const Fp& a) {
@@ -252,12 +270,12 @@ DGI Fp fp_pow_sched(const Fp& x, int first, const int8_t (&steps)[NSTEPS][2]) {
   for (int s = 0; s < NSTEPS; ++s) {
     int k = steps[s][0];
     int idx = steps[s][1];
-    for (int j = 0; j < k; ++j) acc = fp_sqr(acc);
+    for (int j = 0; j < k; ++j) acc = fp_sqr_inl(acc);
     if (idx >= 0) {
       Fp m = fp_sel(idx == 1, t0, t1);
       m = fp_sel(idx == 2, m, t2);
       m = fp_sel(idx == 3, m, t3);
-      acc = fp_mul(acc, m);
+      acc = fp_mul_inl(acc, m);
     }
   }
   return acc;

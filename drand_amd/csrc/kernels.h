@@ -347,21 +347,22 @@ DG_KERNEL void __launch_bounds__(128) k_final_coop(uint32_t npairs, const Fp12* 
 }
 
 // H_r = h_eff(Q_r), affine (individual checks)
-DG_KERNEL void __launch_bounds__(128) k_clear_rounds(uint32_t R, const G2JStore* Q, G2AStore* H) {
+// (skipped when the batch verified and nothing was isolated: flag[0] = batch ok, flag[1] = any isolated)
+DG_KERNEL void __launch_bounds__(128) k_clear_rounds(uint32_t R, const uint32_t* flag, const G2JStore* Q, G2AStore* H) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
+  if (r >= R || (flag[0] && !flag[1])) return;
   store_g2a(H[r], g2_to_aff(g2_clear_cofactor(load_g2j(Q[r]))));
 }
 
-// individual bls.Verify of item i: e(X_slot, H_{i/k}) == e(g1, S_i).  all = 1: every decoded item
-// (after a failed batch); all = 0: only the isolated ones.
-DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, uint32_t all, const G1AStore* keys,
+// individual bls.Verify of item i: e(X_slot, H_{i/k}) == e(g1, S_i): every decoded item after a failed
+// batch (flag[0] == 0), only the isolated ones after a passed batch
+DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
                                                     const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
                                                     const uint8_t* isolate, uint8_t* status) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (status[i] != DG_ST_OK_) return;
-  if (!all && !isolate[i]) return;
+  if (flag[0] && !isolate[i]) return;
   G1A key = load_g1a(keys[item_slot ? item_slot[i] : 0u]);
   G2A h = load_g2a(H[i / k]);
   G2A s = load_g2a(S[i]);

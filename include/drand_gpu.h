@@ -109,6 +109,21 @@ int dg_verify_beacons_dev(const uint8_t* pk48_host, size_t n, const uint64_t* d_
                           const uint8_t* d_prev_sigs, const uint32_t* d_prev_sig_off, const uint8_t* d_sigs96,
                           uint8_t* d_status, uint64_t seed, void* stream);
 
+/* Asynchronous device-resident VerifyBeacon batch (the streaming form of syncFrom's catch-up,
+ * beacon/beacon.go:529-607): enqueues the batch on the next of the library's rotating workspace sets and
+ * returns without waiting, so consecutive batches overlap (one batch's Miller loops and final
+ * exponentiation -- a few workgroups -- run beside the next batch's hashing and decoding).  in_stream
+ * (may be NULL): the inputs are ready when this stream reaches the call; done_stream (may be NULL):
+ * made to wait for the batch's completion (e.g. before an all-gather of the statuses).  d_status is
+ * final after dg_wait_all() or once done_stream passes that point.  The device buffers must stay
+ * untouched until then. */
+int dg_verify_beacons_dev_async(const uint8_t* pk48_host, size_t n, const uint64_t* d_prev_round,
+                                const uint64_t* d_round, const uint8_t* d_prev_sigs, const uint32_t* d_prev_sig_off,
+                                const uint8_t* d_sigs96, uint8_t* d_status, uint64_t seed, void* in_stream,
+                                void* done_stream);
+/* Wait for every batch enqueued by the asynchronous entry points. */
+int dg_wait_all(void);
+
 /* Per-kernel HIP-event timing on the launch stream (off by default); resets the accumulated table. */
 int dg_set_timing(int on);
 
