@@ -36,8 +36,6 @@ struct Set {
   std::vector<size_t> pool_size;
   hipEvent_t done = nullptr;
   bool busy = false;
-  uint8_t pk_bytes[48];
-  bool pk_valid = false;
 };
 
 struct Ctx {
@@ -50,6 +48,13 @@ struct Ctx {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
   std::vector<const char*> pending_names;
   std::vector<hipEvent_t> free_events;
+  // decoded group key of the single-key paths, shared by all sets (kyber keeps it decoded as well)
+  G1AStore* pk_dev = nullptr;
+  uint8_t* pk_status = nullptr;
+  uint8_t* pk_raw = nullptr;
+  hipEvent_t pk_ready = nullptr;
+  uint8_t pk_bytes[48];
+  bool pk_valid = false;
 };
 
 std::mutex g_mu;
@@ -85,7 +90,6 @@ int ws(Slot s, size_t bytes, void** out) {
   }
   if (bytes == 0) bytes = 16;
   if (c.pool_size[s] < bytes) {
-    if (s == S_PK1 || s == S_PK1ST) c.pk_valid = false;
     if (c.pool[s]) HIPCHK(hipFree(c.pool[s]));
     c.pool[s] = nullptr;
     size_t sz = bytes + bytes / 4;
@@ -320,14 +324,31 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   return 0;
 }
 
+// The group key of the single-key paths, decoded once per distinct key and shared by the workspace sets:
+// decompression + [r]P subgroup check is a ~1.5k-Fp-multiplication single-lane job.
 int decode_key(const uint8_t* pk48_host, hipStream_t st, G1AStore** keys, uint8_t** key_status) {
-  Set& c = cur_set();
-  RET(wsT(S_PK1, 1, keys));
-  RET(wsT(S_PK1ST, 1, key_status));
-  if (c.pk_valid && memcmp(c.pk_bytes, pk48_host, 48) == 0) return 0;
-  uint8_t* d_pk;
-  RET(upload(S_PK1RAW, pk48_host, 48, &d_pk, st));
-  RET(launch("k_decode_g1", k_decode_g1, 1, 64, st, 1u, (const uint8_t*)d_pk, *keys, *key_status));
+  Ctx& c = g_ctx;
+  if (!c.pk_dev) {
+    HIPCHK(hipMalloc(&c.pk_dev, sizeof(G1AStore)));
+    HIPCHK(hipMalloc(&c.pk_status, 16));
+    HIPCHK(hipMalloc(&c.pk_raw, 48));
+    HIPCHK(hipEventCreateWithFlags(&c.pk_ready, hipEventDisableTiming));
+  }
+  *keys = c.pk_dev;
+  *key_status = c.pk_status;
+  if (c.pk_valid && memcmp(c.pk_bytes, pk48_host, 48) == 0) {
+    HIPCHK(hipStreamWaitEvent(st, c.pk_ready, 0));
+    return 0;
+  }
+  // a previous key may still be in use by batches in flight on other sets
+  for (Set& x : c.sets)
+    if (x.busy) {
+      HIPCHK(hipEventSynchronize(x.done));
+      x.busy = false;
+    }
+  HIPCHK(hipMemcpyAsync(c.pk_raw, pk48_host, 48, hipMemcpyHostToDevice, st));
+  RET(launch("k_decode_g1", k_decode_g1, 1, 64, st, 1u, (const uint8_t*)c.pk_raw, c.pk_dev, c.pk_status));
+  HIPCHK(hipEventRecord(c.pk_ready, st));
   memcpy(c.pk_bytes, pk48_host, 48);
   c.pk_valid = true;
   return 0;
@@ -433,13 +454,21 @@ void dg_shutdown(void) {
       if (p) (void)hipFree(p);
     x.pool.clear();
     x.pool_size.clear();
-    x.pk_valid = false;
     x.busy = false;
     if (x.stream) (void)hipStreamDestroy(x.stream);
     if (x.done) (void)hipEventDestroy(x.done);
     x.stream = nullptr;
     x.done = nullptr;
   }
+  if (g_ctx.pk_dev) (void)hipFree(g_ctx.pk_dev);
+  if (g_ctx.pk_status) (void)hipFree(g_ctx.pk_status);
+  if (g_ctx.pk_raw) (void)hipFree(g_ctx.pk_raw);
+  if (g_ctx.pk_ready) (void)hipEventDestroy(g_ctx.pk_ready);
+  g_ctx.pk_dev = nullptr;
+  g_ctx.pk_status = nullptr;
+  g_ctx.pk_raw = nullptr;
+  g_ctx.pk_ready = nullptr;
+  g_ctx.pk_valid = false;
   g_ctx.ready = false;
 }
 

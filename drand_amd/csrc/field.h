@@ -14,7 +14,7 @@
 #if defined(__HIP__)
 #include <hip/hip_runtime.h>
 #define DGI __host__ __device__ __forceinline__
-#define DGN __host__ __device__ __noinline__
+#define DGN static __host__ __device__ __noinline__
 #else
 #define DGI static inline
 #define DGN static

@@ -7,6 +7,10 @@
 #include "fr.h"
 #include "coop.h"
 
+#ifndef DG_TU_HOT
+#define DG_TU_HOT 0  // 1 in kernels_hot.hip: only the hot kernels are defined there (DESIGN.md §code generation)
+#endif
+
 namespace dg {
 
 // per-item status codes (mirror include/drand_gpu.h DG_ST_*)
@@ -65,6 +69,7 @@ DGI uint64_t rlc_coeff(uint64_t seed, uint64_t i) {
 #define DG_KERNEL extern "C" __global__
 
 // A1: beacon messages
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(256) k_beacon_msgs(uint32_t n, const uint64_t* prev_round, const uint64_t* round,
                                                     const uint8_t* prev_sigs, const uint32_t* off, uint8_t* out32) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -72,8 +77,10 @@ DG_KERNEL void __launch_bounds__(256) k_beacon_msgs(uint32_t n, const uint64_t* 
   uint32_t a = off[i], b = off[i + 1];
   beacon_message(out32 + 32ull * i, prev_sigs + a, b - a, prev_round[i], round[i]);
 }
+#endif
 
 // A2: randomness
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(256) k_randomness(uint32_t n, const uint8_t* sigs96, uint8_t* out32) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -82,8 +89,10 @@ DG_KERNEL void __launch_bounds__(256) k_randomness(uint32_t n, const uint8_t* si
   sha256_update(s, sigs96 + 96ull * i, 96);
   sha256_final(s, out32 + 32ull * i);
 }
+#endif
 
 // A13: link check
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(256) k_links(uint32_t n, uint64_t cur_round, const uint8_t* cur_sig, uint32_t cur_len,
                                               const uint64_t* prev_round, const uint64_t* round,
                                               const uint8_t* prev_sigs, const uint32_t* off, const uint8_t* sigs96,
@@ -99,8 +108,10 @@ DG_KERNEL void __launch_bounds__(256) k_links(uint32_t n, uint64_t cur_round, co
     for (uint32_t k = 0; k < cl; ++k) ok = ok && prev_sigs[a + k] == cs[k];
   out[i] = ok ? 0 : 1;
 }
+#endif
 
 // A9: full hash-to-G2, compressed
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_hash_to_g2(uint32_t n, const uint8_t* msgs, uint32_t msg_len,
                                                    const uint8_t* dst, uint32_t dst_len, uint8_t* out96) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -108,16 +119,23 @@ DG_KERNEL void __launch_bounds__(128) k_hash_to_g2(uint32_t n, const uint8_t* ms
   G2J h = hash_to_g2(msgs + (size_t)msg_len * i, msg_len, dst, dst_len);
   g2_compress_aff(out96 + 96ull * i, g2_to_aff(h));
 }
+#endif
 
 // hash-to-curve without cofactor clearing (RLC path)
+#if DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_h2c_uncleared(uint32_t n, const uint8_t* msgs, uint32_t msg_len,
                                                       const uint8_t* dst, uint32_t dst_len, G2JStore* outQ) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   store_g2j(outQ[i], hash_to_g2_uncleared(msgs + (size_t)msg_len * i, msg_len, dst, dst_len));
 }
+#else
+DG_KERNEL void __launch_bounds__(128) k_h2c_uncleared(uint32_t n, const uint8_t* msgs, uint32_t msg_len,
+                                                      const uint8_t* dst, uint32_t dst_len, G2JStore* outQ);
+#endif
 
 // sigma decode + subgroup check (A10)
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_decode_sigs(uint32_t n, const uint8_t* sigs, uint32_t stride, uint32_t offset,
                                                     G2AStore* outS, uint8_t* status) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -128,8 +146,10 @@ DG_KERNEL void __launch_bounds__(128) k_decode_sigs(uint32_t n, const uint8_t* s
   store_g2a(outS[i], a);
   status[i] = ok ? DG_ST_OK_ : DG_ST_SIG_DECODE_;
 }
+#endif
 
 // G1 decode (keys, commits), with subgroup check
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(64) k_decode_g1(uint32_t n, const uint8_t* in48, G1AStore* out, uint8_t* status) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -139,6 +159,7 @@ DG_KERNEL void __launch_bounds__(64) k_decode_g1(uint32_t n, const uint8_t* in48
   store_g1a(out[i], a);
   status[i] = ok ? DG_ST_OK_ : DG_ST_PK_DECODE_;
 }
+#endif
 
 // ------------------------------------------------------------------ batch verification engine
 // Items are (round r, key slot s) pairs laid out round-major, k items per round (k = 1 for chain
@@ -167,6 +188,7 @@ DGN Jac<F> jac_mul_small(const Jac<F>& p, uint32_t k) {
 DGI uint32_t be16(const uint8_t* p) { return (uint32_t)p[0] << 8 | p[1]; }
 
 // A12: PubPoly.Eval(idx) = sum_j C_j x^j at x = idx + 1 (Horner), affine (+ compressed when out48)
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(64) k_pubpoly_eval(uint32_t n, uint32_t t, const G1AStore* commits,
                                                     const uint8_t* commit_status, const uint32_t* idx,
                                                     G1AStore* out, uint8_t* out_status, uint8_t* out48) {
@@ -185,9 +207,11 @@ DG_KERNEL void __launch_bounds__(64) k_pubpoly_eval(uint32_t n, uint32_t t, cons
   if (out_status) out_status[i] = ok ? DG_ST_OK_ : DG_ST_PK_DECODE_;
   if (out48) g1_compress_aff(out48 + 48ull * i, a);
 }
+#endif
 
 // decode sigma of every item (96 B at sigs + stride*i + offset) with the G2 subgroup check; claim the
 // item's (round, slot) cell -- a taken cell sends the item to the individual check (`isolate`)
+#if DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_decode_items(uint32_t n, uint32_t k, uint32_t nslots, const uint8_t* sigs,
                                                      uint32_t stride, uint32_t offset, const uint32_t* item_slot,
                                                      const uint8_t* key_status, G2AStore* S, uint8_t* status,
@@ -211,8 +235,15 @@ DG_KERNEL void __launch_bounds__(128) k_decode_items(uint32_t n, uint32_t k, uin
     isolate[i] = old ? 1 : 0;
   }
 }
+#else
+DG_KERNEL void __launch_bounds__(128) k_decode_items(uint32_t n, uint32_t k, uint32_t nslots, const uint8_t* sigs,
+                                                     uint32_t stride, uint32_t offset, const uint32_t* item_slot,
+                                                     const uint8_t* key_status, G2AStore* S, uint8_t* status,
+                                                     uint32_t* cell, uint8_t* isolate);
+#endif
 
 // U_i = beta_slot S_i for batch items, O otherwise
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_scale_items(uint32_t n, uint32_t nslots, uint64_t seed,
                                                     const uint32_t* item_slot, const G2AStore* S,
                                                     const uint8_t* status, const uint8_t* isolate, G2JStore* U) {
@@ -225,10 +256,12 @@ DG_KERNEL void __launch_bounds__(128) k_scale_items(uint32_t n, uint32_t nslots,
   }
   store_g2j(U[i], u);
 }
+#endif
 
 // per round r: V_r = sum_j U_{r,j} over its batch items, active[r] = (any batch item); with several
 // key slots also A_r = alpha_r Q_r (the per-key hash sums are masked by the cell map, so they are not a
 // single MSM); the alpha_r-weighted sums of V (and of Q with one key) are Pippenger MSMs (msm.h)
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_round_combine(uint32_t R, uint32_t k, uint32_t nslots, uint64_t seed,
                                                       const G2JStore* U, const uint8_t* status,
                                                       const uint8_t* isolate, const G2JStore* Q, G2JStore* V,
@@ -248,8 +281,10 @@ DG_KERNEL void __launch_bounds__(128) k_round_combine(uint32_t R, uint32_t k, ui
   active[r] = any ? 1 : 0;
   if (nslots > 1) store_g2j(A[r], any ? jac_mul_u64(load_g2j(Q[r]), rlc_alpha(seed, r)) : jac_infinity<Fp2>());
 }
+#endif
 
 // Kp[s * nchunks + c] = sum of A_r over rounds r in chunk c whose (r, s) cell holds a batch item
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_key_accum(uint32_t R, uint32_t nslots, uint32_t chunk, uint32_t nchunks,
                                                   const uint32_t* cell, const G2JStore* A, G2JStore* Kp) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -261,8 +296,10 @@ DG_KERNEL void __launch_bounds__(128) k_key_accum(uint32_t R, uint32_t nslots, u
     if (cell[(size_t)r * nslots + s]) acc = jac_add(acc, load_g2j(A[r]));
   store_g2j(Kp[g], acc);
 }
+#endif
 
 // 2-D segmented sum: out[row * ocols + j] = sum_{c in [j*chunk, (j+1)*chunk) and < cols} in[row * cols + c]
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_sum_rows(uint32_t rows, uint32_t cols, uint32_t chunk, const G2JStore* in,
                                                  G2JStore* out) {
   uint32_t ocols = (cols + chunk - 1) / chunk;
@@ -275,11 +312,13 @@ DG_KERNEL void __launch_bounds__(128) k_sum_rows(uint32_t rows, uint32_t cols, u
   for (uint32_t c = a + 1; c < b; ++c) acc = jac_add(acc, load_g2j(p[c]));
   store_g2j(out[g], acc);
 }
+#endif
 
 // Pair s on one 128-lane workgroup (coop.h): P side and Q side prepared cooperatively (for key pairs the
 // hash-side sum is cofactor-cleared here, once per key and batch), then the cooperative Miller loop.
 // Pairs: (beta_s X_s, h_eff K_s) for s < nslots, (-g1, T) for s == nslots; f[s] = 1
 // when a side is the identity.
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_pair_miller_coop(uint32_t nslots, uint64_t seed, const G1AStore* keys,
                                                          const G2JStore* K, const G2JStore* T, Fp12* f) {
   __shared__ CoGT gt;
@@ -324,8 +363,10 @@ DG_KERNEL void __launch_bounds__(128) k_pair_miller_coop(uint32_t nslots, uint64
   co_miller_loop(&F, &L, &ml, &gt);
   if (threadIdx.x < 6) ((Fp2*)&f[s])[(threadIdx.x & 1) * 3 + threadIdx.x / 2] = F.e[threadIdx.x];
 }
+#endif
 
 // product of the npairs Miller values and one final exponentiation on one 128-lane workgroup
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_final_coop(uint32_t npairs, const Fp12* f, uint32_t* ok) {
   __shared__ CoGT gt;
   __shared__ Fp12W F, G, S[7];
@@ -345,17 +386,21 @@ DG_KERNEL void __launch_bounds__(128) k_final_coop(uint32_t npairs, const Fp12* 
     *ok = one ? 1u : 0u;
   }
 }
+#endif
 
 // H_r = h_eff(Q_r), affine (individual checks)
 // (skipped when the batch verified and nothing was isolated: flag[0] = batch ok, flag[1] = any isolated)
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_clear_rounds(uint32_t R, const uint32_t* flag, const G2JStore* Q, G2AStore* H) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R || (flag[0] && !flag[1])) return;
   store_g2a(H[r], g2_to_aff(g2_clear_cofactor(load_g2j(Q[r]))));
 }
+#endif
 
 // individual bls.Verify of item i: e(X_slot, H_{i/k}) == e(g1, S_i): every decoded item after a failed
 // batch (flag[0] == 0), only the isolated ones after a passed batch
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
                                                     const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
                                                     const uint8_t* isolate, uint8_t* status) {
@@ -382,17 +427,21 @@ DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, cons
   bool good = np == 0 ? true : fp12_is_one(final_exp_cubed(miller_loop<2>(P, Qa, np)));
   status[i] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
 }
+#endif
 
 // *flag |= 1 if any byte of v[0..n) is non-zero
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(256) k_any(uint32_t n, const uint8_t* v, uint32_t* flag) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n && v[i]) atomicOr(flag, 1u);
 }
+#endif
 
 // ------------------------------------------------------------------ Recover (A6)
 // per round: the first t items (input order) that passed VerifyPartial, sorted by index, duplicates
 // collapsed (kyber xyCommit); round_status NOT_ENOUGH if fewer than t distinct remain.  share_status
 // = the verify status of every item examined, NOT_EXAMINED after the t-th collected one.
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_recover_select(uint32_t R, uint32_t k, uint32_t t, const uint8_t* partials,
                                                        const uint8_t* status, uint32_t* sel, uint32_t* selidx,
                                                        uint8_t* round_status, uint8_t* share_status) {
@@ -431,8 +480,10 @@ DG_KERNEL void __launch_bounds__(128) k_recover_select(uint32_t R, uint32_t k, u
   }
   round_status[r] = distinct >= t ? DG_ST_OK_ : DG_ST_NOT_ENOUGH_;
 }
+#endif
 
 // thread (r, m): lambda_m * S_{r, sel[m]}  (lambda over the round's t selected indices)
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(64) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
                                                      const uint32_t* selidx, const uint8_t* round_status,
                                                      const G2AStore* S, G2JStore* terms) {
@@ -447,8 +498,10 @@ DG_KERNEL void __launch_bounds__(64) k_recover_terms(uint32_t R, uint32_t k, uin
   G2J p = jac_from_aff(load_g2a(S[(size_t)r * k + sel[g]]));
   store_g2j(terms[g], jac_mul_u256(p, lam.l));
 }
+#endif
 
 // compress points (zeros where status != OK)
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_compress_g2(uint32_t n, const G2JStore* P, const uint8_t* st, uint8_t* out96) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -458,8 +511,10 @@ DG_KERNEL void __launch_bounds__(128) k_compress_g2(uint32_t n, const G2JStore* 
   }
   g2_compress_aff(out96 + 96ull * i, g2_to_aff(load_g2j(P[i])));
 }
+#endif
 
 // A7: bls.Sign / tbls.Sign -- x * H(m); scalars are 32 B big-endian (< r)
+#if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128) k_sign(uint32_t n, const uint8_t* sc32, const uint16_t* index, const uint8_t* msgs,
                                              uint32_t msg_len, const uint8_t* dst, uint32_t dst_len, uint8_t* out) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -481,6 +536,7 @@ DG_KERNEL void __launch_bounds__(128) k_sign(uint32_t n, const uint8_t* sc32, co
   }
   g2_compress_aff(o, sig);
 }
+#endif
 #endif
 
 }  // namespace dg

@@ -22,7 +22,7 @@ constexpr uint32_t MSM_C = 8, MSM_WIN = 8, MSM_NB = 256, MSM_NBK = MSM_WIN * MSM
 constexpr uint32_t MSM_CHUNK = 8;   // points per first-level lane
 constexpr uint32_t MSM_BSPLIT = 8;  // lanes per bucket at the second level
 
-#if defined(__HIP__)
+#if defined(__HIP__) && !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(256) k_msm_count(uint32_t R, uint64_t seed, const uint8_t* active, uint32_t* count) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R || !active[r]) return;
