@@ -146,12 +146,46 @@ __device__ __forceinline__ void co_phase(const CoM2 (&j2)[N2], Fp* tmp) {
 
 // ---------------------------------------------------------------- GT arithmetic
 struct CoGT {
-  Fp2 prod[36];  // products a_i b_j
+  Fp ctb[72];   // contributions of the products to the output components
+  Fp half[36];  // first summation level
   Fp tmp[CO_THREADS];
   Fp2 gamma[6];  // Frobenius constants xi^(k (p-1) / 6)
 };
 
-// dst = a * b in GT (dst may alias a or b): 36 Fp2 products (108 lanes), then the 6 convolution sums
+// GT multiplication in three short steps: (1) the 36 Fp2 products as 108 Fp products (Karatsuba, one
+// per lane); (2) 72 lanes turn each product into its contribution to one component of one output
+// coefficient, wrapped terms (i + j >= 6) already multiplied by xi; (3) a two-level sum, 36 then 12
+// lanes.  At most 3 dependent Fp additions per lane after the products, instead of ~16 on 6 lanes.
+//   contribution of a_i b_j = (t0 - t1) + (t2 - t0 - t1) u, times xi = 1 + u when wrapped:
+//   comp 0: t0 - t1 (plain), 2 t0 - t2 (wrapped);  comp 1: t2 - t0 - t1 (plain), t2 - 2 t1 (wrapped)
+__device__ __forceinline__ Fp co_contrib(const Fp* t, int comp, bool wrap) {
+  if (comp == 0) return wrap ? fp_sub(fp_dbl(t[0]), t[2]) : fp_sub(t[0], t[1]);
+  return wrap ? fp_sub(t[2], fp_dbl(t[1])) : fp_sub(fp_sub(t[2], t[0]), t[1]);
+}
+// out coefficient o, component comp: sum of `nterm` contributions ctb[(o * nterm + slot) * 2 + comp]
+__device__ __forceinline__ void co_sum_contribs(Fp12W* dst, Fp* ctb, Fp* half, int nterm) {
+  const int t = threadIdx.x;
+  // level 1 (nterm = 6: 36 lanes add pairs; nterm = 3: 12 lanes add the first two)
+  const int npair = nterm / 2;
+  if (t < 12 * npair) {
+    int o = t / (2 * npair), r = t % (2 * npair), p = r / 2, comp = r % 2;
+    half[t] = fp_add(ctb[(o * nterm + 2 * p) * 2 + comp], ctb[(o * nterm + 2 * p + 1) * 2 + comp]);
+  }
+  __syncthreads();
+  if (t < 12) {
+    int o = t / 2, comp = t % 2;
+    Fp acc = half[(o * npair) * 2 + comp];
+    for (int p = 1; p < npair; ++p) acc = fp_add(acc, half[(o * npair + p) * 2 + comp]);
+    if (nterm & 1) acc = fp_add(acc, ctb[(o * nterm + nterm - 1) * 2 + comp]);
+    if (comp == 0)
+      dst->e[o].c0 = acc;
+    else
+      dst->e[o].c1 = acc;
+  }
+  __syncthreads();
+}
+
+// dst = a * b in GT (dst may alias a or b)
 __device__ __forceinline__ void co_fp12_mul(Fp12W* dst, const Fp12W* a, const Fp12W* b, CoGT* s) {
   const int t = threadIdx.x;
   if (t < 108) {
@@ -159,20 +193,12 @@ __device__ __forceinline__ void co_fp12_mul(Fp12W* dst, const Fp12W* a, const Fp
     s->tmp[t] = fp_mul_inl(co_kara_operand(a->e[q / 6], m), co_kara_operand(b->e[q % 6], m));
   }
   __syncthreads();
-  if (t < 36) s->prod[t] = co_kara_combine(s->tmp + 3 * t);
-  __syncthreads();
-  if (t < 6) {
-    Fp2 lo = fp2_zero(), hi = fp2_zero();
-    for (int i = 0; i < 6; ++i) {
-      int j = t - i;
-      if (j >= 0)
-        lo = fp2_add(lo, s->prod[i * 6 + j]);
-      else
-        hi = fp2_add(hi, s->prod[i * 6 + j + 6]);
-    }
-    dst->e[t] = fp2_add(lo, fp2_mul_xi(hi));
+  if (t < 72) {
+    int q = t / 2, comp = t % 2, i = q / 6, j = q % 6, o = (i + j) % 6;
+    s->ctb[(o * 6 + i) * 2 + comp] = co_contrib(s->tmp + 3 * q, comp, i + j >= 6);
   }
   __syncthreads();
+  co_sum_contribs(dst, s->ctb, s->half, 6);
 }
 // dst = a * l for a line l = l0 + l2 w^2 + l3 w^3 (nonzero coefficients in L->e[0], e[2], e[3])
 __device__ __forceinline__ void co_fp12_mul_line(Fp12W* dst, const Fp12W* a, const Fp12W* L, CoGT* s) {
@@ -183,21 +209,13 @@ __device__ __forceinline__ void co_fp12_mul_line(Fp12W* dst, const Fp12W* a, con
     s->tmp[t] = fp_mul_inl(co_kara_operand(a->e[i], m), co_kara_operand(L->e[jj == 0 ? 0 : jj + 1], m));
   }
   __syncthreads();
-  if (t < 18) s->prod[t] = co_kara_combine(s->tmp + 3 * t);
-  __syncthreads();
-  if (t < 6) {
-    // c_k = a_k l0 + a_{k-2} l2 + a_{k-3} l3 (indices mod 6, wrapped terms times xi)
-    Fp2 lo = fp2_zero(), hi = fp2_zero();
-    for (int jj = 0; jj < 3; ++jj) {
-      int i = t - (jj == 0 ? 0 : jj + 1);
-      if (i >= 0)
-        lo = fp2_add(lo, s->prod[i * 3 + jj]);
-      else
-        hi = fp2_add(hi, s->prod[(i + 6) * 3 + jj]);
-    }
-    dst->e[t] = fp2_add(lo, fp2_mul_xi(hi));
+  if (t < 36) {
+    int q = t / 2, comp = t % 2, i = q / 3, jj = q % 3;
+    int k = i + (jj == 0 ? 0 : jj + 1), o = k % 6;
+    s->ctb[(o * 3 + jj) * 2 + comp] = co_contrib(s->tmp + 3 * q, comp, k >= 6);
   }
   __syncthreads();
+  co_sum_contribs(dst, s->ctb, s->half, 3);
 }
 __device__ __forceinline__ void co_fp12_copy(Fp12W* dst, const Fp12W* a) {
   if (threadIdx.x < 6) dst->e[threadIdx.x] = a->e[threadIdx.x];

@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-for mode in "--sync" ""; do
+for mode in "" "--async"; do
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --recover-rounds 0 --steps 6 $mode ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
 python - <<'PY'
 import json
