@@ -109,11 +109,16 @@ __device__ __forceinline__ void co_phase(const CoM2 (&j2)[N2], const CoM1 (&j1)[
     tmp[t] = fp_mul_inl(m ? j.a->c1 : j.a->c0, *j.b);
   }
   __syncthreads();
-  if (t < N2) {
-    CoM2 j = co_pick(j2, t);
-    *j.o = co_kara_combine(tmp + 3 * t);
-  } else if (t < N2 + N1) {
-    int u = t - N2;
+  if (t < 2 * N2) {
+    int q = t >> 1, c = t & 1;
+    CoM2 j = co_pick(j2, q);
+    const Fp* r = tmp + 3 * q;
+    if (c == 0)
+      j.o->c0 = fp_sub(r[0], r[1]);
+    else
+      j.o->c1 = fp_sub(fp_sub(r[2], r[0]), r[1]);
+  } else if (t < 2 * N2 + N1) {
+    int u = t - 2 * N2;
     CoM1 j = co_pick(j1, u);
     *j.o = Fp2{tmp[3 * N2 + 2 * u], tmp[3 * N2 + 2 * u + 1]};
   }
@@ -129,12 +134,87 @@ __device__ __forceinline__ void co_phase(const CoM2 (&j2)[N2], Fp* tmp) {
     tmp[t] = fp_mul_inl(co_kara_operand(*j.a, m), co_kara_operand(*j.b, m));
   }
   __syncthreads();
-  if (t < N2) {
-    CoM2 j = co_pick(j2, t);
-    *j.o = co_kara_combine(tmp + 3 * t);
+  if (t < 2 * N2) {
+    int q = t >> 1, c = t & 1;
+    CoM2 j = co_pick(j2, q);
+    const Fp* r = tmp + 3 * q;
+    if (c == 0)
+      j.o->c0 = fp_sub(r[0], r[1]);
+    else
+      j.o->c1 = fp_sub(fp_sub(r[2], r[0]), r[1]);
   }
   __syncthreads();
 }
+// Phase with its jobs given as switch-based loaders/storers (lambdas over LDS objects): every operand is
+// a constant LDS address in its own branch, so loads are ds_read (a table of job pointers would be
+// placed in scratch and dereferenced through flat loads).
+template <int N2, int N1, class LD2, class ST2, class LD1, class ST1>
+__device__ __forceinline__ void co_phase_f(LD2 ld2, ST2 st2, LD1 ld1, ST1 st1, Fp* tmp) {
+  static_assert(3 * N2 + 2 * N1 <= CO_THREADS, "phase too wide");
+  const int t = threadIdx.x;
+  if (t < 3 * N2) {
+    int q = t / 3, m = t - 3 * q;
+    Fp2 a, b;
+    ld2(q, a, b);
+    tmp[t] = fp_mul_inl(co_kara_operand(a, m), co_kara_operand(b, m));
+  } else if (t < 3 * N2 + 2 * N1) {
+    int u = t - 3 * N2, q = u / 2, m = u - 2 * q;
+    Fp2 a;
+    Fp b;
+    ld1(q, a, b);
+    tmp[t] = fp_mul_inl(m ? a.c1 : a.c0, b);
+  }
+  __syncthreads();
+  if (t < 2 * N2) {
+    int q = t >> 1, c = t & 1;
+    const Fp* r = tmp + 3 * q;
+    st2(q, c, c == 0 ? fp_sub(r[0], r[1]) : fp_sub(fp_sub(r[2], r[0]), r[1]));
+  } else if (t < 2 * N2 + N1) {
+    int u = t - 2 * N2;
+    st1(u, Fp2{tmp[3 * N2 + 2 * u], tmp[3 * N2 + 2 * u + 1]});
+  }
+  __syncthreads();
+}
+#define CO_L2(k, A, B) \
+  case k:              \
+    a_ = *(A);         \
+    b_ = *(B);         \
+    break;
+#define CO_S2(k, O)     \
+  case k:               \
+    cm((O), c_) = v_;   \
+    break;
+#define CO_L1(k, A, B) \
+  case k:              \
+    a_ = *(A);         \
+    b_ = *(B);         \
+    break;
+#define CO_S1(k, O) \
+  case k:           \
+    *(O) = v_;      \
+    break;
+#define CO_LD2(...) [&](int q_, Fp2& a_, Fp2& b_) { switch (q_) { __VA_ARGS__ } }
+#define CO_ST2(...) [&](int q_, int c_, const Fp& v_) { switch (q_) { __VA_ARGS__ } }
+#define CO_LD1(...) [&](int q_, Fp2& a_, Fp& b_) { switch (q_) { __VA_ARGS__ } }
+#define CO_ST1(...) [&](int q_, const Fp2& v_) { switch (q_) { __VA_ARGS__ } }
+#define CO_NO_LD1 [&](int, Fp2&, Fp&) {}
+#define CO_NO_ST1 [&](int, const Fp2&) {}
+
+// Component-parallel glue: lanes 2g + c, g < ngroups, run the body for component c (0: real, 1: u) of
+// group g's outputs; the linear Fp2 operations of the formulas are component-wise.
+#define CO_LANES(ngroups, ...)                  \
+  do {                                          \
+    const int t_ = threadIdx.x;                 \
+    if (t_ < 2 * (ngroups)) {                   \
+      const int c = t_ & 1, g = t_ >> 1;        \
+      (void)g;                                  \
+      __VA_ARGS__;                              \
+    }                                           \
+    __syncthreads();                            \
+  } while (0)
+__device__ __forceinline__ Fp& cm(Fp2* x, int c) { return c ? x->c1 : x->c0; }
+__device__ __forceinline__ const Fp& cm(const Fp2* x, int c) { return c ? x->c1 : x->c0; }
+__device__ __forceinline__ Fp fp_triple(const Fp& a) { return fp_add(fp_dbl(a), a); }
 // lane-0 glue; everyone waits
 #define CO_SERIAL(...)      \
   do {                      \
@@ -264,7 +344,7 @@ __device__ __forceinline__ void co_fp12_exp_z(Fp12W* dst, const Fp12W* a, Fp12W*
 }
 
 // f <- f^(3 (p^12 - 1) / r), the chain of final_exp_cubed (pairing.h).  scratch: 7 Fp12W.
-__device__ void co_final_exp_cubed(Fp12W* f, Fp12W* sc, CoGT* s) {
+__device__ __forceinline__ void co_final_exp_cubed(Fp12W* f, Fp12W* sc, CoGT* s) {
   Fp12W *f1 = &sc[0], *f2 = &sc[1], *t0 = &sc[2], *t1 = &sc[3], *x = &sc[4], *y = &sc[5], *acc = &sc[6];
   co_fp12_inv(f1, f);
   co_fp12_conj(f2, f);
@@ -303,39 +383,38 @@ struct CoG2Tmp {
   uint32_t flag;
 };
 
-// P <- 2P (dbl-2009-l, a = 0): three product phases
-__device__ void co_g2_dbl(CoG2* P, CoG2Tmp* s) {
+// P <- 2P (dbl-2009-l, a = 0): three product phases, component-parallel glue
+__device__ __forceinline__ void co_g2_dbl(CoG2* P, CoG2Tmp* s) {
   Fp2 *A = &s->v[0], *B = &s->v[1], *YZ = &s->v[2], *E = &s->v[3], *XB = &s->v[4], *C = &s->v[5], *D0 = &s->v[6],
-      *F = &s->v[7], *DX = &s->v[8], *Y3 = &s->v[9];
-  {
-    const CoM2 j[3] = {{&P->x, &P->x, A}, {&P->y, &P->y, B}, {&P->y, &P->z, YZ}};
-    co_phase(j, s->tmp);
-  }
-  CO_SERIAL({
-    *E = fp2_triple(*A);
-    *XB = fp2_add(P->x, *B);
+      *F = &s->v[7], *DX = &s->v[8], *Y3 = &s->v[9], *C8 = &s->v[10];
+  co_phase_f<3, 0>(CO_LD2(CO_L2(0, &P->x, &P->x) CO_L2(1, &P->y, &P->y) CO_L2(2, &P->y, &P->z)), CO_ST2(CO_S2(0, A) CO_S2(1, B) CO_S2(2, YZ)),
+                   CO_NO_LD1, CO_NO_ST1, s->tmp);
+  CO_LANES(2, {
+    if (g == 0) cm(E, c) = fp_triple(cm(A, c));
+    else cm(XB, c) = fp_add(cm(&P->x, c), cm(B, c));
   });
-  {
-    const CoM2 j[3] = {{B, B, C}, {XB, XB, D0}, {E, E, F}};
-    co_phase(j, s->tmp);
-  }
-  CO_SERIAL({
-    Fp2 D = fp2_dbl(fp2_sub(fp2_sub(*D0, *A), *C));
-    Fp2 X3 = fp2_sub(*F, fp2_dbl(D));
-    *DX = fp2_sub(D, X3);
-    P->x = X3;
-    P->z = fp2_dbl(*YZ);
+  co_phase_f<3, 0>(CO_LD2(CO_L2(0, B, B) CO_L2(1, XB, XB) CO_L2(2, E, E)), CO_ST2(CO_S2(0, C) CO_S2(1, D0) CO_S2(2, F)),
+                   CO_NO_LD1, CO_NO_ST1, s->tmp);
+  CO_LANES(3, {
+    if (g == 0) {
+      Fp D = fp_dbl(fp_sub(fp_sub(cm(D0, c), cm(A, c)), cm(C, c)));
+      Fp X3 = fp_sub(cm(F, c), fp_dbl(D));
+      cm(DX, c) = fp_sub(D, X3);
+      cm(&P->x, c) = X3;
+    } else if (g == 1) {
+      cm(&P->z, c) = fp_dbl(cm(YZ, c));
+    } else {
+      cm(C8, c) = fp_dbl(fp_dbl(fp_dbl(cm(C, c))));
+    }
   });
-  {
-    const CoM2 j[1] = {{E, DX, Y3}};
-    co_phase(j, s->tmp);
-  }
-  CO_SERIAL(P->y = fp2_sub(*Y3, fp2_dbl(fp2_dbl(fp2_dbl(*C)))));
+  co_phase_f<1, 0>(CO_LD2(CO_L2(0, E, DX)), CO_ST2(CO_S2(0, Y3)),
+                   CO_NO_LD1, CO_NO_ST1, s->tmp);
+  CO_LANES(1, cm(&P->y, c) = fp_sub(cm(Y3, c), cm(C8, c)));
 }
 
 // O <- P + Q (add-2007-bl); exceptional cases (an input at infinity, P = +-Q) are resolved on lane 0.
 // O may alias P or Q.
-__device__ void co_g2_add(CoG2* O, const CoG2* P, const CoG2* Q, CoG2Tmp* s) {
+__device__ __forceinline__ void co_g2_add(CoG2* O, const CoG2* P, const CoG2* Q, CoG2Tmp* s) {
   Fp2 *Z1Z1 = &s->v[0], *Z2Z2 = &s->v[1], *ZZ = &s->v[2], *Z12 = &s->v[3], *U1 = &s->v[4], *U2 = &s->v[5],
       *S1a = &s->v[6], *S2a = &s->v[7], *S1 = &s->v[8], *S2 = &s->v[9], *H = &s->v[10], *R = &s->v[11],
       *I = &s->v[12], *R2 = &s->v[13], *J = &s->v[14], *V = &s->v[15];
@@ -349,21 +428,22 @@ __device__ void co_g2_add(CoG2* O, const CoG2* P, const CoG2* Q, CoG2Tmp* s) {
     *Z12 = fp2_add(P->z, Q->z);
   });
   if (s->flag) return;
-  {
-    const CoM2 j[3] = {{&P->z, &P->z, Z1Z1}, {&Q->z, &Q->z, Z2Z2}, {Z12, Z12, ZZ}};
-    co_phase(j, s->tmp);
-  }
-  {
-    const CoM2 j[4] = {{&P->x, Z2Z2, U1}, {&Q->x, Z1Z1, U2}, {&P->y, &Q->z, S1a}, {&Q->y, &P->z, S2a}};
-    co_phase(j, s->tmp);
-  }
-  {
-    const CoM2 j[2] = {{S1a, Z2Z2, S1}, {S2a, Z1Z1, S2}};
-    co_phase(j, s->tmp);
-  }
+  co_phase_f<3, 0>(CO_LD2(CO_L2(0, &P->z, &P->z) CO_L2(1, &Q->z, &Q->z) CO_L2(2, Z12, Z12)), CO_ST2(CO_S2(0, Z1Z1) CO_S2(1, Z2Z2) CO_S2(2, ZZ)),
+                   CO_NO_LD1, CO_NO_ST1, s->tmp);
+  co_phase_f<4, 0>(CO_LD2(CO_L2(0, &P->x, Z2Z2) CO_L2(1, &Q->x, Z1Z1) CO_L2(2, &P->y, &Q->z) CO_L2(3, &Q->y, &P->z)), CO_ST2(CO_S2(0, U1) CO_S2(1, U2) CO_S2(2, S1a) CO_S2(3, S2a)),
+                   CO_NO_LD1, CO_NO_ST1, s->tmp);
+  co_phase_f<2, 0>(CO_LD2(CO_L2(0, S1a, Z2Z2) CO_L2(1, S2a, Z1Z1)), CO_ST2(CO_S2(0, S1) CO_S2(1, S2)),
+                   CO_NO_LD1, CO_NO_ST1, s->tmp);
+  CO_LANES(2, {
+    if (g == 0) {
+      Fp h = fp_sub(cm(U2, c), cm(U1, c));
+      cm(H, c) = h;
+      cm(Z12, c) = fp_dbl(h);  // I0 = 2H
+    } else {
+      cm(R, c) = fp_dbl(fp_sub(cm(S2, c), cm(S1, c)));
+    }
+  });
   CO_SERIAL({
-    *H = fp2_sub(*U2, *U1);
-    *R = fp2_dbl(fp2_sub(*S2, *S1));
     s->flag = 0;
     if (fp2_is_zero(*H)) {
       // P = Q: double on this lane (practically never); P = -Q: infinity
@@ -375,37 +455,32 @@ __device__ void co_g2_add(CoG2* O, const CoG2* P, const CoG2* Q, CoG2Tmp* s) {
       }
       s->flag = 1;
     }
-    *Z12 = fp2_dbl(*H);  // I0 = 2H
   });
   if (s->flag) return;
-  {
-    const CoM2 j[2] = {{Z12, Z12, I}, {R, R, R2}};
-    co_phase(j, s->tmp);
-  }
-  {
-    const CoM2 j[2] = {{H, I, J}, {U1, I, V}};
-    co_phase(j, s->tmp);
-  }
-  CO_SERIAL({
-    Fp2 X3 = fp2_sub(fp2_sub(*R2, *J), fp2_dbl(*V));
-    *V = fp2_sub(*V, X3);                       // V - X3
-    *ZZ = fp2_sub(fp2_sub(*ZZ, *Z1Z1), *Z2Z2);  // 2 Z1 Z2
-    *I = X3;
+  co_phase_f<2, 0>(CO_LD2(CO_L2(0, Z12, Z12) CO_L2(1, R, R)), CO_ST2(CO_S2(0, I) CO_S2(1, R2)),
+                   CO_NO_LD1, CO_NO_ST1, s->tmp);
+  co_phase_f<2, 0>(CO_LD2(CO_L2(0, H, I) CO_L2(1, U1, I)), CO_ST2(CO_S2(0, J) CO_S2(1, V)),
+                   CO_NO_LD1, CO_NO_ST1, s->tmp);
+  CO_LANES(2, {
+    if (g == 0) {
+      Fp X3 = fp_sub(fp_sub(cm(R2, c), cm(J, c)), fp_dbl(cm(V, c)));
+      cm(V, c) = fp_sub(cm(V, c), X3);  // V - X3
+      cm(I, c) = X3;
+    } else {
+      cm(ZZ, c) = fp_sub(fp_sub(cm(ZZ, c), cm(Z1Z1, c)), cm(Z2Z2, c));  // 2 Z1 Z2
+    }
   });
-  {
-    // U1 <- r (V - X3), U2 <- S1 J, Z1Z1 <- Z3 = 2 Z1 Z2 H
-    const CoM2 j[3] = {{R, V, U1}, {S1, J, U2}, {ZZ, H, Z1Z1}};
-    co_phase(j, s->tmp);
-  }
-  CO_SERIAL({
-    O->x = *I;
-    O->y = fp2_sub(*U1, fp2_dbl(*U2));
-    O->z = *Z1Z1;
+  co_phase_f<3, 0>(CO_LD2(CO_L2(0, R, V) CO_L2(1, S1, J) CO_L2(2, ZZ, H)), CO_ST2(CO_S2(0, U1) CO_S2(1, U2) CO_S2(2, Z1Z1)),
+                   CO_NO_LD1, CO_NO_ST1, s->tmp);
+  CO_LANES(1, {
+    cm(&O->x, c) = cm(I, c);
+    cm(&O->y, c) = fp_sub(cm(U1, c), fp_dbl(cm(U2, c)));
+    cm(&O->z, c) = cm(Z1Z1, c);
   });
 }
 
 // psi(P) = (conj(x) cx, conj(y) cy, conj(z)) -- one phase; O may alias P
-__device__ void co_g2_psi(CoG2* O, const CoG2* P, CoG2Tmp* s) {
+__device__ __forceinline__ void co_g2_psi(CoG2* O, const CoG2* P, CoG2Tmp* s) {
   Fp2 *cx = &s->v[0], *cy = &s->v[1], *a = &s->v[2], *b = &s->v[3], *ox = &s->v[4], *oy = &s->v[5];
   CO_SERIAL({
     *cx = fp2_const(PSI_CX);
@@ -413,14 +488,12 @@ __device__ void co_g2_psi(CoG2* O, const CoG2* P, CoG2Tmp* s) {
     *a = fp2_conj(P->x);
     *b = fp2_conj(P->y);
   });
-  {
-    const CoM2 j[2] = {{a, cx, ox}, {b, cy, oy}};
-    co_phase(j, s->tmp);
-  }
+  co_phase_f<2, 0>(CO_LD2(CO_L2(0, a, cx) CO_L2(1, b, cy)), CO_ST2(CO_S2(0, ox) CO_S2(1, oy)),
+                   CO_NO_LD1, CO_NO_ST1, s->tmp);
   CO_SERIAL({ *O = CoG2{*ox, *oy, fp2_conj(P->z)}; });
 }
 // O = [z] P (z = -Z_ABS); O must not alias P
-__device__ void co_g2_mul_z(CoG2* O, const CoG2* P, CoG2Tmp* s) {
+__device__ __forceinline__ void co_g2_mul_z(CoG2* O, const CoG2* P, CoG2Tmp* s) {
   CO_SERIAL(*O = *P);
   for (int b = 62; b >= 0; --b) {
     co_g2_dbl(O, s);
@@ -429,7 +502,7 @@ __device__ void co_g2_mul_z(CoG2* O, const CoG2* P, CoG2Tmp* s) {
   CO_SERIAL(O->y = fp2_neg(O->y));
 }
 // P <- h_eff P = [z^2 - z - 1]P + [z - 1]psi(P) + psi^2(2P)  (as g2_clear_cofactor, curve.h); t: 4 CoG2
-__device__ void co_g2_clear_cofactor(CoG2* P, CoG2* t, CoG2Tmp* s) {
+__device__ __forceinline__ void co_g2_clear_cofactor(CoG2* P, CoG2* t, CoG2Tmp* s) {
   CoG2 *t1 = &t[0], *t2 = &t[1], *t3 = &t[2], *p0 = &t[3];
   CO_SERIAL(*p0 = *P);
   co_g2_mul_z(t1, p0, s);  // t1 = [z]P
@@ -461,76 +534,78 @@ struct CoML {
   Fp tmp[CO_THREADS];
 };
 
-__device__ void co_line_dbl(CoML* m, Fp12W* L) {
-  Fp2 *xy = &m->v[0], *b = &m->v[1], *c = &m->v[2], *j = &m->v[3], *yz2 = &m->v[4], *yz = &m->v[5], *a = &m->v[6],
-      *e = &m->v[7], *g = &m->v[8], *h = &m->v[9], *j3 = &m->v[10], *nh = &m->v[11], *bf = &m->v[12],
+__device__ __forceinline__ void co_line_dbl(CoML* m, Fp12W* L) {
+  Fp2 *xy = &m->v[0], *b = &m->v[1], *cc = &m->v[2], *j = &m->v[3], *yz2 = &m->v[4], *yz = &m->v[5], *a = &m->v[6],
+      *e = &m->v[7], *gg = &m->v[8], *h = &m->v[9], *j3 = &m->v[10], *nh = &m->v[11], *bf = &m->v[12],
       *e2 = &m->v[13], *g2 = &m->v[14];
   CoG2* T = &m->T;
-  CO_SERIAL(*yz = fp2_add(T->y, T->z));
-  {
-    const CoM2 jb[5] = {{&T->x, &T->y, xy}, {&T->y, &T->y, b}, {&T->z, &T->z, c}, {&T->x, &T->x, j}, {yz, yz, yz2}};
-    co_phase(jb, m->tmp);
-  }
-  CO_SERIAL({
-    *a = fp2_half(*xy);
-    *e = fp2_mul_b3(*c);
-    Fp2 f = fp2_triple(*e);
-    *g = fp2_half(fp2_add(*b, f));
-    *h = fp2_sub(fp2_sub(*yz2, *b), *c);
-    L->e[0] = fp2_sub(*e, *b);
-    *j3 = fp2_triple(*j);
-    *nh = fp2_neg(*h);
-    *bf = fp2_sub(*b, f);
+  CO_LANES(1, cm(yz, c) = fp_add(cm(&T->y, c), cm(&T->z, c)));
+  co_phase_f<5, 0>(CO_LD2(CO_L2(0, &T->x, &T->y) CO_L2(1, &T->y, &T->y) CO_L2(2, &T->z, &T->z) CO_L2(3, &T->x, &T->x) CO_L2(4, yz, yz)), CO_ST2(CO_S2(0, xy) CO_S2(1, b) CO_S2(2, cc) CO_S2(3, j) CO_S2(4, yz2)),
+                   CO_NO_LD1, CO_NO_ST1, m->tmp);
+  CO_LANES(4, {
+    if (g == 0) {
+      // e = 12 (1 + u) c: component 0 of (1 + u) c is c0 - c1, component 1 is c0 + c1
+      Fp xc = c ? fp_add(cc->c0, cc->c1) : fp_sub(cc->c0, cc->c1);
+      Fp x4 = fp_dbl(fp_dbl(xc));
+      Fp ec = fp_add(fp_dbl(x4), x4);
+      Fp fc = fp_triple(ec);
+      Fp bc = cm(b, c);
+      cm(e, c) = ec;
+      cm(gg, c) = fp_half(fp_add(bc, fc));
+      cm(&L->e[0], c) = fp_sub(ec, bc);
+      cm(bf, c) = fp_sub(bc, fc);
+    } else if (g == 1) {
+      Fp hc = fp_sub(fp_sub(cm(yz2, c), cm(b, c)), cm(cc, c));
+      cm(h, c) = hc;
+      cm(nh, c) = fp_neg(hc);
+    } else if (g == 2) {
+      cm(a, c) = fp_half(cm(xy, c));
+    } else {
+      cm(j3, c) = fp_triple(cm(j, c));
+    }
   });
-  {
-    const CoM2 jb[4] = {{e, e, e2}, {a, bf, &T->x}, {g, g, g2}, {b, h, &T->z}};
-    const CoM1 j1[2] = {{j3, &m->px, &L->e[2]}, {nh, &m->py, &L->e[3]}};
-    co_phase(jb, j1, m->tmp);
-  }
-  CO_SERIAL(T->y = fp2_sub(*g2, fp2_triple(*e2)));
+  co_phase_f<4, 2>(CO_LD2(CO_L2(0, e, e) CO_L2(1, a, bf) CO_L2(2, gg, gg) CO_L2(3, b, h)), CO_ST2(CO_S2(0, e2) CO_S2(1, &T->x) CO_S2(2, g2) CO_S2(3, &T->z)),
+                   CO_LD1(CO_L1(0, j3, &m->px) CO_L1(1, nh, &m->py)), CO_ST1(CO_S1(0, &L->e[2]) CO_S1(1, &L->e[3])), m->tmp);
+  CO_LANES(1, cm(&T->y, c) = fp_sub(cm(g2, c), fp_triple(cm(e2, c))));
 }
 
-__device__ void co_line_add(CoML* m, Fp12W* L) {
+__device__ __forceinline__ void co_line_add(CoML* m, Fp12W* L) {
   Fp2 *qyz = &m->v[0], *qxz = &m->v[1], *th = &m->v[2], *la = &m->v[3], *nth = &m->v[4], *c = &m->v[5],
-      *d = &m->v[6], *tq = &m->v[7], *lq = &m->v[8], *e = &m->v[9], *f = &m->v[10], *g = &m->v[11], *h = &m->v[12],
+      *d = &m->v[6], *tq = &m->v[7], *lq = &m->v[8], *e = &m->v[9], *f = &m->v[10], *gv = &m->v[11], *h = &m->v[12],
       *gh = &m->v[13], *y1 = &m->v[14], *y2 = &m->v[15];
   CoG2* T = &m->T;
-  {
-    const CoM2 jb[2] = {{&m->qy, &T->z, qyz}, {&m->qx, &T->z, qxz}};
-    co_phase(jb, m->tmp);
-  }
-  CO_SERIAL({
-    *th = fp2_sub(T->y, *qyz);
-    *la = fp2_sub(T->x, *qxz);
-    *nth = fp2_neg(*th);
+  co_phase_f<2, 0>(CO_LD2(CO_L2(0, &m->qy, &T->z) CO_L2(1, &m->qx, &T->z)), CO_ST2(CO_S2(0, qyz) CO_S2(1, qxz)),
+                   CO_NO_LD1, CO_NO_ST1, m->tmp);
+  CO_LANES(2, {
+    if (g == 0) {
+      Fp tc = fp_sub(cm(&T->y, c), cm(qyz, c));
+      cm(th, c) = tc;
+      cm(nth, c) = fp_neg(tc);
+    } else {
+      cm(la, c) = fp_sub(cm(&T->x, c), cm(qxz, c));
+    }
   });
-  {
-    const CoM2 jb[4] = {{th, th, c}, {la, la, d}, {th, &m->qx, tq}, {la, &m->qy, lq}};
-    const CoM1 j1[2] = {{nth, &m->px, &L->e[2]}, {la, &m->py, &L->e[3]}};
-    co_phase(jb, j1, m->tmp);
-  }
-  CO_SERIAL(L->e[0] = fp2_sub(*tq, *lq));
-  {
-    const CoM2 jb[3] = {{la, d, e}, {&T->z, c, f}, {&T->x, d, g}};
-    co_phase(jb, m->tmp);
-  }
-  CO_SERIAL({
-    *h = fp2_sub(fp2_add(*e, *f), fp2_dbl(*g));
-    *gh = fp2_sub(*g, *h);
+  co_phase_f<4, 2>(CO_LD2(CO_L2(0, th, th) CO_L2(1, la, la) CO_L2(2, th, &m->qx) CO_L2(3, la, &m->qy)), CO_ST2(CO_S2(0, c) CO_S2(1, d) CO_S2(2, tq) CO_S2(3, lq)),
+                   CO_LD1(CO_L1(0, nth, &m->px) CO_L1(1, la, &m->py)), CO_ST1(CO_S1(0, &L->e[2]) CO_S1(1, &L->e[3])), m->tmp);
+  CO_LANES(1, cm(&L->e[0], c) = fp_sub(cm(tq, c), cm(lq, c)));
+  co_phase_f<3, 0>(CO_LD2(CO_L2(0, la, d) CO_L2(1, &T->z, c) CO_L2(2, &T->x, d)), CO_ST2(CO_S2(0, e) CO_S2(1, f) CO_S2(2, gv)),
+                   CO_NO_LD1, CO_NO_ST1, m->tmp);
+  CO_LANES(1, {
+    Fp hc = fp_sub(fp_add(cm(e, c), cm(f, c)), fp_dbl(cm(gv, c)));
+    cm(h, c) = hc;
+    cm(gh, c) = fp_sub(cm(gv, c), hc);
   });
-  {
-    const CoM2 jb[4] = {{la, h, &T->x}, {th, gh, y1}, {e, &T->y, y2}, {&T->z, e, qyz}};
-    co_phase(jb, m->tmp);
-  }
-  CO_SERIAL({
-    T->y = fp2_sub(*y1, *y2);
-    T->z = *qyz;
+  co_phase_f<4, 0>(CO_LD2(CO_L2(0, la, h) CO_L2(1, th, gh) CO_L2(2, e, &T->y) CO_L2(3, &T->z, e)), CO_ST2(CO_S2(0, &T->x) CO_S2(1, y1) CO_S2(2, y2) CO_S2(3, qyz)),
+                   CO_NO_LD1, CO_NO_ST1, m->tmp);
+  CO_LANES(1, {
+    cm(&T->y, c) = fp_sub(cm(y1, c), cm(y2, c));
+    cm(&T->z, c) = cm(qyz, c);
   });
 }
 
 // f = Miller loop of (P, Q), P = (m->px, m->py) and Q = (m->qx, m->qy) affine, neither at infinity
 // (z < 0: conjugated at the end).  L: line scratch.
-__device__ void co_miller_loop(Fp12W* f, Fp12W* L, CoML* m, CoGT* s) {
+__device__ __forceinline__ void co_miller_loop(Fp12W* f, Fp12W* L, CoML* m, CoGT* s) {
   const int t = threadIdx.x;
   if (t < 6) {
     f->e[t] = t == 0 ? fp2_one() : fp2_zero();

@@ -330,9 +330,8 @@ DG_KERNEL void __launch_bounds__(128) k_pair_miller_coop(uint32_t nslots, uint64
   const uint32_t s = blockIdx.x;
   if (s < nslots) {
     CO_SERIAL({
-      G1J bx = jac_from_aff(load_g1a(keys[s]));
-      if (nslots > 1) bx = jac_mul_u64(bx, rlc_beta(seed, s));
-      G1A pa = g1_to_aff(bx);
+      G1A pa = load_g1a(keys[s]);  // decoded keys are affine already; with one key beta = 1
+      if (nslots > 1) pa = g1_to_aff(jac_mul_u64(jac_from_aff(pa), rlc_beta(seed, s)));
       ml.px = pa.x;
       ml.py = pa.y;
       skip = pa.inf ? 1u : 0u;
