@@ -94,3 +94,11 @@ extern "C" int hc_verify_dbg(const uint8_t* pk48, const uint8_t* msg, uint32_t n
   Fp12 f12 = final_exp_cubed(miller_loop<2>(P, Q, 2));
   return (fp12_is_one(fp12_mul(f1, f2)) ? 1 : 0) | (fp12_is_one(f12) ? 2 : 0);
 }
+// safegcd inversion (fp_inv) and the Fermat cross-check, on a plain 48 B big-endian value < p
+extern "C" void hc_fp_inv(const uint8_t* a48, uint8_t* out_sg48, uint8_t* out_fermat48) {
+  Fp a;
+  fp_from_be48_plain(a, a48);
+  Fp m = fp_to_mont(a);
+  fp_to_be48(out_sg48, fp_inv(m));
+  fp_to_be48(out_fermat48, fp_inv_fermat(m));
+}

@@ -7,14 +7,15 @@
 #include "../../drand_amd/csrc/kernels.h"
 
 namespace dg {
-thread_local uint64_t g_fp_mul_count = 0, g_fp_sqr_count = 0;
+thread_local uint64_t g_fp_mul_count = 0, g_fp_sqr_count = 0, g_fp_inv_count = 0;
 }
 using namespace dg;
 
-static void reset() { g_fp_mul_count = g_fp_sqr_count = 0; }
+static void reset() { g_fp_mul_count = g_fp_sqr_count = g_fp_inv_count = 0; }
 static void take(uint64_t* out) {
   out[0] = g_fp_mul_count;
   out[1] = g_fp_sqr_count;
+  out[2] = g_fp_inv_count;
 }
 
 extern "C" {

@@ -13,6 +13,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 MAC_MUL, MAC_SQR = 288, 222
+# one safegcd inversion (field.h fp_inv): 37 batches x 13 limbs x (6 + 4) signed 32x32->64 multiply-adds
+MAC_INV = 37 * 13 * 10
 DST = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"
 
 
@@ -22,15 +24,16 @@ def main():
     c = json.load(open(os.path.join(ROOT, "tests", "golden", "chain_t3n5.json")))
     rounds = c["rounds"]
     pk = bytes.fromhex(c["pk"])
-    o = (ctypes.c_uint64 * 2)()
+    o = (ctypes.c_uint64 * 3)()
     acc = {}
 
     def add(name, n=1):
-        m, s = o[0], o[1]
-        a = acc.setdefault(name, [0, 0, 0])
+        m, s, v = o[0], o[1], o[2]
+        a = acc.setdefault(name, [0, 0, 0, 0])
         a[0] += m
         a[1] += s
-        a[2] += n
+        a[2] += v
+        a[3] += n
 
     for i, r in enumerate(rounds):
         msg = bytes.fromhex(r["msg"])
@@ -56,10 +59,11 @@ def main():
             add("k_verify_items")
             L.oc_batch_final(pk, sig, nxt, o)
             add("k_pair_miller+k_final_check")
-    out = {"mac_per_mul": MAC_MUL, "mac_per_sqr": MAC_SQR, "sample": "tests/golden/chain_t3n5.json (64 rounds)",
+    out = {"mac_per_mul": MAC_MUL, "mac_per_sqr": MAC_SQR, "mac_per_inv": MAC_INV, "sample": "tests/golden/chain_t3n5.json (64 rounds)",
            "per_unit": {}}
-    for k, (m, s, n) in acc.items():
-        out["per_unit"][k] = {"mul": m / n, "sqr": s / n, "M": (m + s) / n, "macs": (m * MAC_MUL + s * MAC_SQR) / n}
+    for k, (m, s, v, n) in acc.items():
+        out["per_unit"][k] = {"mul": m / n, "sqr": s / n, "inv": v / n, "M": (m + s) / n,
+                              "macs": (m * MAC_MUL + s * MAC_SQR + v * MAC_INV) / n}
     out["per_unit"]["k_key_accum"] = out["per_unit"]["k_sum_rows"]
     with open(os.path.join(ROOT, "profiles", "opcounts.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
