@@ -172,6 +172,7 @@ def main():
     side = torch.cuda.Stream(dev)
     pkb = ctypes.c_char_p(pk)
     counter = [0]
+    fallbacks = []  # seeds whose batch equation failed or isolated items (per-item pass ran)
 
     def step(seed):
         """Enqueue one batch (asynchronously: consecutive batches overlap) and the all-gather of its verdict
@@ -185,6 +186,9 @@ def main():
             L.check(lib.dg_verify_beacons_dev(pkb, n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off),
                                               L.ptr(d_sig), L.ptr(d_st), seed, None))
             side.wait_stream(torch.cuda.current_stream(dev))
+            ok, iso = L.last_batch_flags()  # the call has already waited for the batch
+            if not ok or iso:
+                fallbacks.append(seed)
         else:
             L.check(lib.dg_verify_beacons_dev_async(pkb, n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off),
                                                     L.ptr(d_sig), L.ptr(d_st), seed, None,
@@ -258,6 +262,7 @@ def main():
                                       "shared group key (BASELINE configs[1]; configs[3] at N>1)" % n,
                           "rounds_per_gpu": n, "global_rounds": world * n, "parallelism": "rounds sharded dp%d" % world},
                "roofline": roof, "cpu_baseline": cpu, "recover": rec,
+               "batch_fallbacks": None if args.use_async else fallbacks,
                "kernel_time_share": share,
                "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()}}
         print(json.dumps(out), flush=True)

@@ -46,6 +46,7 @@ SIGNATURES = {
     "dg_verify_beacons_dev": ([_P, _SZ, _P, _P, _P, _P, _P, _P, _U64, _P], _I),
     "dg_verify_beacons_dev_async": ([_P, _SZ, _P, _P, _P, _P, _P, _P, _U64, _P, _P], _I),
     "dg_wait_all": ([], _I),
+    "dg_last_batch_flags": ([_P], _I),
     "dg_set_timing": ([_I], _I),
     "dg_last_timings": ([_P, _P, _P, _I], _I),
 }
@@ -123,6 +124,13 @@ def u8(a, shape=None):
     if shape is not None:
         arr = arr.reshape(shape)
     return arr
+
+
+def last_batch_flags():
+    """(batch equation held, some item isolated) for the most recent verification batch."""
+    out = np.zeros(2, dtype=np.uint32)
+    check(lib().dg_last_batch_flags(ptr(out)))
+    return bool(out[0]), bool(out[1])
 
 
 def timings():

@@ -661,6 +661,16 @@ int dg_verify_beacons_dev_async(const uint8_t* pk48_host, size_t n, const uint64
                              (hipStream_t)in_stream, (hipStream_t)done_stream);
 }
 
+int dg_last_batch_flags(uint32_t* out2) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  RET(wait_all());
+  Set& set = cur_set();
+  if (set.pool.size() < S_COUNT || !set.pool[S_FLAG]) return fail(DG_E_ARG, "no batch has run");
+  HIPCHK(hipMemcpy(out2, set.pool[S_FLAG], 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int dg_wait_all(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   RET(require_ready());

@@ -7,6 +7,9 @@
 #include "fr.h"
 #include "coop.h"
 
+#ifndef DG_HOT_WAVES
+#define DG_HOT_WAVES 2  // min waves per SIMD for the hot kernels: 256 VGPRs each (measured: 2 beats 1 by 6%)
+#endif
 #ifndef DG_TU_HOT
 #define DG_TU_HOT 0  // 1 in kernels_hot.hip: only the hot kernels are defined there (DESIGN.md §code generation)
 #endif
@@ -123,14 +126,14 @@ DG_KERNEL void __launch_bounds__(128) k_hash_to_g2(uint32_t n, const uint8_t* ms
 
 // hash-to-curve without cofactor clearing (RLC path)
 #if DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128) k_h2c_uncleared(uint32_t n, const uint8_t* msgs, uint32_t msg_len,
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_h2c_uncleared(uint32_t n, const uint8_t* msgs, uint32_t msg_len,
                                                       const uint8_t* dst, uint32_t dst_len, G2JStore* outQ) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   store_g2j(outQ[i], hash_to_g2_uncleared(msgs + (size_t)msg_len * i, msg_len, dst, dst_len));
 }
 #else
-DG_KERNEL void __launch_bounds__(128) k_h2c_uncleared(uint32_t n, const uint8_t* msgs, uint32_t msg_len,
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_h2c_uncleared(uint32_t n, const uint8_t* msgs, uint32_t msg_len,
                                                       const uint8_t* dst, uint32_t dst_len, G2JStore* outQ);
 #endif
 
@@ -212,7 +215,7 @@ DG_KERNEL void __launch_bounds__(64) k_pubpoly_eval(uint32_t n, uint32_t t, cons
 // decode sigma of every item (96 B at sigs + stride*i + offset) with the G2 subgroup check; claim the
 // item's (round, slot) cell -- a taken cell sends the item to the individual check (`isolate`)
 #if DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128) k_decode_items(uint32_t n, uint32_t k, uint32_t nslots, const uint8_t* sigs,
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_decode_items(uint32_t n, uint32_t k, uint32_t nslots, const uint8_t* sigs,
                                                      uint32_t stride, uint32_t offset, const uint32_t* item_slot,
                                                      const uint8_t* key_status, G2AStore* S, uint8_t* status,
                                                      uint32_t* cell, uint8_t* isolate) {
@@ -236,7 +239,7 @@ DG_KERNEL void __launch_bounds__(128) k_decode_items(uint32_t n, uint32_t k, uin
   }
 }
 #else
-DG_KERNEL void __launch_bounds__(128) k_decode_items(uint32_t n, uint32_t k, uint32_t nslots, const uint8_t* sigs,
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_decode_items(uint32_t n, uint32_t k, uint32_t nslots, const uint8_t* sigs,
                                                      uint32_t stride, uint32_t offset, const uint32_t* item_slot,
                                                      const uint8_t* key_status, G2AStore* S, uint8_t* status,
                                                      uint32_t* cell, uint8_t* isolate);

@@ -121,6 +121,10 @@ int dg_verify_beacons_dev_async(const uint8_t* pk48_host, size_t n, const uint64
                                 const uint64_t* d_round, const uint8_t* d_prev_sigs, const uint32_t* d_prev_sig_off,
                                 const uint8_t* d_sigs96, uint8_t* d_status, uint64_t seed, void* in_stream,
                                 void* done_stream);
+/* Diagnostics of the most recent verification batch: out2[0] = 1 if the random-linear-combination
+ * batch equation held, out2[1] = 1 if some item was checked on its own (duplicate key cell).  A valid
+ * batch must pass on the batch path; the per-item fallback only decides failures. */
+int dg_last_batch_flags(uint32_t* out2);
 /* Wait for every batch enqueued by the asynchronous entry points. */
 int dg_wait_all(void);
 

@@ -252,3 +252,31 @@ def test_verify_at_size_exact_bitmap():
     st = tbls.verify_recovered_batch(pk, msgs, bad, seed=22)
     assert np.nonzero(st)[0].tolist() == bad_pos
     assert set(st[bad_pos].tolist()) == {L.ST_BAD_SIG}
+
+
+def test_valid_batches_pass_on_the_batch_path_many_seeds():
+    """The RLC batch equation (MSM, cooperative Miller loops, final exponentiation) must accept valid
+    batches for every seed: the per-item fallback would hide a wrong batch path behind correct verdicts."""
+    c = chain()
+    pr, rr, ps, sigs, msgs = chain_arrays(c)
+    pk = hx(c["pk"])
+    bad_seeds = []
+    for seed in range(1, 121):
+        st = tbls.verify_beacons(pk, pr, rr, ps, sigs, seed=seed)
+        ok, iso = L.last_batch_flags()
+        assert not st.any()
+        if not ok or iso:
+            bad_seeds.append(seed)
+    assert bad_seeds == []
+
+
+def test_valid_partial_batches_pass_on_the_batch_path():
+    c = chain()
+    pub = tbls.PubPoly([hx(x) for x in c["commits"]])
+    prs = c["partial_rounds"]
+    msgs = [hx(c["rounds"][k]["msg"]) for k in range(len(prs))]
+    parts = np.array([[list(hx(p)) for p in pr["partials"]] for pr in prs], np.uint8)
+    for seed in range(1, 41):
+        st = tbls.verify_partial_batch(pub, msgs, parts, seed=seed)
+        assert not st.any()
+        assert L.last_batch_flags() == (True, False), seed
