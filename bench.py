@@ -33,6 +33,17 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def traffic_of(kernel):
+    """HBM-side bytes per launch of `kernel` from the committed PMC passes (profiles/traffic.json, made by
+    tools/traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench): 2 x
+    FETCH_SIZE + WRITE_SIZE (the gfx950 correction of FETCH_SIZE), or None without a profile."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None
+    t = json.load(open(p)).get("kernels", {}).get(kernel)
+    return t["bytes_per_launch"] if t else None
+
+
 def load_chain(total):
     """(sigs (total, 96), prev_sig of round 1) for rounds 1..total of the synthetic chain."""
     best = None
@@ -115,13 +126,16 @@ def recover_bench(L, tbls, chain_sigs, first_round, R, t, n, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--rounds", type=int, default=100000, help="rounds per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--async", dest="use_async", action="store_true",
-                    help="enqueue the steps through dg_verify_beacons_dev_async (batches may overlap)")
+    ap.add_argument("--sync", dest="use_sync", action="store_true",
+                    help="blocking dg_verify_beacons_dev per step (default: dg_verify_beacons_dev_async, so the "
+                         "latency-bound tail of one batch overlaps the head of the next)")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="no per-kernel HIP events in the timed region (no roofline)")
     ap.add_argument("--recover-rounds", type=int, default=20000, help="0 disables the Recover line")
     args = ap.parse_args()
 
@@ -155,6 +169,7 @@ def main():
         data = "synthetic rounds, GPU-signed (no chain file: prev_sig pseudo-random, links not checked)"
         linked = False
     n = b - a
+    mbytes = (max(y - x for x, y in (shard.round_range(world * R, world, q) for q in range(world))) + 7) // 8
     rounds = np.arange(a + 1, b + 1, dtype=np.uint64)
     prev_sigs = [bytes(p) for p in prev]
     if a == 0 and linked:
@@ -165,14 +180,13 @@ def main():
     d_ps = torch.from_numpy(psb).to(dev)
     d_off = torch.from_numpy(off.astype(np.int32)).to(dev)
     d_sig = torch.from_numpy(np.ascontiguousarray(sigs)).to(dev)
-    # one status buffer per in-flight batch (the library rotates over 3 workspace sets)
-    nbuf = 3
+    # one status buffer per in-flight batch (the library rotates over DG_SETS = 4 workspace sets)
+    nbuf = 4
     d_sts = [torch.full((n,), 99, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
     gathered = [None] * nbuf
     side = torch.cuda.Stream(dev)
     pkb = ctypes.c_char_p(pk)
     counter = [0]
-    fallbacks = []  # seeds whose batch equation failed or isolated items (per-item pass ran)
 
     def step(seed):
         """Enqueue one batch (asynchronously: consecutive batches overlap) and the all-gather of its verdict
@@ -182,19 +196,16 @@ def main():
         if gathered[i] is not None:
             gathered[i][1].synchronize()  # the all-gather that read this status buffer has finished
         d_st = d_sts[i]
-        if not args.use_async:
+        if args.use_sync:
             L.check(lib.dg_verify_beacons_dev(pkb, n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off),
                                               L.ptr(d_sig), L.ptr(d_st), seed, None))
             side.wait_stream(torch.cuda.current_stream(dev))
-            ok, iso = L.last_batch_flags()  # the call has already waited for the batch
-            if not ok or iso:
-                fallbacks.append(seed)
         else:
             L.check(lib.dg_verify_beacons_dev_async(pkb, n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off),
                                                     L.ptr(d_sig), L.ptr(d_st), seed, None,
                                                     ctypes.c_void_p(side.cuda_stream)))
         with torch.cuda.stream(side):
-            bits = shard.allgather_verdicts(d_st, world)
+            bits = shard.allgather_verdicts(d_st, world, m=mbytes)
             ev = torch.cuda.Event()
             ev.record(side)
         gathered[i] = (bits, ev)
@@ -214,10 +225,11 @@ def main():
     assert bitmap.sum().item() == 0
     if world > 1:
         dist.barrier()
-    L.check(lib.dg_set_timing(1))
+    L.check(lib.dg_set_timing(0 if args.no_kernel_timing else 1))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    fb0 = L.fallback_count()
     t0 = time.perf_counter()
     bits = [step(17 + s) for s in range(args.steps)]
     drain()
@@ -226,7 +238,16 @@ def main():
     dt = time.perf_counter() - t0
     used = min(counter[0], nbuf)
     assert all(int(b.sum().item()) == 0 for b in bits) and all(int(d.max().item()) == 0 for d in d_sts[:used])
+    fallbacks = L.fallback_count() - fb0  # timed batches that ran the per-item pass (0 for valid chains)
     kt = L.timings()
+    # untimed: the same batch through the blocking entry point, so each kernel runs alone on the chip
+    # (inside the overlapped timed region a launch shares the CUs with the other batches in flight)
+    L.check(lib.dg_set_timing(0 if args.no_kernel_timing else 1))
+    for s in range(2):
+        L.check(lib.dg_verify_beacons_dev(pkb, n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off),
+                                          L.ptr(d_sig), L.ptr(d_sts[0]), 900 + s, None))
+    kt_iso = L.timings()
+    assert int(d_sts[0].max().item()) == 0
     L.check(lib.dg_set_timing(0))
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
@@ -236,17 +257,27 @@ def main():
     if rank == 0:
         oc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["per_unit"]
         # dominant kernel over the timed region
-        name, (us, launches) = max(kt.items(), key=lambda kv: kv[1][0] * kv[1][1])
+        name, (us, launches) = max(kt.items(), key=lambda kv: kv[1][0] * kv[1][1]) if kt else (None, (0, 0))
         per_launch_units = n
-        macs = oc.get(name, {}).get("macs")
+        macs = oc.get(name, {}).get("macs") if name else None
         peak = shard.mad_peak()
         roof = None
         if macs is not None:
             achieved = macs * per_launch_units / (us * 1e-6) / 1e12
             roof = {"bound": "valu-int", "achieved": achieved, "peak": peak["tmac_s"], "unit": "TMAC/s",
-                    "frac": achieved / peak["tmac_s"], "traffic": None, "kernel": name,
+                    "frac": achieved / peak["tmac_s"], "traffic": traffic_of(name), "kernel": name,
                     "kernel_avg_us": us, "units_per_launch": per_launch_units, "macs_per_unit": macs,
-                    "peak_source": peak["source"]}
+                    "peak_source": peak["source"],
+                    "note": "kernel_avg_us inside the overlapped timed region (other batches share the chip)"}
+            if name in kt_iso:
+                iso_us = kt_iso[name][0]
+                a_iso = macs * per_launch_units / (iso_us * 1e-6) / 1e12
+                roof["isolated"] = {"kernel_avg_us": iso_us, "achieved": a_iso, "frac": a_iso / peak["tmac_s"]}
+            # whole chip: algorithmic multiply-adds of the per-round work (hash, decode + subgroup check,
+            # 16 bucket additions of the two MSMs) over the step time; per-batch fixed work not counted
+            per_round = sum(oc[k]["macs"] for k in ("k_h2c_uncleared", "k_decode_items")) + 16 * oc["k_sum_rows"]["macs"]
+            chip = per_round * n * args.steps / dt / 1e12
+            roof["chip"] = {"macs_per_round": per_round, "achieved": chip, "frac": chip / peak["tmac_s"]}
         share = {k: round(v[0] * v[1] / (dt * 1e6 / 1.0), 4) for k, v in kt.items()}
         rec = None
         if args.recover_rounds and chain is not None:
@@ -262,9 +293,10 @@ def main():
                                       "shared group key (BASELINE configs[1]; configs[3] at N>1)" % n,
                           "rounds_per_gpu": n, "global_rounds": world * n, "parallelism": "rounds sharded dp%d" % world},
                "roofline": roof, "cpu_baseline": cpu, "recover": rec,
-               "batch_fallbacks": None if args.use_async else fallbacks,
+               "batch_fallbacks": fallbacks,
                "kernel_time_share": share,
-               "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()}}
+               "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
+               "kernel_avg_us_isolated": {k: round(v[0], 1) for k, v in kt_iso.items()}}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -47,6 +47,7 @@ SIGNATURES = {
     "dg_verify_beacons_dev_async": ([_P, _SZ, _P, _P, _P, _P, _P, _P, _U64, _P, _P], _I),
     "dg_wait_all": ([], _I),
     "dg_last_batch_flags": ([_P], _I),
+    "dg_fallback_count": ([_P], _I),
     "dg_set_timing": ([_I], _I),
     "dg_last_timings": ([_P, _P, _P, _I], _I),
 }
@@ -131,6 +132,13 @@ def last_batch_flags():
     out = np.zeros(2, dtype=np.uint32)
     check(lib().dg_last_batch_flags(ptr(out)))
     return bool(out[0]), bool(out[1])
+
+
+def fallback_count():
+    """Batches since dg_init that ran the per-item pass (batch equation failed or items isolated)."""
+    out = np.zeros(1, dtype=np.uint64)
+    check(lib().dg_fallback_count(ptr(out)))
+    return int(out[0])
 
 
 def timings():

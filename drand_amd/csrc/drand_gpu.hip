@@ -29,7 +29,10 @@ struct Timing {
 // A workspace set: its own stream, grow-only device buffers and completion event.  Batches enqueued
 // through the asynchronous entry point rotate over kSets sets, so the latency-bound tail of one batch
 // (Miller loops, final exponentiation: a few workgroups) overlaps the throughput-bound head of the next.
-constexpr int kSets = 3;
+#ifndef DG_SETS
+#define DG_SETS 4
+#endif
+constexpr int kSets = DG_SETS;
 struct Set {
   hipStream_t stream = nullptr;
   std::vector<void*> pool;  // indexed by Slot
@@ -55,6 +58,7 @@ struct Ctx {
   hipEvent_t pk_ready = nullptr;
   uint8_t pk_bytes[48];
   bool pk_valid = false;
+  unsigned long long* fallbacks = nullptr;  // device counter (k_count_fallback)
 };
 
 std::mutex g_mu;
@@ -123,7 +127,7 @@ hipEvent_t get_event() {
     return e;
   }
   hipEvent_t e;
-  hipEventCreate(&e);
+  (void)hipEventCreate(&e);
   return e;
 }
 
@@ -137,13 +141,13 @@ int launch(const char* name, void (*k)(Args...), uint32_t n_threads, uint32_t bl
   if (c.timing) {
     e0 = get_event();
     e1 = get_event();
-    hipEventRecord(e0, st);
+    (void)hipEventRecord(e0, st);
   }
   hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, st, args...);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(DG_E_HIP, std::string("launch ") + name + ": " + hipGetErrorString(e));
   if (c.timing) {
-    hipEventRecord(e1, st);
+    (void)hipEventRecord(e1, st);
     c.pending.push_back({e0, e1});
     c.pending_names.push_back(name);
   }
@@ -154,8 +158,8 @@ void collect_timings() {
   Ctx& c = g_ctx;
   for (size_t i = 0; i < c.pending.size(); ++i) {
     float ms = 0;
-    hipEventSynchronize(c.pending[i].second);
-    hipEventElapsedTime(&ms, c.pending[i].first, c.pending[i].second);
+    (void)hipEventSynchronize(c.pending[i].second);
+    (void)hipEventElapsedTime(&ms, c.pending[i].first, c.pending[i].second);
     bool found = false;
     for (auto& t : c.timings)
       if (t.name == c.pending_names[i]) {
@@ -321,6 +325,7 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, (const uint32_t*)flag, b.Q, H));
   RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
              (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status));
+  RET(launch("k_count_fallback", k_count_fallback, 1, 64, st, (const uint32_t*)flag, g_ctx.fallbacks));
   return 0;
 }
 
@@ -440,6 +445,10 @@ int dg_init(int device) {
     if (!x.stream) HIPCHK(hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking));
     if (!x.done) HIPCHK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
   }
+  if (!g_ctx.fallbacks) {
+    HIPCHK(hipMalloc(&g_ctx.fallbacks, sizeof(unsigned long long)));
+    HIPCHK(hipMemset(g_ctx.fallbacks, 0, sizeof(unsigned long long)));
+  }
   g_ctx.device = device;
   g_ctx.ready = true;
   return 0;
@@ -464,6 +473,8 @@ void dg_shutdown(void) {
   if (g_ctx.pk_status) (void)hipFree(g_ctx.pk_status);
   if (g_ctx.pk_raw) (void)hipFree(g_ctx.pk_raw);
   if (g_ctx.pk_ready) (void)hipEventDestroy(g_ctx.pk_ready);
+  if (g_ctx.fallbacks) (void)hipFree(g_ctx.fallbacks);
+  g_ctx.fallbacks = nullptr;
   g_ctx.pk_dev = nullptr;
   g_ctx.pk_status = nullptr;
   g_ctx.pk_raw = nullptr;
@@ -668,6 +679,17 @@ int dg_last_batch_flags(uint32_t* out2) {
   Set& set = cur_set();
   if (set.pool.size() < S_COUNT || !set.pool[S_FLAG]) return fail(DG_E_ARG, "no batch has run");
   HIPCHK(hipMemcpy(out2, set.pool[S_FLAG], 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int dg_fallback_count(uint64_t* out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  if (!out) return fail(DG_E_ARG, "bad arguments");
+  RET(wait_all());
+  unsigned long long v = 0;
+  HIPCHK(hipMemcpy(&v, g_ctx.fallbacks, sizeof(v), hipMemcpyDeviceToHost));
+  *out = v;
   return 0;
 }
 

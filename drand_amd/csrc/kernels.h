@@ -10,6 +10,12 @@
 #ifndef DG_HOT_WAVES
 #define DG_HOT_WAVES 2  // min waves per SIMD for the hot kernels: 256 VGPRs each (measured: 2 beats 1 by 6%)
 #endif
+#ifndef DG_BULK_WAVES
+#define DG_BULK_WAVES 1  // min waves per SIMD for the other per-lane group-arithmetic kernels
+#endif
+#ifndef DG_COOP_WAVES
+#define DG_COOP_WAVES 1  // min waves per SIMD for the cooperative (latency-bound) kernels
+#endif
 #ifndef DG_TU_HOT
 #define DG_TU_HOT 0  // 1 in kernels_hot.hip: only the hot kernels are defined there (DESIGN.md §code generation)
 #endif
@@ -247,7 +253,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_decode_items(uint32_t n, u
 
 // U_i = beta_slot S_i for batch items, O otherwise
 #if !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128) k_scale_items(uint32_t n, uint32_t nslots, uint64_t seed,
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_scale_items(uint32_t n, uint32_t nslots, uint64_t seed,
                                                     const uint32_t* item_slot, const G2AStore* S,
                                                     const uint8_t* status, const uint8_t* isolate, G2JStore* U) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -265,7 +271,7 @@ DG_KERNEL void __launch_bounds__(128) k_scale_items(uint32_t n, uint32_t nslots,
 // key slots also A_r = alpha_r Q_r (the per-key hash sums are masked by the cell map, so they are not a
 // single MSM); the alpha_r-weighted sums of V (and of Q with one key) are Pippenger MSMs (msm.h)
 #if !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128) k_round_combine(uint32_t R, uint32_t k, uint32_t nslots, uint64_t seed,
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_round_combine(uint32_t R, uint32_t k, uint32_t nslots, uint64_t seed,
                                                       const G2JStore* U, const uint8_t* status,
                                                       const uint8_t* isolate, const G2JStore* Q, G2JStore* V,
                                                       G2JStore* A, uint8_t* active) {
@@ -288,7 +294,7 @@ DG_KERNEL void __launch_bounds__(128) k_round_combine(uint32_t R, uint32_t k, ui
 
 // Kp[s * nchunks + c] = sum of A_r over rounds r in chunk c whose (r, s) cell holds a batch item
 #if !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128) k_key_accum(uint32_t R, uint32_t nslots, uint32_t chunk, uint32_t nchunks,
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_key_accum(uint32_t R, uint32_t nslots, uint32_t chunk, uint32_t nchunks,
                                                   const uint32_t* cell, const G2JStore* A, G2JStore* Kp) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nslots * nchunks) return;
@@ -303,7 +309,7 @@ DG_KERNEL void __launch_bounds__(128) k_key_accum(uint32_t R, uint32_t nslots, u
 
 // 2-D segmented sum: out[row * ocols + j] = sum_{c in [j*chunk, (j+1)*chunk) and < cols} in[row * cols + c]
 #if !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128) k_sum_rows(uint32_t rows, uint32_t cols, uint32_t chunk, const G2JStore* in,
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_sum_rows(uint32_t rows, uint32_t cols, uint32_t chunk, const G2JStore* in,
                                                  G2JStore* out) {
   uint32_t ocols = (cols + chunk - 1) / chunk;
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -322,7 +328,7 @@ DG_KERNEL void __launch_bounds__(128) k_sum_rows(uint32_t rows, uint32_t cols, u
 // Pairs: (beta_s X_s, h_eff K_s) for s < nslots, (-g1, T) for s == nslots; f[s] = 1
 // when a side is the identity.
 #if !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128) k_pair_miller_coop(uint32_t nslots, uint64_t seed, const G1AStore* keys,
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_pair_miller_coop(uint32_t nslots, uint64_t seed, const G1AStore* keys,
                                                          const G2JStore* K, const G2JStore* T, Fp12* f) {
   __shared__ CoGT gt;
   __shared__ CoML ml;
@@ -369,7 +375,7 @@ DG_KERNEL void __launch_bounds__(128) k_pair_miller_coop(uint32_t nslots, uint64
 
 // product of the npairs Miller values and one final exponentiation on one 128-lane workgroup
 #if !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128) k_final_coop(uint32_t npairs, const Fp12* f, uint32_t* ok) {
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_final_coop(uint32_t npairs, const Fp12* f, uint32_t* ok) {
   __shared__ CoGT gt;
   __shared__ Fp12W F, G, S[7];
   const int t = threadIdx.x;
@@ -393,7 +399,7 @@ DG_KERNEL void __launch_bounds__(128) k_final_coop(uint32_t npairs, const Fp12* 
 // H_r = h_eff(Q_r), affine (individual checks)
 // (skipped when the batch verified and nothing was isolated: flag[0] = batch ok, flag[1] = any isolated)
 #if !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128) k_clear_rounds(uint32_t R, const uint32_t* flag, const G2JStore* Q, G2AStore* H) {
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_clear_rounds(uint32_t R, const uint32_t* flag, const G2JStore* Q, G2AStore* H) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R || (flag[0] && !flag[1])) return;
   store_g2a(H[r], g2_to_aff(g2_clear_cofactor(load_g2j(Q[r]))));
@@ -436,6 +442,11 @@ DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, cons
 DG_KERNEL void __launch_bounds__(256) k_any(uint32_t n, const uint8_t* v, uint32_t* flag) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n && v[i]) atomicOr(flag, 1u);
+}
+// batches whose random-linear-combination check failed or that isolated items (the per-item pass ran):
+// stream-ordered diagnostics counter, read with dg_fallback_count
+DG_KERNEL void __launch_bounds__(64) k_count_fallback(const uint32_t* flag, unsigned long long* counter) {
+  if (threadIdx.x == 0 && (!flag[0] || flag[1])) atomicAdd(counter, 1ull);
 }
 #endif
 

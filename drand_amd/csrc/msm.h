@@ -84,7 +84,7 @@ DG_KERNEL void __launch_bounds__(256) k_msm_scatter(uint32_t R, uint64_t seed, c
 
 // lane g: side = g / max_chunks, chunk c = g % max_chunks; sums its chunk of points of side `side`
 // (side 0: PA, side 1: PB) into out[side * max_chunks + c]
-DG_KERNEL void __launch_bounds__(128) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, const uint32_t* count,
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, const uint32_t* count,
                                                    const uint32_t* offset, const uint32_t* chunk_off,
                                                    const uint32_t* list, const G2JStore* PA, const G2JStore* PB,
                                                    G2JStore* out) {
@@ -113,7 +113,7 @@ DG_KERNEL void __launch_bounds__(128) k_msm_chunks(uint32_t max_chunks, uint32_t
 
 // lane g: side, bucket b, lane-in-bucket q < MSM_BSPLIT: strided partial sum of the bucket's chunks,
 // BP[(side * NBK + b) * MSM_BSPLIT + q]; the MSM_BSPLIT partials are then row-summed into B[side][b]
-DG_KERNEL void __launch_bounds__(128) k_msm_buckets(uint32_t max_chunks, uint32_t nsides, const uint32_t* chunk_off,
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_buckets(uint32_t max_chunks, uint32_t nsides, const uint32_t* chunk_off,
                                                     const G2JStore* chunks, G2JStore* BP) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= MSM_NBK * MSM_BSPLIT * nsides) return;
@@ -127,7 +127,7 @@ DG_KERNEL void __launch_bounds__(128) k_msm_buckets(uint32_t max_chunks, uint32_
 
 // Bucket aggregation by bit slices: sum_b b B_b = sum_k 2^k S_k with S_k = sum of the buckets whose
 // digit b has bit k set (128 of the 255).  Level 1: lane (side, w, k, c < 16) sums 8 of those buckets.
-DG_KERNEL void __launch_bounds__(128) k_msm_slices(uint32_t nsides, const G2JStore* B, G2JStore* P1) {
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_slices(uint32_t nsides, const G2JStore* B, G2JStore* P1) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nsides * MSM_WIN * MSM_C * 16) return;
   uint32_t c = g % 16, k = (g / 16) % MSM_C, w = (g / (16 * MSM_C)) % MSM_WIN, side = g / (16 * MSM_C * MSM_WIN);
@@ -143,7 +143,7 @@ DG_KERNEL void __launch_bounds__(128) k_msm_slices(uint32_t nsides, const G2JSto
 
 // one 128-lane workgroup per (side, window): W_w = sum_k 2^k S_{w,k} (Horner with cooperative doublings
 // and additions, coop.h), then 2^(8w) W_w
-DG_KERNEL void __launch_bounds__(128) k_msm_horner_coop(const G2JStore* S, G2JStore* Wout) {
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_horner_coop(const G2JStore* S, G2JStore* Wout) {
   __shared__ CoG2Tmp tmp;
   __shared__ CoG2 acc, nxt;
   const uint32_t sw = blockIdx.x, w = sw % MSM_WIN;
@@ -165,7 +165,7 @@ DG_KERNEL void __launch_bounds__(128) k_msm_horner_coop(const G2JStore* S, G2JSt
 }
 
 // one 128-lane workgroup per side: out[side] = sum_w W[side][w]
-DG_KERNEL void __launch_bounds__(128) k_msm_final_coop(const G2JStore* W, G2JStore* out) {
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_final_coop(const G2JStore* W, G2JStore* out) {
   __shared__ CoG2Tmp tmp;
   __shared__ CoG2 acc, nxt;
   const uint32_t side = blockIdx.x;

@@ -25,21 +25,27 @@ def pack_bits(status):
     pad = (-bad.numel()) % 8
     if pad:
         bad = torch.cat([bad, torch.zeros(pad, dtype=torch.uint8, device=bad.device)])
-    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=bad.device)
-    return (bad.view(-1, 8) * w).sum(dim=1).to(torch.uint8)
+    # bit weights made on the device (a host-built tensor would be a blocking copy on the current stream,
+    # which serialises it with the batch it waits for)
+    shift = torch.arange(8, dtype=torch.uint8, device=bad.device)
+    return (bad.view(-1, 8) << shift).sum(dim=1).to(torch.uint8)
 
 
-def allgather_verdicts(status, world, group=None):
-    """All-gather every rank's packed verdict bitmap (equal-size shards padded to the largest)."""
+def allgather_verdicts(status, world, group=None, m=None):
+    """All-gather every rank's packed verdict bitmap (equal-size shards padded to the largest).
+
+    m = bitmap bytes of the largest shard; when the caller knows it (round_range makes the shard sizes a
+    function of the global size), no host round trip is needed and the gather stays stream-ordered."""
     import torch
     import torch.distributed as dist
 
     bits = pack_bits(status)
     if world == 1:
         return bits
-    n = torch.tensor([bits.numel()], device=bits.device, dtype=torch.int64)
-    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
-    m = int(n.item())
+    if m is None:
+        n = torch.tensor([bits.numel()], device=bits.device, dtype=torch.int64)
+        dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+        m = int(n.item())
     if bits.numel() < m:
         bits = torch.cat([bits, torch.zeros(m - bits.numel(), dtype=torch.uint8, device=bits.device)])
     if dist.get_backend(group) == "nccl":  # RCCL on ROCm

@@ -125,6 +125,9 @@ int dg_verify_beacons_dev_async(const uint8_t* pk48_host, size_t n, const uint64
  * batch equation held, out2[1] = 1 if some item was checked on its own (duplicate key cell).  A valid
  * batch must pass on the batch path; the per-item fallback only decides failures. */
 int dg_last_batch_flags(uint32_t* out2);
+/* Number of batches since dg_init whose batch equation failed or that isolated items, i.e. ran the
+ * per-item pass (waits for batches in flight).  A stream of valid batches keeps it at 0. */
+int dg_fallback_count(uint64_t* out);
 /* Wait for every batch enqueued by the asynchronous entry points. */
 int dg_wait_all(void);
 
