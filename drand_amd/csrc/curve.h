@@ -141,13 +141,14 @@ DGH bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
   return f_eq(f_mul(f_mul(p.y, q.z), Z2Z2), f_mul(f_mul(q.y, p.z), Z1Z1));
 }
 
-// [k]P for a 64-bit scalar (double-and-add, MSB first)
+// [k]P for a 64-bit scalar (double-and-add, MSB first); mixed additions when P has Z = 1
 template <class F>
 DGH Jac<F> jac_mul_u64(const Jac<F>& p, uint64_t k) {
+  const bool aff = f_eq(p.z, f_one_of(F{}));
   Jac<F> acc = jac_infinity<F>();
   for (int b = 63; b >= 0; --b) {
     acc = jac_dbl(acc);
-    if ((k >> b) & 1) acc = jac_add(acc, p);
+    if ((k >> b) & 1) acc = aff ? jac_add_aff(acc, p.x, p.y) : jac_add(acc, p);
   }
   return acc;
 }
@@ -188,6 +189,21 @@ DGH G2J g2_psi(const G2J& p) {
 DGI G2J g2_mul_z(const G2J& p) { return jac_neg(jac_mul_u64(p, Z_ABS)); }
 // P in G2  <=>  psi(P) == [z]P   (Scott, "A note on group membership tests for G1, G2 and GT")
 DGH bool g2_in_subgroup(const G2J& p) { return jac_eq(g2_psi(p), g2_mul_z(p)); }
+// the same test for an affine point (decoded signatures): [|z|]P by double-and-add from the top bit with
+// mixed additions (P has Z = 1), psi(P) affine, and a Z1 = 1 comparison
+DGH bool g2_in_subgroup_aff(const Fp2& x, const Fp2& y) {
+  G2J acc{x, y, fp2_one()};
+  for (int b = 62; b >= 0; --b) {
+    acc = jac_dbl(acc);
+    if ((Z_ABS >> b) & 1) acc = jac_add_aff(acc, x, y);
+  }
+  // [z]P = -acc; psi(P) = (conj(x) cx, conj(y) cy) affine
+  if (jac_is_inf(acc)) return false;  // psi(P) is never the identity for an affine P
+  Fp2 px = fp2_mul(fp2_conj(x), fp2_const(PSI_CX)), py = fp2_mul(fp2_conj(y), fp2_const(PSI_CY));
+  Fp2 zz = fp2_sqr(acc.z);
+  if (!fp2_eq(fp2_mul(px, zz), acc.x)) return false;
+  return fp2_eq(fp2_mul(py, fp2_mul(zz, acc.z)), fp2_neg(acc.y));
+}
 // RFC 9380 Appendix G.3 (Budroni-Pintore): h_eff * P = [z^2 - z - 1]P + [z - 1]psi(P) + psi^2(2P)
 DGH G2J g2_clear_cofactor(const G2J& p) {
   G2J t1 = g2_mul_z(p);
@@ -255,7 +271,7 @@ DGH bool g2_decompress(G2A& out, const uint8_t* in, bool subgroup_check) {
   if (!fp2_sqrt(y, rhs)) return false;
   if (((f & 0x20) != 0) != fp2_lex_largest(y)) y = fp2_neg(y);
   out = G2A{x, y, false};
-  if (subgroup_check && !g2_in_subgroup(jac_from_aff(out))) return false;
+  if (subgroup_check && !g2_in_subgroup_aff(x, y)) return false;
   return true;
 }
 DGI void g1_compress_aff(uint8_t* out, const G1A& a) {

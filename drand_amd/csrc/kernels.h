@@ -136,7 +136,9 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_h2c_uncleared(uint32_t n, 
                                                       const uint8_t* dst, uint32_t dst_len, G2JStore* outQ) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  store_g2j(outQ[i], hash_to_g2_uncleared(msgs + (size_t)msg_len * i, msg_len, dst, dst_len));
+  // normalised to Z = 1 (one safegcd inversion): the MSM and the scalar multiplications downstream
+  // then use mixed additions
+  store_g2j(outQ[i], jac_from_aff(g2_to_aff(hash_to_g2_uncleared(msgs + (size_t)msg_len * i, msg_len, dst, dst_len))));
 }
 #else
 DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_h2c_uncleared(uint32_t n, const uint8_t* msgs, uint32_t msg_len,

@@ -7,10 +7,13 @@
 //   2. k_msm_scan     bucket offsets and per-bucket chunk offsets (one workgroup)
 //   3. k_msm_scatter  round indices into bucket order (atomics: order inside a bucket is arbitrary,
 //                     sums are exact group elements, so the result does not depend on it)
-//   4. k_msm_chunks   each lane sums one chunk of <= MSM_CHUNK points of one bucket
-//   5. k_msm_buckets  each lane sums the chunks of one bucket
-//   6. k_msm_groups   running sums over groups of 17 buckets: sum_b (b - lo + 1) B_b + (lo - 1) sum_b B_b
-//   7. k_msm_windows  per window: sum of its groups, times 2^(8w); then the 8 window terms are summed
+//   4. k_msm_chunks       each lane sums one chunk of <= MSM_CHUNK points of one bucket (mixed additions
+//                         for Z = 1 inputs)
+//   5. k_msm_buckets      MSM_BSPLIT lanes per bucket sum its chunks strided; k_sum_rows folds the partials
+//   6. k_msm_slices       bucket aggregation by bit slices: sum_b b B_b = sum_k 2^k S_k, S_k = sum of the
+//                         buckets whose digit has bit k set (16 lanes per (window, k), then k_sum_rows)
+//   7. k_msm_horner_coop  per window, cooperatively (coop.h): W_w = sum_k 2^k S_k, times 2^(8w)
+//   8. k_msm_final_coop   the sum of the 8 window terms
 // Work: 8 bucket additions per point instead of a 64-bit double-and-add (64 doublings + 64 divergent
 // additions) per point.
 #pragma once
@@ -107,7 +110,15 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_chunks(uint32_t max_c
   if (last > first + MSM_CHUNK) last = first + MSM_CHUNK;
   const G2JStore* P = side ? PB : PA;
   G2J acc = load_g2j(P[list[first]]);
-  for (uint32_t i = first + 1; i < last; ++i) acc = jac_add(acc, load_g2j(P[list[i]]));
+  const Fp2 one = fp2_one();
+  for (uint32_t i = first + 1; i < last; ++i) {
+    const G2JStore& q = P[list[i]];
+    // decoded signatures enter with Z = 1: mixed addition (7M + 4S instead of 11M + 5S in Fp2)
+    if (fp2_eq(q.z, one))
+      acc = jac_add_aff(acc, q.x, q.y);
+    else
+      acc = jac_add(acc, load_g2j(q));
+  }
   store_g2j(out[side * max_chunks + c], acc);
 }
 

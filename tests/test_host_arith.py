@@ -40,3 +40,26 @@ def test_hash_to_g2_host_build_matches_golden(hc):
         m = hx(x["msg"])
         hc.hc_hash_to_g2(m, len(m), dst, len(dst), out)
         assert out.raw.hex() == x["h"]
+
+
+def test_g2_decode_edges_host_build(hc):
+    """ZCash decode + the affine psi subgroup check (curve.h g2_in_subgroup_aff) on the committed edge cases."""
+    for c in load("g2_decode_edges.json")["cases"]:
+        out = ctypes.create_string_buffer(96)
+        assert bool(hc.hc_g2_roundtrip(hx(c["enc"]), out)) == c["decodes"], c["name"]
+
+
+def test_g2_subgroup_check_host_build_matches_pyref(hc):
+    """Uncleared hash outputs (on the curve, almost never in G2) and cleared ones (in G2): the device
+    decode's subgroup verdict equals the pyref's [r]P == O test."""
+    dst = B.DST_G2
+    for i in range(6):
+        m = b"subgroup %d" % i
+        for pt, in_g2 in ((B.hash_to_g2_uncleared(m, dst), None), (B.hash_to_g2(m, dst), True)):
+            enc = B.g2_compress(pt)
+            want = B.g2_in_subgroup(pt) if in_g2 is None else in_g2
+            out = ctypes.create_string_buffer(96)
+            got = bool(hc.hc_g2_roundtrip(enc, out))
+            assert got == want, (i, want)
+            if got:
+                assert out.raw == enc

@@ -22,7 +22,7 @@ extern "C" {
 // out[0..1] = (mul, sqr) of hash_to_g2_uncleared(msg) -- k_h2c_uncleared per round
 void oc_h2c_uncleared(const uint8_t* msg, uint32_t len, const uint8_t* dst, uint32_t dl, uint64_t* out) {
   reset();
-  G2J q = hash_to_g2_uncleared(msg, len, dst, dl);
+  G2J q = jac_from_aff(g2_to_aff(hash_to_g2_uncleared(msg, len, dst, dl)));  // as k_h2c_uncleared stores it
   (void)q;
   take(out);
 }
@@ -37,7 +37,7 @@ int oc_decode_g2(const uint8_t* sig96, uint64_t* out) {
 // k_round_combine per round (k = 1): W = alpha sigma, A = alpha Q (Q = uncleared hash of msg)
 void oc_round_combine(const uint8_t* msg, uint32_t len, const uint8_t* dst, uint32_t dl, const uint8_t* sig96,
                       uint64_t alpha, uint64_t* out) {
-  G2J q = hash_to_g2_uncleared(msg, len, dst, dl);
+  G2J q = jac_from_aff(g2_to_aff(hash_to_g2_uncleared(msg, len, dst, dl)));
   G2A s;
   g2_decompress(s, sig96, true);
   reset();
@@ -55,6 +55,17 @@ void oc_g2_add(const uint8_t* sig_a, const uint8_t* sig_b, uint64_t* out) {
   G2J ja = jac_dbl(jac_from_aff(a)), jb = jac_dbl(jac_from_aff(b));  // generic Z != 1
   reset();
   G2J c = jac_add(ja, jb);
+  (void)c;
+  take(out);
+}
+// one mixed addition (Jacobian + affine): k_msm_chunks per decoded signature
+void oc_g2_add_aff(const uint8_t* sig_a, const uint8_t* sig_b, uint64_t* out) {
+  G2A a, b;
+  g2_decompress(a, sig_a, false);
+  g2_decompress(b, sig_b, false);
+  G2J ja = jac_dbl(jac_from_aff(a));
+  reset();
+  G2J c = jac_add_aff(ja, b.x, b.y);
   (void)c;
   take(out);
 }

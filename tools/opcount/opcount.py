@@ -50,6 +50,8 @@ def main():
         nxt = bytes.fromhex(rounds[(i + 1) % len(rounds)]["sig"])
         L.oc_g2_add(sig, nxt, o)
         add("k_sum_rows")
+        L.oc_g2_add_aff(sig, nxt, o)
+        add("k_msm_chunks[mixed add]")
         lam = (ctypes.c_uint32 * 8)(*[int.from_bytes(hashlib.sha256(b"l%d%d" % (i, w)).digest()[:4], "little")
                                       for w in range(7)] + [0x3fffffff])
         L.oc_recover_term(sig, lam, o)
