@@ -123,6 +123,59 @@ def recover_bench(L, tbls, chain_sigs, first_round, R, t, n, steps):
                     "recovered signatures equal the chain's" % (R * n * 98 // 10**6)}
 
 
+def adversarial_bench(L, tbls, chain_sigs, R, t=129, n=256, frac=0.10, n_short=3):
+    """BASELINE configs C5: n = 256, t = 129, R rounds, ~10% of the (round, share) cells
+    corrupted with the six cycling modes of tools/corrupt.py, plus `n_short` rounds with more than n - t
+    corrupted shares (-> "not enough shares").  One dg_recover over all R x n partials (VerifyPartial on
+    every share -- the batch equation fails, so every share takes the exact per-item check -- then
+    Recover).  Checked without the CPU: recovered signatures equal the chain's, exactly the short rounds
+    report NOT_ENOUGH, every examined corrupted share is rejected and every examined clean one accepted
+    (per-share parity with the CPU twin is tests/test_gpu_parity.py's job)."""
+    from tools import corrupt
+
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "groups.json")))["t%d" % t]
+    pub = tbls.PubPoly([bytes.fromhex(c) for c in g])
+    coeffs = S.poly_coeffs(t)
+    shares = [S.share_value(coeffs, i) for i in range(n)]
+    rounds = np.arange(1, R + 2, dtype=np.uint64)  # one extra round for the "other_round" mode
+    prev = [S.GENESIS_SEED] + [bytes(chain_sigs[r - 2]) for r in rounds.tolist()[1:]]
+    msgs_all = tbls.beacon_messages(rounds - 1, rounds, prev)
+    msgs = msgs_all[:R]
+    t0 = time.perf_counter()
+    parts = tbls.sign_batch([shares[i] for _ in range(R) for i in range(n)], np.repeat(msgs, n, axis=0),
+                            [i for _ in range(R) for i in range(n)]).reshape(R, n, 98)
+    items = corrupt.pick(R, n, frac)
+    short = set(range(n_short))
+    items = [it for it in items if it[0] not in short] + [(r, j, "random_bytes") for r in short
+                                                           for j in range(n - t + 2)]
+
+    def resign(reqs):
+        sc = [shares[idx] + ds for _, idx, ds, _ in reqs]
+        return tbls.sign_batch(sc, np.stack([msgs_all[r + dr] for r, _, _, dr in reqs]))
+
+    corrupt.corrupt_batch(parts, items, n, resign)
+    gen_s = time.perf_counter() - t0
+    bad = np.zeros((R, n), dtype=bool)
+    for r, j, _ in items:
+        bad[r, j] = True
+    sigs, rs, ss = tbls.recover_batch(pub, msgs, parts, t, n, seed=11)  # warmup + check
+    ok_r = np.array([r not in short for r in range(R)])
+    assert np.array_equal(rs != 0, ~ok_r) and (rs[~ok_r] == 5).all(), "round statuses"
+    assert np.array_equal(sigs[ok_r], chain_sigs[:R][ok_r]), "recovered signatures differ from the chain"
+    examined = ss != 255
+    assert (ss[examined & bad] != 0).all() and (ss[examined & ~bad] == 0).all(), "share statuses"
+    t0 = time.perf_counter()
+    tbls.recover_batch(pub, msgs, parts, t, n, seed=12)
+    dt = time.perf_counter() - t0
+    return {"metric": "adversarial Recover/s at n=%d t=%d, %.0f%% of shares corrupted (C5)" % (n, t, 100 * frac),
+            "value": R / dt, "unit": "recovers/s", "rounds": R, "partials_per_round": n,
+            "corrupted_shares": int(bad.sum()), "short_rounds": n_short, "s_per_step": dt,
+            "partials_verified_per_s": R * n / dt, "setup_s": gen_s,
+            "note": "host-buffer C-ABI (dg_recover), PCIe transfer of %d MB of partials inside the timed region; "
+                    "every batch fails its RLC check, so all shares take the per-item pairing check"
+                    % (R * n * 98 // 10**6)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,6 +190,7 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no per-kernel HIP events in the timed region (no roofline)")
     ap.add_argument("--recover-rounds", type=int, default=20000, help="0 disables the Recover line")
+    ap.add_argument("--c5-rounds", type=int, default=10000, help="0 disables the adversarial (C5) line")
     args = ap.parse_args()
 
     import torch
@@ -284,6 +338,9 @@ def main():
         rec = None
         if args.recover_rounds and chain is not None:
             rec = recover_bench(L, tbls, chain, 1, min(args.recover_rounds, len(chain)), 33, 64, 1)
+        adv = None
+        if args.c5_rounds and chain is not None:
+            adv = adversarial_bench(L, tbls, chain, min(args.c5_rounds, len(chain) - 1))
         cpu = None
         if not args.no_cpu_baseline:
             m = tbls.beacon_messages(rounds[:4096] - 1, rounds[:4096], prev_sigs[:4096])
@@ -294,7 +351,7 @@ def main():
                "config": {"workload": "batch bls.Verify / beacon.VerifyBeacon of %d linked chain rounds per GPU, one "
                                       "shared group key (BASELINE configs[1]; configs[3] at N>1)" % n,
                           "rounds_per_gpu": n, "global_rounds": world * n, "parallelism": "rounds sharded dp%d" % world},
-               "roofline": roof, "cpu_baseline": cpu, "recover": rec,
+               "roofline": roof, "cpu_baseline": cpu, "recover": rec, "adversarial": adv,
                "batch_fallbacks": fallbacks,
                "kernel_time_share": share,
                "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},

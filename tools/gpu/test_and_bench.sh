@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --recover-rounds 0 --steps ${BENCH_STEPS:-12} $BENCH_FLAGS > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --recover-rounds 0 --c5-rounds 0 --steps ${BENCH_STEPS:-12} $BENCH_FLAGS > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
 python - <<'PY'
 import json
 d = json.loads(open("gpurun_out/bench.json").read().strip().splitlines()[-1])
