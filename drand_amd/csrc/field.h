@@ -1,9 +1,8 @@
 // BLS12-381 field tower for the HIP kernels (gfx950), one field element per lane.
 //
-// Fp:  12 x 32-bit limbs, Montgomery form (R = 2^384), values kept fully reduced in [0, p).
-//      Multiplication is CIOS with the "no final carry" shortcut (p's top limb 0x1a0111ea < 2^31 - 1),
-//      every 32x32+32+32 step is one v_mad_u64_u32 on gfx950 (full issue rate, see
-//      tools/microbench/intmul.hip and DESIGN.md §roofline).
+// Fp:  12 x 32-bit limbs, Montgomery form (R = 2^392), values kept fully reduced in [0, p).
+//      Multiplication scans 14 digits of 28 bits with carry-free 64-bit column sums (fp28.h): one
+//      v_mad_u64_u32 per partial product on gfx950.
 // Fp2 = Fp[u]/(u^2+1), Fp6 = Fp2[v]/(v^3 - xi), Fp12 = Fp6[w]/(w^2 - v), xi = 1 + u.
 //
 // This restates the arithmetic of the reference's pairing suite (github.com/drand/bls12-381 v0.2.0,
@@ -32,7 +31,7 @@
 #endif
 
 #include "bls_constants.h"
-#include "fp_asm.h"
+#include "fp28.h"
 
 namespace dg {
 
@@ -143,44 +142,30 @@ DGI Fp fp_neg(const Fp& a) {
   return fp_sel(fp_is_zero(a), d, a);
 }
 
-// Host CIOS (tests/native and tools/opcount only): no extra carry word (valid since p[11] < 2^31 - 1).
-DGI Fp fp_mul_cios(const Fp& a, const Fp& b) {
-  uint32_t t[12];
-#pragma unroll
-  for (int j = 0; j < 12; ++j) t[j] = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t p = (uint64_t)a.l[0] * b.l[i] + t[0];
-    uint32_t A = (uint32_t)(p >> 32);
-    uint32_t t0 = (uint32_t)p;
-    uint32_t m = t0 * P_INV32;
-    uint64_t q = (uint64_t)m * P_LIMBS[0] + t0;
-    uint32_t C = (uint32_t)(q >> 32);
-#pragma unroll
-    for (int j = 1; j < 12; ++j) {
-      p = (uint64_t)a.l[j] * b.l[i] + t[j] + A;
-      A = (uint32_t)(p >> 32);
-      q = (uint64_t)m * P_LIMBS[j] + (uint32_t)p + C;
-      C = (uint32_t)(q >> 32);
-      t[j - 1] = (uint32_t)q;
-    }
-    t[11] = C + A;
-  }
+// Montgomery multiplication / squaring (fp28.h), then one conditional subtraction.
+DGI Fp fp28_mul(const Fp& a, const Fp& b) {
   Fp r;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) r.l[j] = t[j];
+  fp28_mont_mul(a.l, b.l, r.l);
   return fp_reduce_once(r);
 }
-
-// Montgomery multiplication / squaring.  Device: one product-scanning inline-asm block each
-// (tools/gen_fp_asm.py: 288 / 222 v_mad_u64_u32).  DG_FP_CALL selects how callers reach it:
-//   0  out-of-line, operands by reference (through the stack)
+DGI Fp fp28_sqr(const Fp& a) {
+  Fp r;
+  fp28_mont_sqr(a.l, r.l);
+  return fp_reduce_once(r);
+}
+// How device callers reach it (DG_FP_CALL):
 //   1  out-of-line, the 24 operand limbs passed as scalar arguments (VGPRs), result returned in VGPRs
 //   2  inlined at every call site
+// fp_mul_inl / fp_sqr_inl are always inlined: the innermost loops (exponentiation chains, the per-lane
+// products of the cooperative phases in coop.h).  Host builds (tests/native, tools/opcount) inline
+// everything and count the calls (DG_OPCOUNT).
 #ifndef DG_FP_CALL
 #define DG_FP_CALL 1
 #endif
-#if defined(DG_FP_ASM) && DG_FP_CALL == 1
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp28_mul(a, b); }
+__device__ __forceinline__ Fp fp_sqr_inl(const Fp& a) { return fp28_sqr(a); }
+#if DG_FP_CALL == 1
 #define DG_L12(p) p##0, p##1, p##2, p##3, p##4, p##5, p##6, p##7, p##8, p##9, p##10, p##11
 #define DG_P12(p)                                                                                      \
   uint32_t p##0, uint32_t p##1, uint32_t p##2, uint32_t p##3, uint32_t p##4, uint32_t p##5, uint32_t p##6, \
@@ -189,59 +174,30 @@ DGI Fp fp_mul_cios(const Fp& a, const Fp& b) {
 __device__ __noinline__ Fp fp_mul_r(DG_P12(a), DG_P12(b)) {
   const uint32_t a[12] = {DG_L12(a)}, b[12] = {DG_L12(b)};
   Fp r;
-  fp_mont_mul_asm(r.l, a, b, P_LIMBS, P_INV32);
+  fp28_mont_mul(a, b, r.l);
   return fp_reduce_once(r);
 }
 __device__ __noinline__ Fp fp_sqr_r(DG_P12(a)) {
   const uint32_t a[12] = {DG_L12(a)};
   Fp r;
-  fp_mont_sqr_asm(r.l, a, P_LIMBS, P_INV32);
+  fp28_mont_sqr(a, r.l);
   return fp_reduce_once(r);
 }
 DGI Fp fp_mul(const Fp& a, const Fp& b) { return fp_mul_r(DG_A12(a), DG_A12(b)); }
 DGI Fp fp_sqr(const Fp& a) { return fp_sqr_r(DG_A12(a)); }
 #else
-#if defined(DG_FP_ASM) && DG_FP_CALL == 2
-#define DGF DGI
-#else
-#define DGF DGN
+DGI Fp fp_mul(const Fp& a, const Fp& b) { return fp28_mul(a, b); }
+DGI Fp fp_sqr(const Fp& a) { return fp28_sqr(a); }
 #endif
-DGF Fp fp_mul(const Fp& a, const Fp& b) {
+#else
+DGI Fp fp_mul(const Fp& a, const Fp& b) {
   DG_COUNT_MUL();
-#if defined(DG_FP_ASM)
-  Fp r;
-  fp_mont_mul_asm(r.l, a.l, b.l, P_LIMBS, P_INV32);
-  return fp_reduce_once(r);
-#else
-  return fp_mul_cios(a, b);
-#endif
+  return fp28_mul(a, b);
 }
-DGF Fp fp_sqr(const Fp& a) {
+DGI Fp fp_sqr(const Fp& a) {
   DG_COUNT_SQR();
-#if defined(DG_FP_ASM)
-  Fp r;
-  fp_mont_sqr_asm(r.l, a.l, P_LIMBS, P_INV32);
-  return fp_reduce_once(r);
-#else
-  return fp_mul_cios(a, a);
-#endif
+  return fp28_sqr(a);
 }
-#endif
-
-// Inlined variants for the innermost loops (exponentiation chains, the per-lane products of the
-// cooperative phases in coop.h): no call, operands stay in registers.
-#if defined(DG_FP_ASM)
-__device__ __forceinline__ Fp fp_mul_inl(const Fp& a, const Fp& b) {
-  Fp r;
-  fp_mont_mul_asm(r.l, a.l, b.l, P_LIMBS, P_INV32);
-  return fp_reduce_once(r);
-}
-__device__ __forceinline__ Fp fp_sqr_inl(const Fp& a) {
-  Fp r;
-  fp_mont_sqr_asm(r.l, a.l, P_LIMBS, P_INV32);
-  return fp_reduce_once(r);
-}
-#else
 DGI Fp fp_mul_inl(const Fp& a, const Fp& b) { return fp_mul(a, b); }
 DGI Fp fp_sqr_inl(const Fp& a) { return fp_sqr(a); }
 #endif
@@ -296,8 +252,6 @@ struct S30 {
 DG_CONST int32_t P30[S30_N] = {1073719979, 670826495, 356515835, 721420204, 821437470, 55215066, 288093811,
                                 316751073, 752313463, 517541166, 698659258, 982409209, 1704209};
 DG_CONST uint32_t P_INV30 = 0x30003u;  // p^-1 mod 2^30
-DG_CONST uint32_t FP_R3[12] = {0xd94ca1e0u, 0xed48ac6bu, 0x03a7adf8u, 0x315f831eu, 0x615e29ddu, 0x9a53352au,
-                               0x921e1761u, 0x34c04e5eu, 0x65724728u, 0x2512d435u, 0x91755d4du, 0x0aa63460u};  // R^3 mod p
 
 DGI int32_t s30_divsteps(int32_t zeta, uint32_t f, uint32_t g, int32_t& tu, int32_t& tv, int32_t& tq, int32_t& tr) {
   uint32_t u = 1, v = 0, q = 0, r = 1;

@@ -1,7 +1,8 @@
 """Per-unit Montgomery multiplication/squaring counts of each verify-path kernel, from the instrumented
 host build of the device arithmetic (liboc.so), averaged over the committed 64-round chain fixture.
 Writes profiles/opcounts.json, which bench.py reads to convert kernel time into multiply-adds/s.
-MACs: one fp_mul = 288 v_mad_u64_u32, one fp_sqr = 222 (counted in drand_amd/csrc/fp_asm.h)."""
+MACs: one fp_mul = 288, one fp_sqr = 222 -- the 32x32-bit multiply-adds of a 12-limb Montgomery product
+(the algorithmic unit; the radix-2^28 kernels of fp28.h execute 392 / 301 narrower ones)."""
 import ctypes
 import hashlib
 import json
