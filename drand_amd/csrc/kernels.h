@@ -510,8 +510,7 @@ DG_KERNEL void __launch_bounds__(64) k_recover_terms(uint32_t R, uint32_t k, uin
     return;
   }
   Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, m);
-  G2J p = jac_from_aff(load_g2a(S[(size_t)r * k + sel[g]]));
-  store_g2j(terms[g], jac_mul_u256(p, lam.l));
+  store_g2j(terms[g], g2_mul_u256_psi(load_g2a(S[(size_t)r * k + sel[g]]), lam.l));
 }
 #endif
 
@@ -541,7 +540,7 @@ DG_KERNEL void __launch_bounds__(128) k_sign(uint32_t n, const uint8_t* sc32, co
     kl[w] = (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | q[3];
   }
   G2J h = hash_to_g2(msgs + (size_t)msg_len * i, msg_len, dst, dst_len);
-  G2A sig = g2_to_aff(jac_mul_u256(h, kl));
+  G2A sig = g2_to_aff(g2_mul_u256_psi(g2_to_aff(h), kl));
   uint32_t rec = index ? 98u : 96u;
   uint8_t* o = out + (size_t)rec * i;
   if (index) {

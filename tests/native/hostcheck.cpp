@@ -102,3 +102,12 @@ extern "C" void hc_fp_inv(const uint8_t* a48, uint8_t* out_sg48, uint8_t* out_fe
   fp_to_be48(out_sg48, fp_inv(m));
   fp_to_be48(out_fermat48, fp_inv_fermat(m));
 }
+
+// [k]P two ways: psi-decomposed Straus (g2_mul_u256_psi) and 255-bit double-and-add; 1 if they agree
+extern "C" int hc_g2_mul_psi_check(const uint8_t* sig96, const uint32_t* k8) {
+  G2A a;
+  if (!g2_decompress(a, sig96, true)) return -1;
+  G2J u = g2_mul_u256_psi(a, k8);
+  G2J v = jac_mul_u256(jac_from_aff(a), k8);
+  return jac_eq(u, v) ? 1 : 0;
+}

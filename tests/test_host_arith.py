@@ -63,3 +63,15 @@ def test_g2_subgroup_check_host_build_matches_pyref(hc):
             assert got == want, (i, want)
             if got:
                 assert out.raw == enc
+
+
+def test_g2_mul_psi_decomposition_host_build(hc):
+    """Recover's lambda * S via the base-|z| digits and psi (curve.h g2_mul_u256_psi) equals 255-bit
+    double-and-add, on edge and random scalars."""
+    z = 0xD201000000010000
+    sig = hx(load("chain_t3n5.json")["rounds"][3]["sig"])
+    rng = random.Random(11)
+    ks = [0, 1, 2, z - 1, z, z + 1, z * z, z ** 3, z ** 3 - 1, B.R - 1, B.R - z] + [rng.randrange(B.R) for _ in range(12)]
+    for k in ks:
+        k8 = (ctypes.c_uint32 * 8)(*[(k >> (32 * w)) & 0xFFFFFFFF for w in range(8)])
+        assert hc.hc_g2_mul_psi_check(sig, k8) == 1, hex(k)

@@ -118,7 +118,7 @@ void oc_recover_term(const uint8_t* sig96, const uint32_t* lam8, uint64_t* out) 
   G2A s;
   g2_decompress(s, sig96, false);
   reset();
-  G2J u = jac_mul_u256(jac_from_aff(s), lam8);
+  G2J u = g2_mul_u256_psi(s, lam8);
   (void)u;
   take(out);
 }
