@@ -212,8 +212,8 @@ DGI void g2_psi_aff(Fp2& x, Fp2& y) {
 // [k]P for P in G2 (affine) and a plain scalar k < r (8 little-endian limbs).  psi acts on G2 as [z],
 // z = -Z_ABS, and r < Z_ABS^4, so with the base-Z_ABS digits k = d0 + d1 Z + d2 Z^2 + d3 Z^3
 // (d_i < 2^64):  [k]P = [d0]P + [d1](-psi P) + [d2](psi^2 P) + [d3](-psi^3 P).  Straus over the four
-// 64-bit digits: 64 shared doublings and mixed additions, ~2x fewer group operations than 255-bit
-// double-and-add (jac_mul_u256).
+// digits in non-adjacent form: 64 shared doublings and ~86 mixed additions, ~2.5x fewer group
+// operations than 255-bit double-and-add (jac_mul_u256).
 DGH G2J g2_mul_u256_psi(const G2A& p, const uint32_t* k) {
   if (p.inf) return jac_infinity<Fp2>();
   uint32_t q[8];
@@ -233,11 +233,24 @@ DGH G2J g2_mul_u256_psi(const G2A& p, const uint32_t* k) {
   }
   py[1] = fp2_neg(py[1]);
   py[3] = fp2_neg(py[3]);
+  // non-adjacent forms of the digits (65 signed digits, ~1/3 non-zero): h = 3d, digit j = h_{j+1} - d_{j+1}
+  uint64_t pos[4], neg[4];
+  uint32_t pos64 = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t hl = d[i] + (d[i] << 1), hh = (d[i] >> 63) + (hl < d[i] ? 1u : 0u);
+    pos[i] = ((hl & ~d[i]) >> 1) | (hh << 63);  // bits 0..63; bit 64 of the form is hh >> 1
+    neg[i] = (~hl & d[i]) >> 1;
+    pos64 |= (uint32_t)(hh >> 1) << i;
+  }
   G2J acc = jac_infinity<Fp2>();
+  for (int i = 0; i < 4; ++i)
+    if ((pos64 >> i) & 1) acc = jac_add_aff(acc, px[i], py[i]);
   for (int b = 63; b >= 0; --b) {
     acc = jac_dbl(acc);
-    for (int i = 0; i < 4; ++i)
-      if ((d[i] >> b) & 1) acc = jac_add_aff(acc, px[i], py[i]);
+    for (int i = 0; i < 4; ++i) {
+      if ((pos[i] >> b) & 1) acc = jac_add_aff(acc, px[i], py[i]);
+      if ((neg[i] >> b) & 1) acc = jac_add_aff(acc, px[i], fp2_neg(py[i]));
+    }
   }
   return acc;
 }

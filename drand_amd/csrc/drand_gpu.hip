@@ -81,7 +81,8 @@ enum Slot {
   S_MSGS, S_DST, S_Q, S_S, S_U, S_STATUS, S_ISO, S_CELL, S_W, S_A, S_TMP, S_KP, S_F, S_H, S_FLAG, S_KEYS, S_KEYST,
   S_COMMITS, S_COMMITST, S_SLOTIDX, S_ITEMSLOT, S_SEL, S_SELIDX, S_RST, S_SST, S_TERMS, S_IN0, S_IN1, S_IN2, S_IN3,
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
-  S_MSM_P1, S_MSM_W, S_MSM_OUT, S_COUNT
+  S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
+  S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -272,6 +273,48 @@ int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA
   return 0;
 }
 
+// Keyed MSM (msm.h) of the multi-key batch: T = sum_s beta_s sum_{items i of slot s} alpha_{r(i)} S_i.
+int msm_run_keyed(const Batch& b, uint64_t seed, const uint8_t* iso, G2JStore** T, hipStream_t st) {
+  const uint32_t N = b.R * b.k, nsets = b.nslots, nkeys = MSM_NBK * nsets;
+  const uint32_t nblocks = (nkeys + KSCAN_B - 1) / KSCAN_B;
+  uint32_t *cnt, *tot, *list;
+  G2JStore *chunks, *B, *P1, *tmp, *W, *Ts, *BT;
+  RET(wsT(S_KMSM_CNT, (size_t)4 * nkeys + 1, &cnt));
+  uint32_t *offset = cnt + nkeys, *cursor = offset + nkeys, *chunk_off = cursor + nkeys;  // chunk_off: nkeys + 1
+  RET(wsT(S_KMSM_TOT, (size_t)2 * nblocks, &tot));
+  RET(wsT(S_KMSM_LIST, (size_t)MSM_WIN * N + 1, &list));
+  const uint32_t max_chunks = N + nkeys;  // sum of ceil(count / 8) <= 8N / 8 + nkeys
+  RET(wsT(S_KMSM_CHUNKS, max_chunks, &chunks));
+  RET(wsT(S_KMSM_B, nkeys, &B));
+  RET(wsT(S_KMSM_P1, (size_t)nsets * MSM_WIN * MSM_C * 16, &P1));
+  RET(wsT(S_KMSM_TMP, (size_t)nsets * MSM_WIN * MSM_C * 16, &tmp));
+  RET(wsT(S_KMSM_W, (size_t)nsets * MSM_WIN, &W));
+  RET(wsT(S_KMSM_T, nsets, &Ts));
+  RET(wsT(S_KMSM_BT, nsets, &BT));
+  HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * nkeys, st));
+  RET(launch("k_kmsm_count", k_kmsm_count, N, 256, st, N, b.k, nsets, seed, b.item_slot, (const uint8_t*)b.status,
+             iso, cnt));
+  RET(launch("k_kscan_local", k_kscan_local, nblocks * 256, 256, st, nkeys, (const uint32_t*)cnt, offset, chunk_off,
+             tot));
+  RET(launch("k_kscan_top", k_kscan_top, 64, 64, st, nblocks, nkeys, tot, chunk_off));
+  RET(launch("k_kscan_add", k_kscan_add, nkeys, 256, st, nkeys, (const uint32_t*)tot, offset, cursor, chunk_off));
+  RET(launch("k_kmsm_scatter", k_kmsm_scatter, N, 256, st, N, b.k, nsets, seed, b.item_slot,
+             (const uint8_t*)b.status, iso, cursor, list));
+  RET(launch("k_kmsm_chunks", k_kmsm_chunks, max_chunks, 128, st, max_chunks, nkeys, (const uint32_t*)cnt,
+             (const uint32_t*)offset, (const uint32_t*)chunk_off, (const uint32_t*)list, (const G2AStore*)b.S,
+             chunks));
+  RET(launch("k_kmsm_buckets", k_kmsm_buckets, nkeys, 128, st, nkeys, (const uint32_t*)chunk_off,
+             (const G2JStore*)chunks, B));
+  RET(launch("k_kmsm_slices", k_kmsm_slices, nsets * MSM_WIN * MSM_C * 16, 128, st, nsets, (const G2JStore*)B, P1));
+  RET(reduce_rows(P1, tmp, nsets * MSM_WIN * MSM_C, 16, st, 4));  // S[set][w][k] = P1[...]
+  RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * MSM_WIN * nsets, 128, st, (const G2JStore*)P1, W));
+  RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsets, 128, st, (const G2JStore*)W, Ts));
+  RET(launch("k_kmsm_beta", k_kmsm_beta, nsets, 64, st, nsets, seed, (const G2JStore*)Ts, BT));
+  RET(reduce_rows(BT, tmp, 1, nsets, st));  // T = BT[0]
+  *T = BT;
+  return 0;
+}
+
 int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   const uint32_t N = b.R * b.k;
   uint8_t *iso, *active;
@@ -282,15 +325,20 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   RET(wsT(S_ACTIVE, b.R, &active));
   RET(wsT(S_CELL, (size_t)b.R * b.nslots, &cell));
   RET(wsT(S_FLAG, 4, &flag));
-  RET(wsT(S_U, N, &U));
-  RET(wsT(S_W, b.R, &V));
-  if (b.nslots > 1) RET(wsT(S_A, b.R, &A));
+  U = V = nullptr;
+  if (b.nslots == 1) {
+    RET(wsT(S_U, N, &U));
+    RET(wsT(S_W, b.R, &V));
+  } else {
+    RET(wsT(S_A, b.R, &A));
+  }
   RET(wsT(S_F, b.nslots + 1, &f));
   HIPCHK(hipMemsetAsync(cell, 0, sizeof(uint32_t) * (size_t)b.R * b.nslots, st));
   RET(launch("k_decode_items", k_decode_items, N, 128, st, N, b.k, b.nslots, b.sigs, b.stride, b.offset, b.item_slot,
              b.key_status, b.S, b.status, cell, iso));
-  RET(launch("k_scale_items", k_scale_items, N, 128, st, N, b.nslots, seed, b.item_slot, (const G2AStore*)b.S,
-             (const uint8_t*)b.status, (const uint8_t*)iso, U));
+  if (b.nslots == 1)
+    RET(launch("k_scale_items", k_scale_items, N, 128, st, N, b.nslots, seed, b.item_slot, (const G2AStore*)b.S,
+               (const uint8_t*)b.status, (const uint8_t*)iso, U));
   RET(launch("k_round_combine", k_round_combine, b.R, 128, st, b.R, b.k, b.nslots, seed, (const G2JStore*)U,
              (const uint8_t*)b.status, (const uint8_t*)iso, b.Q, V, A, active));
   const G2JStore *T, *K;
@@ -300,7 +348,8 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
     T = msm;
     K = msm + 1;
   } else {
-    RET(msm_run(b.R, seed, active, V, nullptr, &msm, st));
+    // T = sum_s beta_s sum_{i in s} alpha_{r(i)} S_i by the keyed MSM (no per-item scalar multiplication)
+    RET(msm_run_keyed(b, seed, iso, &msm, st));
     T = msm;
     uint32_t nchunks = 16384 / b.nslots;
     if (nchunks < 1) nchunks = 1;

@@ -284,11 +284,11 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_round_combine(uint32_t R,
   for (uint32_t j = 0; j < k; ++j) {
     size_t i = (size_t)r * k + j;
     if (status[i] == DG_ST_OK_ && !isolate[i]) {
-      v = any ? jac_add(v, load_g2j(U[i])) : load_g2j(U[i]);
+      if (U) v = any ? jac_add(v, load_g2j(U[i])) : load_g2j(U[i]);
       any = true;
     }
   }
-  store_g2j(V[r], v);
+  if (V) store_g2j(V[r], v);  // V (and U) only on the single-key path; the keyed MSM reads S directly
   active[r] = any ? 1 : 0;
   if (nslots > 1) store_g2j(A[r], any ? jac_mul_u64(load_g2j(Q[r]), rlc_alpha(seed, r)) : jac_infinity<Fp2>());
 }

@@ -194,6 +194,161 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_final_coop(const G2JS
   CO_SERIAL(store_g2j(out[side], G2J{acc.x, acc.y, acc.z}));
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Keyed MSM for the multi-key batch (VerifyPartial / Recover): T_s = sum over the batch items i of key
+// slot s of alpha_{r(i)} S_i, for every slot at once.  Bucket key = (window, digit, set) with the set
+// (the item's key slot) fastest, so one bucket sort serves all sets.  Then T = sum_s beta_s T_s -- the
+// same alpha_r beta_s item coefficients as before, without a 64-bit scalar multiplication per item.
+//   k_kmsm_count / k_kscan_* / k_kmsm_scatter   bucket sort of the item indices (multi-block scan)
+//   k_kmsm_chunks                               chunk sums of <= MSM_CHUNK affine signatures
+//   k_kmsm_buckets                              one lane per bucket sums its chunks
+//   k_kmsm_slices                               bit-slice partials per (set, window, bit)
+//   k_msm_horner_coop / k_msm_final_coop        per (set, window) / per set, as above
+//   k_kmsm_beta                                 beta_s T_s, then a row sum
+constexpr uint32_t KSCAN_B = 1024;  // keys per scan block
+
+DGI uint32_t kmsm_key(uint32_t w, uint32_t d, uint32_t set, uint32_t nsets) { return (w * MSM_NB + d) * nsets + set; }
+
+DG_KERNEL void __launch_bounds__(256) k_kmsm_count(uint32_t N, uint32_t k, uint32_t nsets, uint64_t seed,
+                                                   const uint32_t* item_slot, const uint8_t* status,
+                                                   const uint8_t* isolate, uint32_t* count) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N || status[i] != DG_ST_OK_ || isolate[i]) return;
+  uint64_t a = rlc_alpha(seed, i / k);
+  uint32_t s = item_slot[i];
+  for (uint32_t w = 0; w < MSM_WIN; ++w) {
+    uint32_t d = (uint32_t)(a >> (MSM_C * w)) & (MSM_NB - 1);
+    if (d) atomicAdd(&count[kmsm_key(w, d, s, nsets)], 1u);
+  }
+}
+
+// block b of KSCAN_B keys: exclusive scans of count and of ceil(count / MSM_CHUNK) within the block,
+// block totals into tot[b], tot[nblocks + b]
+DG_KERNEL void __launch_bounds__(256) k_kscan_local(uint32_t nkeys, const uint32_t* count, uint32_t* offset,
+                                                    uint32_t* chunk_off, uint32_t* tot) {
+  __shared__ uint32_t s_c[256], s_k[256];
+  const uint32_t t = threadIdx.x, base = blockIdx.x * KSCAN_B + t * 4;
+  uint32_t c[4], kk[4], sc = 0, sk = 0;
+  for (int j = 0; j < 4; ++j) {
+    uint32_t v = base + j < nkeys ? count[base + j] : 0u;
+    c[j] = sc;
+    kk[j] = sk;
+    sc += v;
+    sk += (v + MSM_CHUNK - 1) / MSM_CHUNK;
+  }
+  s_c[t] = sc;
+  s_k[t] = sk;
+  __syncthreads();
+  for (uint32_t o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan
+    uint32_t a = t >= o ? s_c[t - o] : 0u, b = t >= o ? s_k[t - o] : 0u;
+    __syncthreads();
+    s_c[t] += a;
+    s_k[t] += b;
+    __syncthreads();
+  }
+  const uint32_t pc = t ? s_c[t - 1] : 0u, pk = t ? s_k[t - 1] : 0u;
+  for (int j = 0; j < 4; ++j)
+    if (base + j < nkeys) {
+      offset[base + j] = pc + c[j];
+      chunk_off[base + j] = pk + kk[j];
+    }
+  if (t == 255) {
+    tot[blockIdx.x] = s_c[255];
+    tot[gridDim.x + blockIdx.x] = s_k[255];
+  }
+}
+// one workgroup: exclusive scan of the nblocks block totals (in place), grand totals to chunk_off[nkeys]
+DG_KERNEL void __launch_bounds__(64) k_kscan_top(uint32_t nblocks, uint32_t nkeys, uint32_t* tot, uint32_t* chunk_off) {
+  if (threadIdx.x != 0) return;
+  uint32_t a = 0, b = 0;
+  for (uint32_t i = 0; i < nblocks; ++i) {
+    uint32_t x = tot[i], y = tot[nblocks + i];
+    tot[i] = a;
+    tot[nblocks + i] = b;
+    a += x;
+    b += y;
+  }
+  chunk_off[nkeys] = b;
+}
+DG_KERNEL void __launch_bounds__(256) k_kscan_add(uint32_t nkeys, const uint32_t* tot, uint32_t* offset,
+                                                  uint32_t* cursor, uint32_t* chunk_off) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nkeys) return;
+  uint32_t b = i / KSCAN_B, nblocks = (nkeys + KSCAN_B - 1) / KSCAN_B;
+  offset[i] += tot[b];
+  cursor[i] = offset[i];
+  chunk_off[i] += tot[nblocks + b];
+}
+
+DG_KERNEL void __launch_bounds__(256) k_kmsm_scatter(uint32_t N, uint32_t k, uint32_t nsets, uint64_t seed,
+                                                     const uint32_t* item_slot, const uint8_t* status,
+                                                     const uint8_t* isolate, uint32_t* cursor, uint32_t* list) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N || status[i] != DG_ST_OK_ || isolate[i]) return;
+  uint64_t a = rlc_alpha(seed, i / k);
+  uint32_t s = item_slot[i];
+  for (uint32_t w = 0; w < MSM_WIN; ++w) {
+    uint32_t d = (uint32_t)(a >> (MSM_C * w)) & (MSM_NB - 1);
+    if (d) list[atomicAdd(&cursor[kmsm_key(w, d, s, nsets)], 1u)] = i;
+  }
+}
+
+// lane c: the c-th chunk (<= MSM_CHUNK affine points of one bucket)
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_chunks(uint32_t max_chunks, uint32_t nkeys,
+                                                                   const uint32_t* count, const uint32_t* offset,
+                                                                   const uint32_t* chunk_off, const uint32_t* list,
+                                                                   const G2AStore* S, G2JStore* out) {
+  uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= max_chunks || c >= chunk_off[nkeys]) return;
+  uint32_t lo = 0, hi = nkeys;
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) / 2;
+    if (chunk_off[mid] <= c)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  uint32_t first = offset[lo] + (c - chunk_off[lo]) * MSM_CHUNK;
+  uint32_t last = offset[lo] + count[lo];
+  if (last > first + MSM_CHUNK) last = first + MSM_CHUNK;
+  G2J acc = jac_from_aff(load_g2a(S[list[first]]));
+  for (uint32_t i = first + 1; i < last; ++i) {
+    const G2AStore& q = S[list[i]];
+    if (!q.inf) acc = jac_add_aff(acc, q.x, q.y);  // the identity encoding decodes (status OK)
+  }
+  store_g2j(out[c], acc);
+}
+
+// lane = bucket key: sum of its chunks (identity when empty)
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_buckets(uint32_t nkeys, const uint32_t* chunk_off,
+                                                                    const G2JStore* chunks, G2JStore* B) {
+  uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nkeys) return;
+  G2J acc = jac_infinity<Fp2>();
+  for (uint32_t c = chunk_off[b]; c < chunk_off[b + 1]; ++c) acc = jac_add(acc, load_g2j(chunks[c]));
+  store_g2j(B[b], acc);
+}
+
+// lane (set, w, k, c < 16): 8 of the buckets of (set, w) whose digit has bit k set; rows (set, w, k)
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_slices(uint32_t nsets, const G2JStore* B, G2JStore* P1) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nsets * MSM_WIN * MSM_C * 16) return;
+  uint32_t c = g % 16, k = (g / 16) % MSM_C, w = (g / (16 * MSM_C)) % MSM_WIN, set = g / (16 * MSM_C * MSM_WIN);
+  G2J acc = jac_infinity<Fp2>();
+  for (uint32_t i = 8 * c; i < 8 * c + 8; ++i) {
+    uint32_t d = ((i >> k) << (k + 1)) | (1u << k) | (i & ((1u << k) - 1));
+    acc = jac_add(acc, load_g2j(B[kmsm_key(w, d, set, nsets)]));
+  }
+  store_g2j(P1[g], acc);
+}
+
+// lane s: beta_s T_s
+DG_KERNEL void __launch_bounds__(64) k_kmsm_beta(uint32_t nsets, uint64_t seed, const G2JStore* Tset, G2JStore* out) {
+  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nsets) return;
+  store_g2j(out[s], jac_mul_u64(load_g2j(Tset[s]), rlc_beta(seed, s)));
+}
+
 #endif
 
 }  // namespace dg

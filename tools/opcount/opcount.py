@@ -45,9 +45,9 @@ def main():
         assert L.oc_decode_g2(sig, o) == 1
         add("k_decode_items")
         L.oc_round_combine(msg, 32, DST, len(DST), sig, ctypes.c_uint64(alpha), o)
-        add("k_round_combine")
+        add("k_round_combine (k > 1)")
         L.oc_scale_item(sig, ctypes.c_uint64(alpha), o)
-        add("k_scale_items[nslots>1]")
+        add("k_kmsm_beta (per key)")
         nxt = bytes.fromhex(rounds[(i + 1) % len(rounds)]["sig"])
         L.oc_g2_add(sig, nxt, o)
         add("k_sum_rows")
