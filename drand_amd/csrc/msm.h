@@ -85,9 +85,13 @@ DG_KERNEL void __launch_bounds__(256) k_msm_scatter(uint32_t R, uint64_t seed, c
   }
 }
 
+#endif
+
+// the chunk sums are the MSM's bulk work: hot translation unit (kernels_hot.hip, flat, 2 waves/SIMD)
+#if defined(__HIP__) && DG_TU_HOT
 // lane g: side = g / max_chunks, chunk c = g % max_chunks; sums its chunk of points of side `side`
 // (side 0: PA, side 1: PB) into out[side * max_chunks + c]
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, const uint32_t* count,
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, const uint32_t* count,
                                                    const uint32_t* offset, const uint32_t* chunk_off,
                                                    const uint32_t* list, const G2JStore* PA, const G2JStore* PB,
                                                    G2JStore* out) {
@@ -122,6 +126,14 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_chunks(uint32_t max_c
   store_g2j(out[side * max_chunks + c], acc);
 }
 
+#elif defined(__HIP__)
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, const uint32_t* count,
+                                                   const uint32_t* offset, const uint32_t* chunk_off,
+                                                   const uint32_t* list, const G2JStore* PA, const G2JStore* PB,
+                                                   G2JStore* out);
+#endif
+
+#if defined(__HIP__) && !DG_TU_HOT
 // lane g: side, bucket b, lane-in-bucket q < MSM_BSPLIT: strided partial sum of the bucket's chunks,
 // BP[(side * NBK + b) * MSM_BSPLIT + q]; the MSM_BSPLIT partials are then row-summed into B[side][b]
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_buckets(uint32_t max_chunks, uint32_t nsides, const uint32_t* chunk_off,

@@ -11,6 +11,6 @@ import json
 d = json.loads(open("gpurun_out/bench.json").read().strip().splitlines()[-1])
 print("%.0f rounds/s" % d["value"], "ms/step %.2f" % d["ms_per_step"], "fallbacks", d.get("batch_fallbacks"))
 r = d["roofline"] or {}
-print("roofline", r.get("kernel"), "frac %.3f" % r.get("frac", 0), "isolated", r.get("isolated"), "chip", r.get("chip"))
+print("roofline", r.get("kernel"), "frac %.3f" % r.get("frac", 0), "us %.0f" % r.get("kernel_avg_us", 0), "overlapped", r.get("overlapped"), "chip", r.get("chip"))
 print("iso", d.get("kernel_avg_us_isolated"))
 PY
