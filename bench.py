@@ -340,11 +340,11 @@ def main():
                 roof["overlapped"] = {"kernel_avg_us": o_us, "achieved": a_o, "frac": a_o / peak["tmac_s"],
                                       "note": "instrumented replay of the timed region: the launch shares the "
                                               "chip with the other batches in flight"}
-            # whole chip: algorithmic multiply-adds of the per-round work (hash, decode + subgroup check,
-            # 16 bucket additions of the two MSMs, mixed: signatures and hashes are stored with Z = 1) over
-            # the step time; per-batch fixed work not counted
+            # whole chip: algorithmic multiply-adds of the per-round work (hash, decode, 16 bucket additions
+            # of the two MSMs + 10 of the subgroup-check test windows, mixed: signatures and hashes are
+            # stored with Z = 1) over the step time; per-batch fixed work not counted
             per_round = (sum(oc[k]["macs"] for k in ("k_h2c_uncleared", "k_decode_items")) +
-                         16 * oc["k_msm_chunks[mixed add]"]["macs"])
+                         26 * oc["k_msm_chunks[mixed add]"]["macs"])
             chip = per_round * n * args.steps / dt / 1e12
             roof["chip"] = {"macs_per_round": per_round, "achieved": chip, "frac": chip / peak["tmac_s"]}
         share = {k: round(v[0] * v[1] / (dt * 1e6 / 1.0), 4) for k, v in kt.items()}

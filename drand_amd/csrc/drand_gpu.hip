@@ -241,35 +241,37 @@ struct Batch {
 };
 
 // Pippenger MSM (msm.h): out[0] = sum_r alpha_r PA_r, out[1] = sum_r alpha_r PB_r (PB may be null),
-// over the rounds with active[r] != 0.
-int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA, const G2JStore* PB, G2JStore** out,
-            hipStream_t st) {
-  const uint32_t nsides = PB ? 2 : 1;
+// over the rounds with active[r] != 0.  With `test_windows` side A also gets the MSM_TWIN test windows of
+// the batched subgroup check; *win = its MSM_WT window sums (checked by k_msm_subgroup).
+int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA, const G2JStore* PB, bool test_windows,
+            G2JStore** out, G2JStore** win, hipStream_t st) {
+  const uint32_t nsides = PB ? 2 : 1, nwin = test_windows ? MSM_WT : MSM_WIN, nbk = nwin * MSM_NB;
   uint32_t *cnt, *list;
   G2JStore *chunks, *BP, *tmp, *P1, *W;
-  RET(wsT(S_MSM_CNT, 4 * MSM_NBK + 1, &cnt));
-  uint32_t *offset = cnt + MSM_NBK, *cursor = offset + MSM_NBK, *chunk_off = cursor + MSM_NBK;
-  RET(wsT(S_MSM_LIST, (size_t)MSM_WIN * R + 1, &list));
-  const uint32_t max_chunks = (MSM_WIN * R) / MSM_CHUNK + MSM_NBK;
+  RET(wsT(S_MSM_CNT, 4 * nbk + 1, &cnt));
+  uint32_t *offset = cnt + nbk, *cursor = offset + nbk, *chunk_off = cursor + nbk;
+  RET(wsT(S_MSM_LIST, (size_t)nwin * R + 1, &list));
+  const uint32_t max_chunks = (nwin * R) / MSM_CHUNK + nbk;
   RET(wsT(S_MSM_CHUNKS, (size_t)max_chunks * nsides, &chunks));
-  RET(wsT(S_MSM_B, (size_t)MSM_NBK * MSM_BSPLIT * nsides, &BP));
-  RET(wsT(S_MSM_G, (size_t)MSM_NBK * MSM_BSPLIT * nsides, &tmp));
-  RET(wsT(S_MSM_P1, (size_t)MSM_WIN * MSM_C * 16 * nsides, &P1));
-  RET(wsT(S_MSM_W, (size_t)MSM_WIN * nsides, &W));
+  RET(wsT(S_MSM_B, (size_t)nbk * MSM_BSPLIT * nsides, &BP));
+  RET(wsT(S_MSM_G, (size_t)nbk * MSM_BSPLIT * nsides, &tmp));
+  RET(wsT(S_MSM_P1, (size_t)nwin * MSM_C * 16 * nsides, &P1));
+  RET(wsT(S_MSM_W, (size_t)nwin * nsides, &W));
   RET(wsT(S_MSM_OUT, 2, out));
-  HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * MSM_NBK, st));
-  RET(launch("k_msm_count", k_msm_count, R, 256, st, R, seed, active, cnt));
-  RET(launch("k_msm_scan", k_msm_scan, 256, 256, st, (const uint32_t*)cnt, offset, cursor, chunk_off));
-  RET(launch("k_msm_scatter", k_msm_scatter, R, 256, st, R, seed, active, cursor, list));
-  RET(launch("k_msm_chunks", k_msm_chunks, max_chunks * nsides, 128, st, max_chunks, nsides, (const uint32_t*)cnt,
+  HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * nbk, st));
+  RET(launch("k_msm_count", k_msm_count, R, 256, st, R, nwin, seed, active, cnt));
+  RET(launch("k_msm_scan", k_msm_scan, 256, 256, st, nbk, (const uint32_t*)cnt, offset, cursor, chunk_off));
+  RET(launch("k_msm_scatter", k_msm_scatter, R, 256, st, R, nwin, seed, active, cursor, list));
+  RET(launch("k_msm_chunks", k_msm_chunks, max_chunks * nsides, 128, st, max_chunks, nsides, nbk, (const uint32_t*)cnt,
              (const uint32_t*)offset, (const uint32_t*)chunk_off, (const uint32_t*)list, PA, PB, chunks));
-  RET(launch("k_msm_buckets", k_msm_buckets, MSM_NBK * MSM_BSPLIT * nsides, 128, st, max_chunks, nsides,
+  RET(launch("k_msm_buckets", k_msm_buckets, nbk * MSM_BSPLIT * nsides, 128, st, max_chunks, nsides, nbk,
              (const uint32_t*)chunk_off, (const G2JStore*)chunks, BP));
-  RET(reduce_rows(BP, tmp, MSM_NBK * nsides, MSM_BSPLIT, st));  // B[side][b] = BP[side * NBK + b]
-  RET(launch("k_msm_slices", k_msm_slices, nsides * MSM_WIN * MSM_C * 16, 128, st, nsides, (const G2JStore*)BP, P1));
-  RET(reduce_rows(P1, tmp, nsides * MSM_WIN * MSM_C, 16, st, 4));  // S[side][w][k] = P1[...]
-  RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * MSM_WIN * nsides, 128, st, (const G2JStore*)P1, W));
-  RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsides, 128, st, (const G2JStore*)W, *out));
+  RET(reduce_rows(BP, tmp, nbk * nsides, MSM_BSPLIT, st));  // B[side][b] = BP[side * nbk + b]
+  RET(launch("k_msm_slices", k_msm_slices, nsides * nwin * MSM_C * 16, 128, st, nsides, nwin, (const G2JStore*)BP, P1));
+  RET(reduce_rows(P1, tmp, nsides * nwin * MSM_C, 16, st, 4));  // S[side][w][k] = P1[...]
+  RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * nwin * nsides, 128, st, nwin, (const G2JStore*)P1, W));
+  RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsides, 128, st, nwin, (const G2JStore*)W, *out));
+  if (win) *win = W;
   return 0;
 }
 
@@ -307,8 +309,8 @@ int msm_run_keyed(const Batch& b, uint64_t seed, const uint8_t* iso, G2JStore** 
              (const G2JStore*)chunks, B));
   RET(launch("k_kmsm_slices", k_kmsm_slices, nsets * MSM_WIN * MSM_C * 16, 128, st, nsets, (const G2JStore*)B, P1));
   RET(reduce_rows(P1, tmp, nsets * MSM_WIN * MSM_C, 16, st, 4));  // S[set][w][k] = P1[...]
-  RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * MSM_WIN * nsets, 128, st, (const G2JStore*)P1, W));
-  RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsets, 128, st, (const G2JStore*)W, Ts));
+  RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * MSM_WIN * nsets, 128, st, MSM_WIN, (const G2JStore*)P1, W));
+  RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsets, 128, st, MSM_WIN, (const G2JStore*)W, Ts));
   RET(launch("k_kmsm_beta", k_kmsm_beta, nsets, 64, st, nsets, seed, (const G2JStore*)Ts, BT));
   RET(reduce_rows(BT, tmp, 1, nsets, st));  // T = BT[0]
   *T = BT;
@@ -334,17 +336,21 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   }
   RET(wsT(S_F, b.nslots + 1, &f));
   HIPCHK(hipMemsetAsync(cell, 0, sizeof(uint32_t) * (size_t)b.R * b.nslots, st));
+  // one key, one item per round: the G2 subgroup checks of the signatures are batched on the MSM's window
+  // sums (msm.h) instead of a psi check per item
+  const uint32_t batched_sub = (b.nslots == 1 && b.k == 1) ? 1u : 0u;
   RET(launch("k_decode_items", k_decode_items, N, 128, st, N, b.k, b.nslots, b.sigs, b.stride, b.offset, b.item_slot,
-             b.key_status, b.S, b.status, cell, iso));
+             b.key_status, b.S, b.status, cell, iso, 1u - batched_sub));
   if (b.nslots == 1)
     RET(launch("k_scale_items", k_scale_items, N, 128, st, N, b.nslots, seed, b.item_slot, (const G2AStore*)b.S,
                (const uint8_t*)b.status, (const uint8_t*)iso, U));
   RET(launch("k_round_combine", k_round_combine, b.R, 128, st, b.R, b.k, b.nslots, seed, (const G2JStore*)U,
              (const uint8_t*)b.status, (const uint8_t*)iso, b.Q, V, A, active));
   const G2JStore *T, *K;
+  G2JStore* win = nullptr;
   if (b.nslots == 1) {
     // T = sum alpha_r V_r and K = sum alpha_r Q_r in one MSM (shared bucket sort)
-    RET(msm_run(b.R, seed, active, V, b.Q, &msm, st));
+    RET(msm_run(b.R, seed, active, V, b.Q, batched_sub != 0, &msm, &win, st));
     T = msm;
     K = msm + 1;
   } else {
@@ -365,6 +371,7 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   }
   RET(launch("k_pair_miller_coop", k_pair_miller_coop, 128 * (b.nslots + 1), 128, st, b.nslots, seed, b.keys, K, T, f));
   RET(launch("k_final_coop", k_final_coop, 128, 128, st, b.nslots + 1, (const Fp12*)f, flag));
+  if (batched_sub) RET(launch("k_msm_subgroup", k_msm_subgroup, 128 * MSM_WT, 128, st, (const G2JStore*)win, flag));
   // isolated items present?  The per-item pass decides on the device (no host round trip), so a batch
   // is one stream-ordered sequence of launches.
   HIPCHK(hipMemsetAsync(flag + 1, 0, 4, st));
@@ -373,7 +380,7 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   RET(wsT(S_H, b.R, &H));
   RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, (const uint32_t*)flag, b.Q, H));
   RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
-             (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status));
+             (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status, batched_sub));
   RET(launch("k_count_fallback", k_count_fallback, 1, 64, st, (const uint32_t*)flag, g_ctx.fallbacks));
   return 0;
 }

@@ -61,14 +61,19 @@ DGI void store_g1a(G1AStore& s, const G1A& a) {
   s.inf = a.inf ? 1u : 0u;
 }
 
-// 64-bit RLC coefficient for item i: first 8 bytes of SHA-256(seed || i), forced odd and non-zero
-DGI uint64_t rlc_coeff(uint64_t seed, uint64_t i) {
+// SHA-256(BE64 seed || BE64 i)
+DGI void rlc_digest(uint64_t seed, uint64_t i, uint8_t d[32]) {
   Sha256 s;
   sha256_init(s);
   for (int b = 7; b >= 0; --b) sha256_byte(s, (uint8_t)(seed >> (8 * b)));
   for (int b = 7; b >= 0; --b) sha256_byte(s, (uint8_t)(i >> (8 * b)));
-  uint8_t d[32];
   sha256_final(s, d);
+}
+
+// 64-bit RLC coefficient for item i: first 8 bytes of SHA-256(seed || i), forced odd and non-zero
+DGI uint64_t rlc_coeff(uint64_t seed, uint64_t i) {
+  uint8_t d[32];
+  rlc_digest(seed, i, d);
   uint64_t r = 0;
   for (int b = 0; b < 8; ++b) r = (r << 8) | d[b];
   return r | 1ull;
@@ -220,13 +225,14 @@ DG_KERNEL void __launch_bounds__(64) k_pubpoly_eval(uint32_t n, uint32_t t, cons
 }
 #endif
 
-// decode sigma of every item (96 B at sigs + stride*i + offset) with the G2 subgroup check; claim the
-// item's (round, slot) cell -- a taken cell sends the item to the individual check (`isolate`)
+// decode sigma of every item (96 B at sigs + stride*i + offset), with the G2 subgroup check unless the
+// batch checks subgroup membership on the MSM window sums (`subgroup` == 0, msm.h); claim the item's
+// (round, slot) cell -- a taken cell sends the item to the individual check (`isolate`)
 #if DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_decode_items(uint32_t n, uint32_t k, uint32_t nslots, const uint8_t* sigs,
                                                      uint32_t stride, uint32_t offset, const uint32_t* item_slot,
                                                      const uint8_t* key_status, G2AStore* S, uint8_t* status,
-                                                     uint32_t* cell, uint8_t* isolate) {
+                                                     uint32_t* cell, uint8_t* isolate, uint32_t subgroup) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t slot = item_slot ? item_slot[i] : 0u;
@@ -237,7 +243,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_decode_items(uint32_t n, u
     return;
   }
   G2A a;
-  bool ok = g2_decompress(a, sigs + (size_t)stride * i + offset, true);
+  bool ok = g2_decompress(a, sigs + (size_t)stride * i + offset, subgroup != 0);
   if (!ok) a = G2A{fp2_zero(), fp2_zero(), true};
   store_g2a(S[i], a);
   status[i] = ok ? DG_ST_OK_ : DG_ST_SIG_DECODE_;
@@ -250,7 +256,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_decode_items(uint32_t n, u
 DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_decode_items(uint32_t n, uint32_t k, uint32_t nslots, const uint8_t* sigs,
                                                      uint32_t stride, uint32_t offset, const uint32_t* item_slot,
                                                      const uint8_t* key_status, G2AStore* S, uint8_t* status,
-                                                     uint32_t* cell, uint8_t* isolate);
+                                                     uint32_t* cell, uint8_t* isolate, uint32_t subgroup);
 #endif
 
 // U_i = beta_slot S_i for batch items, O otherwise
@@ -409,11 +415,13 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_clear_rounds(uint32_t R, 
 #endif
 
 // individual bls.Verify of item i: e(X_slot, H_{i/k}) == e(g1, S_i): every decoded item after a failed
-// batch (flag[0] == 0), only the isolated ones after a passed batch
+// batch (flag[0] == 0), only the isolated ones after a passed batch; with `subgroup` the decode skipped
+// the per-item G2 subgroup check (batched on the MSM windows), so it is done here: a sigma outside G2
+// is a decode error, as in g2_decompress
 #if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
                                                     const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
-                                                    const uint8_t* isolate, uint8_t* status) {
+                                                    const uint8_t* isolate, uint8_t* status, uint32_t subgroup) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (status[i] != DG_ST_OK_) return;
@@ -421,6 +429,10 @@ DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, cons
   G1A key = load_g1a(keys[item_slot ? item_slot[i] : 0u]);
   G2A h = load_g2a(H[i / k]);
   G2A s = load_g2a(S[i]);
+  if (subgroup && !s.inf && !g2_in_subgroup_aff(s.x, s.y)) {
+    status[i] = DG_ST_SIG_DECODE_;
+    return;
+  }
   G1A P[2];
   G2A Qa[2];
   int np = 0;

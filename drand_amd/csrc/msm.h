@@ -16,35 +16,61 @@
 //   8. k_msm_final_coop   the sum of the 8 window terms
 // Work: 8 bucket additions per point instead of a 64-bit double-and-add (64 doublings + 64 divergent
 // additions) per point.
+//
+// Batched G2 subgroup check (single-key path, one item per round): with nwin = MSM_WT the signature
+// side also sums MSM_TWIN "test windows" whose 8-bit digits come from an independent hash of (seed, r),
+// and every window sum W_w of that side (the 8 alpha windows, whose digits are the independent bytes of
+// alpha_r, and the test windows) must lie in G2 (k_msm_subgroup).  The E'(Fp2) cofactor h2 is prime to
+// r and its smallest prime factor is 13, so a non-zero torsion component E_r of some sigma_r survives
+// in W_w = sum_r d_{w,r} sigma_r unless d_{w,r} falls in one residue class mod ord(E_r) >= 13: at most
+// 20 of the 256 digit values (10 of the 128 odd low digits of alpha) -- <= 2^-3.68 per window, 2^-66
+// over 18 windows.  A failed check sends the batch to the exact per-item pass, which subgroup-checks
+// each signature itself.  This replaces a 64-doubling psi check per signature by 10 bucket additions.
 #pragma once
 // included from kernels.h (uses rlc_alpha, the G2JStore layout and jac_mul_small defined there)
 
 namespace dg {
 
 constexpr uint32_t MSM_C = 8, MSM_WIN = 8, MSM_NB = 256, MSM_NBK = MSM_WIN * MSM_NB;  // 2048 bucket slots
+constexpr uint32_t MSM_TWIN = 10, MSM_WT = MSM_WIN + MSM_TWIN;  // test windows of the batched subgroup check
+constexpr uint32_t MSM_NBT = MSM_WT * MSM_NB;                   // 4608 bucket slots with the test windows
 constexpr uint32_t MSM_CHUNK = 8;   // points per first-level lane
 constexpr uint32_t MSM_BSPLIT = 8;  // lanes per bucket at the second level
 
 #if defined(__HIP__) && !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(256) k_msm_count(uint32_t R, uint64_t seed, const uint8_t* active, uint32_t* count) {
+// digits of round r in windows 0..nwin-1: the bytes of alpha_r, then (nwin > MSM_WIN) the first
+// MSM_TWIN bytes of SHA-256(seed' || r), an independent hash
+struct MsmDigits {
+  uint64_t a;
+  uint8_t t[32];
+  DGI MsmDigits(uint64_t seed, uint32_t r, uint32_t nwin) : a(rlc_alpha(seed, r)) {
+    if (nwin > MSM_WIN) rlc_digest(seed ^ 0x5375626772705465ull, r, t);  // "SubgrpTe"
+  }
+  DGI uint32_t operator()(uint32_t w) const {
+    return w < MSM_WIN ? (uint32_t)(a >> (MSM_C * w)) & (MSM_NB - 1) : (uint32_t)t[w - MSM_WIN];
+  }
+};
+
+DG_KERNEL void __launch_bounds__(256) k_msm_count(uint32_t R, uint32_t nwin, uint64_t seed, const uint8_t* active,
+                                                  uint32_t* count) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R || !active[r]) return;
-  uint64_t a = rlc_alpha(seed, r);
-  for (uint32_t w = 0; w < MSM_WIN; ++w) {
-    uint32_t d = (uint32_t)(a >> (MSM_C * w)) & (MSM_NB - 1);
+  const MsmDigits dg(seed, r, nwin);
+  for (uint32_t w = 0; w < nwin; ++w) {
+    uint32_t d = dg(w);
     if (d) atomicAdd(&count[w * MSM_NB + d], 1u);
   }
 }
 
 // offset[b] = exclusive scan of count; cursor = offset; chunk_off[b] = exclusive scan of ceil(count/CHUNK),
-// chunk_off[MSM_NBK] = total chunks.  One workgroup of 256 lanes, 8 slots each.
-DG_KERNEL void __launch_bounds__(256) k_msm_scan(const uint32_t* count, uint32_t* offset, uint32_t* cursor,
-                                                 uint32_t* chunk_off) {
+// chunk_off[nbk] = total chunks.  One workgroup of 256 lanes, nbk / 256 (= nwin) slots each.
+DG_KERNEL void __launch_bounds__(256) k_msm_scan(uint32_t nbk, const uint32_t* count, uint32_t* offset,
+                                                 uint32_t* cursor, uint32_t* chunk_off) {
   __shared__ uint32_t s_cnt[256], s_chk[256];
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x, per = nbk / 256;
   uint32_t c = 0, k = 0;
-  for (uint32_t j = 0; j < 8; ++j) {
-    uint32_t v = count[t * 8 + j];
+  for (uint32_t j = 0; j < per; ++j) {
+    uint32_t v = count[t * per + j];
     c += v;
     k += (v + MSM_CHUNK - 1) / MSM_CHUNK;
   }
@@ -60,12 +86,12 @@ DG_KERNEL void __launch_bounds__(256) k_msm_scan(const uint32_t* count, uint32_t
       a += x;
       b += y;
     }
-    chunk_off[MSM_NBK] = b;
+    chunk_off[nbk] = b;
   }
   __syncthreads();
   uint32_t a = s_cnt[t], b = s_chk[t];
-  for (uint32_t j = 0; j < 8; ++j) {
-    uint32_t i = t * 8 + j, v = count[i];
+  for (uint32_t j = 0; j < per; ++j) {
+    uint32_t i = t * per + j, v = count[i];
     offset[i] = a;
     cursor[i] = a;
     chunk_off[i] = b;
@@ -74,13 +100,13 @@ DG_KERNEL void __launch_bounds__(256) k_msm_scan(const uint32_t* count, uint32_t
   }
 }
 
-DG_KERNEL void __launch_bounds__(256) k_msm_scatter(uint32_t R, uint64_t seed, const uint8_t* active, uint32_t* cursor,
-                                                    uint32_t* list) {
+DG_KERNEL void __launch_bounds__(256) k_msm_scatter(uint32_t R, uint32_t nwin, uint64_t seed, const uint8_t* active,
+                                                    uint32_t* cursor, uint32_t* list) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R || !active[r]) return;
-  uint64_t a = rlc_alpha(seed, r);
-  for (uint32_t w = 0; w < MSM_WIN; ++w) {
-    uint32_t d = (uint32_t)(a >> (MSM_C * w)) & (MSM_NB - 1);
+  const MsmDigits dg(seed, r, nwin);
+  for (uint32_t w = 0; w < nwin; ++w) {
+    uint32_t d = dg(w);
     if (d) list[atomicAdd(&cursor[w * MSM_NB + d], 1u)] = r;
   }
 }
@@ -90,17 +116,17 @@ DG_KERNEL void __launch_bounds__(256) k_msm_scatter(uint32_t R, uint64_t seed, c
 // the chunk sums are the MSM's bulk work: hot translation unit (kernels_hot.hip, flat, 2 waves/SIMD)
 #if defined(__HIP__) && DG_TU_HOT
 // lane g: side = g / max_chunks, chunk c = g % max_chunks; sums its chunk of points of side `side`
-// (side 0: PA, side 1: PB) into out[side * max_chunks + c]
-DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, const uint32_t* count,
+// (side 0: PA, side 1: PB) into out[side * max_chunks + c]; side 1 has no test windows (buckets >= MSM_NBK)
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, uint32_t nbk, const uint32_t* count,
                                                    const uint32_t* offset, const uint32_t* chunk_off,
                                                    const uint32_t* list, const G2JStore* PA, const G2JStore* PB,
                                                    G2JStore* out) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= max_chunks * nsides) return;
   uint32_t side = g / max_chunks, c = g % max_chunks;
-  if (c >= chunk_off[MSM_NBK]) return;
+  if (c >= chunk_off[side ? MSM_NBK : nbk]) return;
   // bucket of chunk c: last b with chunk_off[b] <= c
-  uint32_t lo = 0, hi = MSM_NBK;
+  uint32_t lo = 0, hi = nbk;
   while (hi - lo > 1) {
     uint32_t mid = (lo + hi) / 2;
     if (chunk_off[mid] <= c)
@@ -127,7 +153,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_ch
 }
 
 #elif defined(__HIP__)
-DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, const uint32_t* count,
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, uint32_t nbk, const uint32_t* count,
                                                    const uint32_t* offset, const uint32_t* chunk_off,
                                                    const uint32_t* list, const G2JStore* PA, const G2JStore* PB,
                                                    G2JStore* out);
@@ -136,13 +162,14 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_ch
 #if defined(__HIP__) && !DG_TU_HOT
 // lane g: side, bucket b, lane-in-bucket q < MSM_BSPLIT: strided partial sum of the bucket's chunks,
 // BP[(side * NBK + b) * MSM_BSPLIT + q]; the MSM_BSPLIT partials are then row-summed into B[side][b]
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_buckets(uint32_t max_chunks, uint32_t nsides, const uint32_t* chunk_off,
-                                                    const G2JStore* chunks, G2JStore* BP) {
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_buckets(uint32_t max_chunks, uint32_t nsides, uint32_t nbk,
+                                                                   const uint32_t* chunk_off, const G2JStore* chunks,
+                                                                   G2JStore* BP) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= MSM_NBK * MSM_BSPLIT * nsides) return;
+  if (g >= nbk * MSM_BSPLIT * nsides) return;
   uint32_t q = g % MSM_BSPLIT, sb = g / MSM_BSPLIT;
-  uint32_t side = sb / MSM_NBK, b = sb % MSM_NBK;
-  uint32_t c0 = chunk_off[b], c1 = chunk_off[b + 1];
+  uint32_t side = sb / nbk, b = sb % nbk;
+  uint32_t c0 = chunk_off[b], c1 = side && b >= MSM_NBK ? c0 : chunk_off[b + 1];
   G2J acc = jac_infinity<Fp2>();
   for (uint32_t c = c0 + q; c < c1; c += MSM_BSPLIT) acc = jac_add(acc, load_g2j(chunks[side * max_chunks + c]));
   store_g2j(BP[g], acc);
@@ -150,13 +177,14 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_buckets(uint32_t max_
 
 // Bucket aggregation by bit slices: sum_b b B_b = sum_k 2^k S_k with S_k = sum of the buckets whose
 // digit b has bit k set (128 of the 255).  Level 1: lane (side, w, k, c < 16) sums 8 of those buckets.
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_slices(uint32_t nsides, const G2JStore* B, G2JStore* P1) {
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_slices(uint32_t nsides, uint32_t nwin, const G2JStore* B,
+                                                                  G2JStore* P1) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nsides * MSM_WIN * MSM_C * 16) return;
-  uint32_t c = g % 16, k = (g / 16) % MSM_C, w = (g / (16 * MSM_C)) % MSM_WIN, side = g / (16 * MSM_C * MSM_WIN);
-  const G2JStore* Bw = B + side * MSM_NBK + w * MSM_NB;
+  if (g >= nsides * nwin * MSM_C * 16) return;
+  uint32_t c = g % 16, k = (g / 16) % MSM_C, w = (g / (16 * MSM_C)) % nwin, side = g / (16 * MSM_C * nwin);
+  const G2JStore* Bw = B + (side * nwin + w) * MSM_NB;
   G2J acc = jac_infinity<Fp2>();
-  for (uint32_t i = 8 * c; i < 8 * c + 8; ++i) {
+  for (uint32_t i = 8 * c; i < (side && w >= MSM_WIN ? 0 : 8 * c + 8); ++i) {
     // i-th digit in 0..255 with bit k set: insert a 1 at bit k of i
     uint32_t b = ((i >> k) << (k + 1)) | (1u << k) | (i & ((1u << k) - 1));
     acc = jac_add(acc, load_g2j(Bw[b]));
@@ -165,11 +193,12 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_slices(uint32_t nside
 }
 
 // one 128-lane workgroup per (side, window): W_w = sum_k 2^k S_{w,k} (Horner with cooperative doublings
-// and additions, coop.h), then 2^(8w) W_w
-DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_horner_coop(const G2JStore* S, G2JStore* Wout) {
+// and additions, coop.h), then 2^(8w) W_w (alpha windows; test windows stay unshifted, side 1 has none)
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_horner_coop(uint32_t nwin, const G2JStore* S, G2JStore* Wout) {
   __shared__ CoG2Tmp tmp;
   __shared__ CoG2 acc, nxt;
-  const uint32_t sw = blockIdx.x, w = sw % MSM_WIN;
+  const uint32_t sw = blockIdx.x, w = sw % nwin;
+  if (sw >= nwin && w >= MSM_WIN) return;
   const G2JStore* Sw = S + sw * MSM_C;
   CO_SERIAL({
     G2J a = load_g2j(Sw[MSM_C - 1]);
@@ -183,27 +212,44 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_horner_coop(const G2J
     });
     co_g2_add(&acc, &acc, &nxt, &tmp);
   }
-  for (uint32_t d = 0; d < MSM_C * w; ++d) co_g2_dbl(&acc, &tmp);
+  for (uint32_t d = 0; d < (w < MSM_WIN ? MSM_C * w : 0u); ++d) co_g2_dbl(&acc, &tmp);
   CO_SERIAL(store_g2j(Wout[sw], G2J{acc.x, acc.y, acc.z}));
 }
 
-// one 128-lane workgroup per side: out[side] = sum_w W[side][w]
-DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_final_coop(const G2JStore* W, G2JStore* out) {
+// one 128-lane workgroup per side: out[side] = sum_{w < MSM_WIN} W[side][w]
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_final_coop(uint32_t nwin, const G2JStore* W, G2JStore* out) {
   __shared__ CoG2Tmp tmp;
   __shared__ CoG2 acc, nxt;
   const uint32_t side = blockIdx.x;
   CO_SERIAL({
-    G2J a = load_g2j(W[side * MSM_WIN]);
+    G2J a = load_g2j(W[side * nwin]);
     acc = CoG2{a.x, a.y, a.z};
   });
   for (uint32_t w = 1; w < MSM_WIN; ++w) {
     CO_SERIAL({
-      G2J a = load_g2j(W[side * MSM_WIN + w]);
+      G2J a = load_g2j(W[side * nwin + w]);
       nxt = CoG2{a.x, a.y, a.z};
     });
     co_g2_add(&acc, &acc, &nxt, &tmp);
   }
   CO_SERIAL(store_g2j(out[side], G2J{acc.x, acc.y, acc.z}));
+}
+
+// batched subgroup check: one 128-lane workgroup per side-0 window sum W[w] tests psi(P) == [z]P
+// cooperatively (coop.h); any failure clears flag[0] (the batch verdict written by k_final_coop), so the
+// per-item pass runs
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_subgroup(const G2JStore* W, uint32_t* flag) {
+  __shared__ CoG2Tmp tmp;
+  __shared__ CoG2 p, zp, pp;
+  CO_SERIAL({
+    G2J a = load_g2j(W[blockIdx.x]);
+    p = CoG2{a.x, a.y, a.z};
+  });
+  co_g2_mul_z(&zp, &p, &tmp);
+  co_g2_psi(&pp, &p, &tmp);
+  CO_SERIAL({
+    if (!jac_eq(G2J{pp.x, pp.y, pp.z}, G2J{zp.x, zp.y, zp.z})) flag[0] = 0u;
+  });
 }
 
 // ---------------------------------------------------------------------------------------------------

@@ -280,3 +280,58 @@ def test_valid_partial_batches_pass_on_the_batch_path():
         st = tbls.verify_partial_batch(pub, msgs, parts, seed=seed)
         assert not st.any()
         assert L.last_batch_flags() == (True, False), seed
+
+
+def test_torsion_signatures_rejected_like_the_twin():
+    """On-curve signatures outside G2 (sigma + E with E of order 13, 23, 299; uncleared hash outputs,
+    tests/golden/g2_torsion.json): the beacon path decodes without a per-item subgroup check and batches
+    it on the MSM window sums (msm.h), so each such item must still end as a decode error (status 2),
+    alone in an otherwise valid chain and all together, for many seeds, exactly as the twin's per-item
+    bls.Verify (decode with subgroup check) says."""
+    c = chain()
+    pr, rr, ps, sigs, msgs = chain_arrays(c)
+    pk = hx(c["pk"])
+    cases = load("g2_torsion.json")["cases"]
+    for case in cases:
+        i = case["round_index"]
+        bad = sigs.copy()
+        bad[i] = np.frombuffer(hx(case["sig"]), np.uint8)
+        assert twin.verify(pk, bytes(msgs[i]), bytes(bad[i])) == L.ST_SIG_DECODE
+        for seed in (3, 4, 5):
+            st = tbls.verify_beacons(pk, pr, rr, ps, bad, seed=seed)
+            assert np.nonzero(st)[0].tolist() == [i], (case["kind"], seed)
+            assert st[i] == L.ST_SIG_DECODE
+            assert L.last_batch_flags()[0] is False  # the batch check caught it
+    bad = sigs.copy()
+    idx = [case["round_index"] for case in cases]
+    for case in cases:
+        bad[case["round_index"]] = np.frombuffer(hx(case["sig"]), np.uint8)
+    bad[7] = sigs[8]  # plus a wrong-round signature (pairing failure)
+    want = [twin.verify(pk, bytes(msgs[j]), bytes(bad[j])) for j in range(len(rr))]
+    for seed in range(20, 30):
+        st = tbls.verify_beacons(pk, pr, rr, ps, bad, seed=seed)
+        assert list(st) == want
+    assert sorted(np.nonzero(want)[0].tolist()) == sorted(idx + [7])
+
+
+def test_torsion_signature_in_a_large_batch():
+    """One valid signature plus a torsion point E (ord 13) among 4096 GPU-signed valid rounds: exactly
+    that item is rejected, as a decode error."""
+    from oracle.pyref import bls12381 as B
+
+    R = 4096
+    x = S.master_secret()
+    pk = twin.g1_mul_gen(x)
+    case = load("g2_torsion.json")["cases"][0]
+    j = case["round_index"]
+    e = B.G2C.add(B.g2_decompress(hx(case["sig"]), subgroup_check=False),
+                  B.G2C.neg(B.g2_decompress(hx(chain()["rounds"][j]["sig"]))))
+    msgs = np.frombuffer(b"".join(hashlib.sha256(b"tor/%d" % r).digest() for r in range(R)), np.uint8).reshape(R, 32)
+    sigs = tbls.sign_batch([x] * R, msgs)
+    st = tbls.verify_recovered_batch(pk, msgs, sigs, seed=31)
+    assert not st.any() and L.last_batch_flags() == (True, False)
+    bad = B.g2_compress(B.G2C.add(B.g2_decompress(bytes(sigs[1234])), e))
+    assert twin.verify(pk, bytes(msgs[1234]), bad) == L.ST_SIG_DECODE
+    sigs[1234] = np.frombuffer(bad, np.uint8)
+    st = tbls.verify_recovered_batch(pk, msgs, sigs, seed=32)
+    assert np.nonzero(st)[0].tolist() == [1234] and st[1234] == L.ST_SIG_DECODE

@@ -173,3 +173,18 @@ def test_group_commits_fixture():
         for j in (1, t - 1):
             assert twin.g1_mul_gen(coeffs[j]).hex() == g["t%d" % t][j]
     assert g["t3"] == chain()["commits"]
+
+
+def test_torsion_fixture_decodes_outside_g2():
+    """tests/golden/g2_torsion.json: on the curve (decodes without the subgroup check), outside G2, and
+    the twin's bls.Verify rejects each as a decode error."""
+    from oracle.pyref import bls12381 as B
+    from tests.fixtures import chain, hx, load
+
+    c = chain()
+    pk = hx(c["pk"])
+    for case in load("g2_torsion.json")["cases"]:
+        pt = B.g2_decompress(hx(case["sig"]), subgroup_check=False)
+        assert B.G2C.on_curve(pt) and not B.g2_in_subgroup(pt)
+        msg = hx(c["rounds"][case["round_index"]]["msg"])
+        assert twin.verify(pk, msg, hx(case["sig"])) == 2

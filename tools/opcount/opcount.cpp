@@ -26,11 +26,12 @@ void oc_h2c_uncleared(const uint8_t* msg, uint32_t len, const uint8_t* dst, uint
   (void)q;
   take(out);
 }
-// g2_decompress + subgroup check -- k_decode_items per item; returns decode ok
-int oc_decode_g2(const uint8_t* sig96, uint64_t* out) {
+// g2_decompress (+ subgroup check when `subgroup`: multi-key batches; the beacon path batches it on the
+// MSM window sums) -- k_decode_items per item; returns decode ok
+int oc_decode_g2(const uint8_t* sig96, int subgroup, uint64_t* out) {
   reset();
   G2A a;
-  bool ok = g2_decompress(a, sig96, true);
+  bool ok = g2_decompress(a, sig96, subgroup != 0);
   take(out);
   return ok;
 }

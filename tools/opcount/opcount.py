@@ -42,8 +42,10 @@ def main():
         alpha = int.from_bytes(hashlib.sha256(b"a%d" % i).digest()[:8], "big") | 1
         L.oc_h2c_uncleared(msg, 32, DST, len(DST), o)
         add("k_h2c_uncleared")
-        assert L.oc_decode_g2(sig, o) == 1
-        add("k_decode_items")
+        assert L.oc_decode_g2(sig, 0, o) == 1
+        add("k_decode_items")  # one key, one item per round: subgroup check batched (msm.h)
+        assert L.oc_decode_g2(sig, 1, o) == 1
+        add("k_decode_items[+subgroup]")
         L.oc_round_combine(msg, 32, DST, len(DST), sig, ctypes.c_uint64(alpha), o)
         add("k_round_combine (k > 1)")
         L.oc_scale_item(sig, ctypes.c_uint64(alpha), o)
