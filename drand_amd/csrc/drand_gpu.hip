@@ -59,6 +59,16 @@ struct Ctx {
   uint8_t pk_bytes[48];
   bool pk_valid = false;
   unsigned long long* fallbacks = nullptr;  // device counter (k_count_fallback)
+  // share keys X_i = PubPoly.Eval(i) of the multi-key paths for the last (commits, distinct indices):
+  // a drand group verifies every round against the same polynomial (the reference's build caches X_i
+  // per group too), and decode + Horner are latency-bound single-lane jobs of ~15 ms
+  G1AStore* poly_keys = nullptr;
+  uint8_t* poly_kst = nullptr;
+  size_t poly_cap = 0;
+  hipEvent_t poly_ready = nullptr;
+  std::vector<uint8_t> poly_commits;
+  std::vector<uint32_t> poly_idx;
+  bool poly_valid = false;
 };
 
 std::mutex g_mu;
@@ -78,7 +88,7 @@ int fail(int code, const std::string& msg) {
 
 // workspace slots
 enum Slot {
-  S_MSGS, S_DST, S_Q, S_S, S_U, S_STATUS, S_ISO, S_CELL, S_W, S_A, S_TMP, S_KP, S_F, S_H, S_FLAG, S_KEYS, S_KEYST,
+  S_MSGS, S_DST, S_Q, S_S, S_U, S_STATUS, S_ISO, S_CELL, S_W, S_A, S_TMP, S_KP, S_F, S_H, S_FLAG, S_KEYS, S_KEYST, S_XC,
   S_COMMITS, S_COMMITST, S_SLOTIDX, S_ITEMSLOT, S_SEL, S_SELIDX, S_RST, S_SST, S_TERMS, S_IN0, S_IN1, S_IN2, S_IN3,
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
@@ -269,49 +279,54 @@ int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA
   RET(reduce_rows(BP, tmp, nbk * nsides, MSM_BSPLIT, st));  // B[side][b] = BP[side * nbk + b]
   RET(launch("k_msm_slices", k_msm_slices, nsides * nwin * MSM_C * 16, 128, st, nsides, nwin, (const G2JStore*)BP, P1));
   RET(reduce_rows(P1, tmp, nsides * nwin * MSM_C, 16, st, 4));  // S[side][w][k] = P1[...]
-  RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * nwin * nsides, 128, st, nwin, (const G2JStore*)P1, W));
+  RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * nwin * nsides, 128, st, nwin, 1u, (const G2JStore*)P1, W));
   RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsides, 128, st, nwin, (const G2JStore*)W, *out));
   if (win) *win = W;
   return 0;
 }
 
 // Keyed MSM (msm.h) of the multi-key batch: T = sum_s beta_s sum_{items i of slot s} alpha_{r(i)} S_i.
-int msm_run_keyed(const Batch& b, uint64_t seed, const uint8_t* iso, G2JStore** T, hipStream_t st) {
-  const uint32_t N = b.R * b.k, nsets = b.nslots, nkeys = MSM_NBK * nsets;
+// With `test_windows` every key set also gets the MSM_TWIN test windows; *win = the nsets x MSM_WT window
+// sums of the batched subgroup check.
+int msm_run_keyed(const Batch& b, uint64_t seed, const uint8_t* iso, bool test_windows, G2JStore** T, G2JStore** win,
+                  hipStream_t st) {
+  const uint32_t nwin = test_windows ? MSM_WT : MSM_WIN;
+  const uint32_t N = b.R * b.k, nsets = b.nslots, nkeys = nwin * MSM_NB * nsets;
   const uint32_t nblocks = (nkeys + KSCAN_B - 1) / KSCAN_B;
   uint32_t *cnt, *tot, *list;
   G2JStore *chunks, *B, *P1, *tmp, *W, *Ts, *BT;
   RET(wsT(S_KMSM_CNT, (size_t)4 * nkeys + 1, &cnt));
   uint32_t *offset = cnt + nkeys, *cursor = offset + nkeys, *chunk_off = cursor + nkeys;  // chunk_off: nkeys + 1
   RET(wsT(S_KMSM_TOT, (size_t)2 * nblocks, &tot));
-  RET(wsT(S_KMSM_LIST, (size_t)MSM_WIN * N + 1, &list));
-  const uint32_t max_chunks = N + nkeys;  // sum of ceil(count / 8) <= 8N / 8 + nkeys
+  RET(wsT(S_KMSM_LIST, (size_t)nwin * N + 1, &list));
+  const uint32_t max_chunks = (nwin * N) / MSM_CHUNK + 1 + nkeys;  // sum of ceil(count / 8) <= nwin N / 8 + nkeys
   RET(wsT(S_KMSM_CHUNKS, max_chunks, &chunks));
   RET(wsT(S_KMSM_B, nkeys, &B));
-  RET(wsT(S_KMSM_P1, (size_t)nsets * MSM_WIN * MSM_C * 16, &P1));
-  RET(wsT(S_KMSM_TMP, (size_t)nsets * MSM_WIN * MSM_C * 16, &tmp));
-  RET(wsT(S_KMSM_W, (size_t)nsets * MSM_WIN, &W));
+  RET(wsT(S_KMSM_P1, (size_t)nsets * nwin * MSM_C * 16, &P1));
+  RET(wsT(S_KMSM_TMP, (size_t)nsets * nwin * MSM_C * 16, &tmp));
+  RET(wsT(S_KMSM_W, (size_t)nsets * nwin, &W));
   RET(wsT(S_KMSM_T, nsets, &Ts));
   RET(wsT(S_KMSM_BT, nsets, &BT));
   HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * nkeys, st));
-  RET(launch("k_kmsm_count", k_kmsm_count, N, 256, st, N, b.k, nsets, seed, b.item_slot, (const uint8_t*)b.status,
+  RET(launch("k_kmsm_count", k_kmsm_count, N, 256, st, N, b.k, nsets, nwin, seed, b.item_slot, (const uint8_t*)b.status,
              iso, cnt));
   RET(launch("k_kscan_local", k_kscan_local, nblocks * 256, 256, st, nkeys, (const uint32_t*)cnt, offset, chunk_off,
              tot));
   RET(launch("k_kscan_top", k_kscan_top, 64, 64, st, nblocks, nkeys, tot, chunk_off));
   RET(launch("k_kscan_add", k_kscan_add, nkeys, 256, st, nkeys, (const uint32_t*)tot, offset, cursor, chunk_off));
-  RET(launch("k_kmsm_scatter", k_kmsm_scatter, N, 256, st, N, b.k, nsets, seed, b.item_slot,
+  RET(launch("k_kmsm_scatter", k_kmsm_scatter, N, 256, st, N, b.k, nsets, nwin, seed, b.item_slot,
              (const uint8_t*)b.status, iso, cursor, list));
   RET(launch("k_kmsm_chunks", k_kmsm_chunks, max_chunks, 128, st, max_chunks, nkeys, (const uint32_t*)cnt,
              (const uint32_t*)offset, (const uint32_t*)chunk_off, (const uint32_t*)list, (const G2AStore*)b.S,
              chunks));
   RET(launch("k_kmsm_buckets", k_kmsm_buckets, nkeys, 128, st, nkeys, (const uint32_t*)chunk_off,
              (const G2JStore*)chunks, B));
-  RET(launch("k_kmsm_slices", k_kmsm_slices, nsets * MSM_WIN * MSM_C * 16, 128, st, nsets, (const G2JStore*)B, P1));
-  RET(reduce_rows(P1, tmp, nsets * MSM_WIN * MSM_C, 16, st, 4));  // S[set][w][k] = P1[...]
-  RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * MSM_WIN * nsets, 128, st, MSM_WIN, (const G2JStore*)P1, W));
-  RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsets, 128, st, MSM_WIN, (const G2JStore*)W, Ts));
-  RET(launch("k_kmsm_beta", k_kmsm_beta, nsets, 64, st, nsets, seed, (const G2JStore*)Ts, BT));
+  RET(launch("k_kmsm_slices", k_kmsm_slices, nsets * nwin * MSM_C * 16, 128, st, nsets, nwin, (const G2JStore*)B, P1));
+  RET(reduce_rows(P1, tmp, nsets * nwin * MSM_C, 16, st, 4));  // S[set][w][k] = P1[...]
+  RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * nwin * nsets, 128, st, nwin, nsets, (const G2JStore*)P1, W));
+  RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsets, 128, st, nwin, (const G2JStore*)W, Ts));
+  if (win) *win = W;
+  RET(launch("k_kmsm_beta", k_kmsm_beta, 128 * nsets, 128, st, seed, (const G2JStore*)Ts, BT));
   RET(reduce_rows(BT, tmp, 1, nsets, st));  // T = BT[0]
   *T = BT;
   return 0;
@@ -334,19 +349,20 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   } else {
     RET(wsT(S_A, b.R, &A));
   }
-  RET(wsT(S_F, b.nslots + 1, &f));
+  RET(wsT(S_F, b.nslots + 2, &f));
   HIPCHK(hipMemsetAsync(cell, 0, sizeof(uint32_t) * (size_t)b.R * b.nslots, st));
-  // one key, one item per round: the G2 subgroup checks of the signatures are batched on the MSM's window
-  // sums (msm.h) instead of a psi check per item
-  const uint32_t batched_sub = (b.nslots == 1 && b.k == 1) ? 1u : 0u;
+  // one item per (round, key): the G2 subgroup checks of the signatures are batched on the MSM's window
+  // sums (msm.h) instead of a psi check per item (several items of one key in a round share their digits)
+  const uint32_t batched_sub = (b.nslots > 1 || b.k == 1) ? 1u : 0u;
   RET(launch("k_decode_items", k_decode_items, N, 128, st, N, b.k, b.nslots, b.sigs, b.stride, b.offset, b.item_slot,
              b.key_status, b.S, b.status, cell, iso, 1u - batched_sub));
   if (b.nslots == 1)
     RET(launch("k_scale_items", k_scale_items, N, 128, st, N, b.nslots, seed, b.item_slot, (const G2AStore*)b.S,
                (const uint8_t*)b.status, (const uint8_t*)iso, U));
   RET(launch("k_round_combine", k_round_combine, b.R, 128, st, b.R, b.k, b.nslots, seed, (const G2JStore*)U,
-             (const uint8_t*)b.status, (const uint8_t*)iso, b.Q, V, A, active));
-  const G2JStore *T, *K;
+             (const uint8_t*)b.status, (const uint8_t*)iso, b.Q, (const uint32_t*)cell, V, A, active));
+  const G2JStore *T, *K, *Kc = nullptr;
+  G1AStore* Xc = nullptr;
   G2JStore* win = nullptr;
   if (b.nslots == 1) {
     // T = sum alpha_r V_r and K = sum alpha_r Q_r in one MSM (shared bucket sort)
@@ -355,7 +371,7 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
     K = msm + 1;
   } else {
     // T = sum_s beta_s sum_{i in s} alpha_{r(i)} S_i by the keyed MSM (no per-item scalar multiplication)
-    RET(msm_run_keyed(b, seed, iso, &msm, st));
+    RET(msm_run_keyed(b, seed, iso, batched_sub != 0, &msm, &win, st));
     T = msm;
     uint32_t nchunks = 16384 / b.nslots;
     if (nchunks < 1) nchunks = 1;
@@ -365,13 +381,23 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
     RET(wsT(S_KP, (size_t)b.nslots * nchunks, &Kp));
     RET(wsT(S_TMP, (size_t)b.nslots * nchunks, &tmp));
     RET(launch("k_key_accum", k_key_accum, b.nslots * nchunks, 128, st, b.R, b.nslots, chunk, nchunks,
-               (const uint32_t*)cell, (const G2JStore*)A, Kp));
-    RET(reduce_rows(Kp, tmp, b.nslots, nchunks, st));  // K_s = Kp[s]
+               (const uint32_t*)cell, (const uint8_t*)active, (const G2JStore*)A, Kp));
+    RET(reduce_rows(Kp, tmp, b.nslots, nchunks, st));  // -C_s = Kp[s]
     K = Kp;
+    // Kc = sum over the active rounds of alpha_r Q_r (one MSM), Xc = sum_s beta_s X_s
+    G2JStore* kmsm;
+    RET(msm_run(b.R, seed, active, b.Q, nullptr, false, &kmsm, nullptr, st));
+    Kc = kmsm;
+    RET(wsT(S_XC, 1, &Xc));
+    RET(launch("k_key_combine", k_key_combine, 256, 256, st, b.nslots, seed, b.keys, b.key_status, Xc));
   }
-  RET(launch("k_pair_miller_coop", k_pair_miller_coop, 128 * (b.nslots + 1), 128, st, b.nslots, seed, b.keys, K, T, f));
-  RET(launch("k_final_coop", k_final_coop, 128, 128, st, b.nslots + 1, (const Fp12*)f, flag));
-  if (batched_sub) RET(launch("k_msm_subgroup", k_msm_subgroup, 128 * MSM_WT, 128, st, (const G2JStore*)win, flag));
+  const uint32_t npairs = b.nslots + (b.nslots > 1 ? 2u : 1u);
+  RET(launch("k_pair_miller_coop", k_pair_miller_coop, 128 * npairs, 128, st, b.nslots, seed, b.keys, K, T,
+             (const G1AStore*)Xc, Kc, f));
+  RET(launch("k_final_coop", k_final_coop, 128, 128, st, npairs, (const Fp12*)f, flag));
+  if (batched_sub)  // every window sum of the signature side: MSM_WT, or MSM_WT per key set
+    RET(launch("k_msm_subgroup", k_msm_subgroup, 128 * MSM_WT * (b.nslots > 1 ? b.nslots : 1u), 128, st,
+               (const G2JStore*)win, flag));
   // isolated items present?  The per-item pass decides on the device (no host round trip), so a batch
   // is one stream-ordered sequence of launches.
   HIPCHK(hipMemsetAsync(flag + 1, 0, 4, st));
@@ -438,6 +464,51 @@ int verify_single_key(const uint8_t* pk48_host, uint32_t n, const uint8_t* d_msg
   return 0;
 }
 
+// X_i = PubPoly.Eval(i) for the distinct indices idx (slot order), from the context cache when the commits
+// and indices are those of the previous call
+int poly_keys(const uint8_t* commits48, uint32_t t, const std::vector<uint32_t>& idx, hipStream_t st, G1AStore** keys,
+              uint8_t** kst) {
+  Ctx& c = g_ctx;
+  const uint32_t nslots = (uint32_t)idx.size();
+  if (c.poly_valid && c.poly_idx == idx && c.poly_commits.size() == (size_t)t * 48 &&
+      memcmp(c.poly_commits.data(), commits48, (size_t)t * 48) == 0) {
+    HIPCHK(hipStreamWaitEvent(st, c.poly_ready, 0));
+    *keys = c.poly_keys;
+    *kst = c.poly_kst;
+    return 0;
+  }
+  // the multi-key entry points are blocking, so no batch in flight reads the cached keys
+  c.poly_valid = false;
+  if (!c.poly_ready) HIPCHK(hipEventCreateWithFlags(&c.poly_ready, hipEventDisableTiming));
+  if (c.poly_cap < nslots) {
+    if (c.poly_keys) HIPCHK(hipFree(c.poly_keys));
+    if (c.poly_kst) HIPCHK(hipFree(c.poly_kst));
+    c.poly_keys = nullptr;
+    c.poly_kst = nullptr;
+    c.poly_cap = 0;
+    HIPCHK(hipMalloc(&c.poly_keys, sizeof(G1AStore) * nslots));
+    HIPCHK(hipMalloc(&c.poly_kst, nslots));
+    c.poly_cap = nslots;
+  }
+  uint8_t *d_c, *d_cst;
+  G1AStore* cA;
+  uint32_t* d_slotidx;
+  RET(upload(S_IN0, commits48, (size_t)t * 48, &d_c, st));
+  RET(wsT(S_COMMITS, t, &cA));
+  RET(wsT(S_COMMITST, t, &d_cst));
+  RET(launch("k_decode_g1", k_decode_g1, t, 64, st, t, (const uint8_t*)d_c, cA, d_cst));
+  RET(upload(S_SLOTIDX, idx.data(), nslots, &d_slotidx, st));
+  RET(launch("k_pubpoly_eval", k_pubpoly_eval, nslots, 64, st, nslots, t, (const G1AStore*)cA, (const uint8_t*)d_cst,
+             (const uint32_t*)d_slotidx, c.poly_keys, c.poly_kst, (uint8_t*)nullptr));
+  HIPCHK(hipEventRecord(c.poly_ready, st));
+  c.poly_commits.assign(commits48, commits48 + (size_t)t * 48);
+  c.poly_idx = idx;
+  c.poly_valid = true;
+  *keys = c.poly_keys;
+  *kst = c.poly_kst;
+  return 0;
+}
+
 // VerifyPartial over R rounds x k partials: keys X_i = PubPoly.Eval(i) for every distinct index
 int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const uint8_t* msgs, uint32_t msg_len,
                         uint32_t k, const uint8_t* partials98, uint64_t seed, hipStream_t st, uint8_t** d_status,
@@ -455,19 +526,11 @@ int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const 
     item_slot[i] = (uint32_t)slot_of[idx];
   }
   uint32_t nslots = (uint32_t)slot_idx.size();
-  uint8_t *d_c, *d_cst, *d_m, *d_p, *kst;
-  G1AStore *cA, *keys;
-  uint32_t *d_slotidx, *d_itemslot;
-  RET(upload(S_IN0, commits48, (size_t)t * 48, &d_c, st));
-  RET(wsT(S_COMMITS, t, &cA));
-  RET(wsT(S_COMMITST, t, &d_cst));
-  RET(launch("k_decode_g1", k_decode_g1, t, 64, st, t, (const uint8_t*)d_c, cA, d_cst));
-  RET(upload(S_SLOTIDX, slot_idx.data(), nslots, &d_slotidx, st));
+  uint8_t *d_m, *d_p, *kst;
+  G1AStore* keys;
+  uint32_t* d_itemslot;
+  RET(poly_keys(commits48, t, slot_idx, st, &keys, &kst));
   RET(upload(S_ITEMSLOT, item_slot.data(), N, &d_itemslot, st));
-  RET(wsT(S_KEYS, nslots, &keys));
-  RET(wsT(S_KEYST, nslots, &kst));
-  RET(launch("k_pubpoly_eval", k_pubpoly_eval, nslots, 64, st, nslots, t, (const G1AStore*)cA, (const uint8_t*)d_cst,
-             (const uint32_t*)d_slotidx, keys, kst, (uint8_t*)nullptr));
   RET(upload(S_MSGS, msgs, (size_t)R * msg_len, &d_m, st));
   RET(upload(S_IN1, partials98, N * 98, &d_p, st));
   G2JStore* Q;
@@ -531,6 +594,14 @@ void dg_shutdown(void) {
   if (g_ctx.pk_ready) (void)hipEventDestroy(g_ctx.pk_ready);
   if (g_ctx.fallbacks) (void)hipFree(g_ctx.fallbacks);
   g_ctx.fallbacks = nullptr;
+  if (g_ctx.poly_keys) (void)hipFree(g_ctx.poly_keys);
+  if (g_ctx.poly_kst) (void)hipFree(g_ctx.poly_kst);
+  if (g_ctx.poly_ready) (void)hipEventDestroy(g_ctx.poly_ready);
+  g_ctx.poly_keys = nullptr;
+  g_ctx.poly_kst = nullptr;
+  g_ctx.poly_ready = nullptr;
+  g_ctx.poly_cap = 0;
+  g_ctx.poly_valid = false;
   g_ctx.pk_dev = nullptr;
   g_ctx.pk_status = nullptr;
   g_ctx.pk_raw = nullptr;

@@ -276,13 +276,15 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_scale_items(uint32_t n, u
 #endif
 
 // per round r: V_r = sum_j U_{r,j} over its batch items, active[r] = (any batch item); with several
-// key slots also A_r = alpha_r Q_r (the per-key hash sums are masked by the cell map, so they are not a
-// single MSM); the alpha_r-weighted sums of V (and of Q with one key) are Pippenger MSMs (msm.h)
+// key slots also A_r = alpha_r Q_r, but only for an active round with an empty (r, s) cell: the hash side
+// of key s is K_s = K - C_s with K = sum over the active rounds of alpha_r Q_r (one Pippenger MSM, msm.h)
+// and C_s = sum of A_r over the active rounds without an item of s (k_key_accum) -- nothing when every
+// share is present in every round
 #if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_round_combine(uint32_t R, uint32_t k, uint32_t nslots, uint64_t seed,
                                                       const G2JStore* U, const uint8_t* status,
-                                                      const uint8_t* isolate, const G2JStore* Q, G2JStore* V,
-                                                      G2JStore* A, uint8_t* active) {
+                                                      const uint8_t* isolate, const G2JStore* Q, const uint32_t* cell,
+                                                      G2JStore* V, G2JStore* A, uint8_t* active) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   bool any = false;
@@ -296,22 +298,48 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_round_combine(uint32_t R,
   }
   if (V) store_g2j(V[r], v);  // V (and U) only on the single-key path; the keyed MSM reads S directly
   active[r] = any ? 1 : 0;
-  if (nslots > 1) store_g2j(A[r], any ? jac_mul_u64(load_g2j(Q[r]), rlc_alpha(seed, r)) : jac_infinity<Fp2>());
+  if (nslots > 1) {
+    bool gap = false;
+    for (uint32_t s = 0; any && s < nslots && !gap; ++s) gap = cell[(size_t)r * nslots + s] == 0u;
+    if (gap) store_g2j(A[r], jac_mul_u64(load_g2j(Q[r]), rlc_alpha(seed, r)));
+  }
 }
 #endif
 
-// Kp[s * nchunks + c] = sum of A_r over rounds r in chunk c whose (r, s) cell holds a batch item
+// Kp[s * nchunks + c] = -(sum of A_r over the active rounds r in chunk c without an item of key s), so the
+// row sums are -C_s (k_round_combine)
 #if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_key_accum(uint32_t R, uint32_t nslots, uint32_t chunk, uint32_t nchunks,
-                                                  const uint32_t* cell, const G2JStore* A, G2JStore* Kp) {
+                                                  const uint32_t* cell, const uint8_t* active, const G2JStore* A,
+                                                  G2JStore* Kp) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nslots * nchunks) return;
   uint32_t s = g / nchunks, c = g % nchunks;
   uint32_t a = c * chunk, b = a + chunk < R ? a + chunk : R;
   G2J acc = jac_infinity<Fp2>();
   for (uint32_t r = a; r < b; ++r)
-    if (cell[(size_t)r * nslots + s]) acc = jac_add(acc, load_g2j(A[r]));
-  store_g2j(Kp[g], acc);
+    if (active[r] && !cell[(size_t)r * nslots + s]) acc = jac_add(acc, load_g2j(A[r]));
+  store_g2j(Kp[g], jac_neg(acc));
+}
+
+// Xc = sum_s beta_s X_s over the key slots with a decoded key: per-lane 64-bit products, LDS tree sum
+DG_KERNEL void __launch_bounds__(256) k_key_combine(uint32_t nslots, uint64_t seed, const G1AStore* keys,
+                                                   const uint8_t* key_status, G1AStore* out) {
+  __shared__ G1J part[256];
+  const uint32_t t = threadIdx.x;
+  G1J acc = jac_infinity<Fp>();
+  for (uint32_t s = t; s < nslots; s += 256) {
+    G1A a = load_g1a(keys[s]);
+    if (key_status[s] != DG_ST_OK_ || a.inf) continue;
+    acc = jac_add(acc, jac_mul_u64(jac_from_aff(a), rlc_beta(seed, s)));
+  }
+  part[t] = acc;
+  __syncthreads();
+  for (uint32_t w = 128; w > 0; w >>= 1) {
+    if (t < w) part[t] = jac_add(part[t], part[t + w]);
+    __syncthreads();
+  }
+  if (t == 0) store_g1a(out[0], g1_to_aff(part[0]));
 }
 #endif
 
@@ -333,11 +361,13 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_sum_rows(uint32_t rows, u
 
 // Pair s on one 128-lane workgroup (coop.h): P side and Q side prepared cooperatively (for key pairs the
 // hash-side sum is cofactor-cleared here, once per key and batch), then the cooperative Miller loop.
-// Pairs: (beta_s X_s, h_eff K_s) for s < nslots, (-g1, T) for s == nslots; f[s] = 1
-// when a side is the identity.
+// Pairs: (beta_s X_s, h_eff K_s) for s < nslots, (-g1, T) for s == nslots; with several keys (Kc given)
+// K_s = -C_s and one more pair (Xc, h_eff Kc), Xc = sum_s beta_s X_s: prod_s e(beta_s X_s, h(Kc - C_s)).
+// f[s] = 1 when a side is the identity (every correction pair when all shares are present).
 #if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_pair_miller_coop(uint32_t nslots, uint64_t seed, const G1AStore* keys,
-                                                         const G2JStore* K, const G2JStore* T, Fp12* f) {
+                                                         const G2JStore* K, const G2JStore* T, const G1AStore* Xc,
+                                                         const G2JStore* Kc, Fp12* f) {
   __shared__ CoGT gt;
   __shared__ CoML ml;
   __shared__ CoG2Tmp g2t;
@@ -345,16 +375,23 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_pair_miller_coop(uint32_t
   __shared__ Fp12W F, L;
   __shared__ uint32_t skip;
   const uint32_t s = blockIdx.x;
-  if (s < nslots) {
+  if (s < nslots || s == nslots + 1) {
     CO_SERIAL({
-      G1A pa = load_g1a(keys[s]);  // decoded keys are affine already; with one key beta = 1
-      if (nslots > 1) pa = g1_to_aff(jac_mul_u64(jac_from_aff(pa), rlc_beta(seed, s)));
-      ml.px = pa.x;
-      ml.py = pa.y;
-      skip = pa.inf ? 1u : 0u;
-      G2J k = load_g2j(K[s]);
+      G2J k = load_g2j(s < nslots ? K[s] : Kc[0]);
       Kp = CoG2{k.x, k.y, k.z};
+      skip = jac_is_inf(k) ? 1u : 0u;
+      if (!skip) {
+        G1A pa = load_g1a(s < nslots ? keys[s] : Xc[0]);  // decoded keys are affine already; one key: beta = 1
+        if (s < nslots && nslots > 1) pa = g1_to_aff(jac_mul_u64(jac_from_aff(pa), rlc_beta(seed, s)));
+        ml.px = pa.x;
+        ml.py = pa.y;
+        skip = pa.inf ? 1u : 0u;
+      }
     });
+    if (skip) {
+      if (threadIdx.x == 0) f[s] = fp12_one();
+      return;
+    }
     co_g2_clear_cofactor(&Kp, tp, &g2t);
     CO_SERIAL({
       G2A qa = g2_to_aff(G2J{Kp.x, Kp.y, Kp.z});
@@ -509,20 +546,24 @@ DG_KERNEL void __launch_bounds__(128) k_recover_select(uint32_t R, uint32_t k, u
 }
 #endif
 
-// thread (r, m): lambda_m * S_{r, sel[m]}  (lambda over the round's t selected indices)
+// thread (m, r), rounds fastest: terms[r * t + m] = lambda_m * S_{r, sel[m]} (lambda over the round's t
+// selected indices).  A wave covers 64 rounds of the same position m, so while the rounds select the same
+// index set (every round with no bad share among its first t) its lanes share lambda_m and the scalar
+// multiplication's digit-dependent branches are uniform across the wave.
 #if !DG_TU_HOT
 DG_KERNEL void __launch_bounds__(64) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
                                                      const uint32_t* selidx, const uint8_t* round_status,
                                                      const G2AStore* S, G2JStore* terms) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= R * t) return;
-  uint32_t r = g / t, m = g % t;
+  uint32_t m = g / R, r = g % R;
+  size_t o = (size_t)r * t + m;
   if (round_status[r] != DG_ST_OK_) {
-    store_g2j(terms[g], jac_infinity<Fp2>());
+    store_g2j(terms[o], jac_infinity<Fp2>());
     return;
   }
   Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, m);
-  store_g2j(terms[g], g2_mul_u256_psi(load_g2a(S[(size_t)r * k + sel[g]]), lam.l));
+  store_g2j(terms[o], g2_mul_u256_psi(load_g2a(S[(size_t)r * k + sel[o]]), lam.l));
 }
 #endif
 

@@ -193,12 +193,14 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_slices(uint32_t nside
 }
 
 // one 128-lane workgroup per (side, window): W_w = sum_k 2^k S_{w,k} (Horner with cooperative doublings
-// and additions, coop.h), then 2^(8w) W_w (alpha windows; test windows stay unshifted, side 1 has none)
-DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_horner_coop(uint32_t nwin, const G2JStore* S, G2JStore* Wout) {
+// and additions, coop.h), then 2^(8w) W_w (alpha windows; test windows stay unshifted and exist only on
+// the first `tsides` sides)
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_horner_coop(uint32_t nwin, uint32_t tsides, const G2JStore* S,
+                                                                       G2JStore* Wout) {
   __shared__ CoG2Tmp tmp;
   __shared__ CoG2 acc, nxt;
   const uint32_t sw = blockIdx.x, w = sw % nwin;
-  if (sw >= nwin && w >= MSM_WIN) return;
+  if (sw / nwin >= tsides && w >= MSM_WIN) return;
   const G2JStore* Sw = S + sw * MSM_C;
   CO_SERIAL({
     G2J a = load_g2j(Sw[MSM_C - 1]);
@@ -235,7 +237,8 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_final_coop(uint32_t n
   CO_SERIAL(store_g2j(out[side], G2J{acc.x, acc.y, acc.z}));
 }
 
-// batched subgroup check: one 128-lane workgroup per side-0 window sum W[w] tests psi(P) == [z]P
+// batched subgroup check: one 128-lane workgroup per window sum W[w] (the first side's, or every key
+// set's in the keyed MSM) tests psi(P) == [z]P
 // cooperatively (coop.h); any failure clears flag[0] (the batch verdict written by k_final_coop), so the
 // per-item pass runs
 DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_subgroup(const G2JStore* W, uint32_t* flag) {
@@ -267,15 +270,15 @@ constexpr uint32_t KSCAN_B = 1024;  // keys per scan block
 
 DGI uint32_t kmsm_key(uint32_t w, uint32_t d, uint32_t set, uint32_t nsets) { return (w * MSM_NB + d) * nsets + set; }
 
-DG_KERNEL void __launch_bounds__(256) k_kmsm_count(uint32_t N, uint32_t k, uint32_t nsets, uint64_t seed,
+DG_KERNEL void __launch_bounds__(256) k_kmsm_count(uint32_t N, uint32_t k, uint32_t nsets, uint32_t nwin, uint64_t seed,
                                                    const uint32_t* item_slot, const uint8_t* status,
                                                    const uint8_t* isolate, uint32_t* count) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N || status[i] != DG_ST_OK_ || isolate[i]) return;
-  uint64_t a = rlc_alpha(seed, i / k);
+  const MsmDigits dg(seed, i / k, nwin);
   uint32_t s = item_slot[i];
-  for (uint32_t w = 0; w < MSM_WIN; ++w) {
-    uint32_t d = (uint32_t)(a >> (MSM_C * w)) & (MSM_NB - 1);
+  for (uint32_t w = 0; w < nwin; ++w) {
+    uint32_t d = dg(w);
     if (d) atomicAdd(&count[kmsm_key(w, d, s, nsets)], 1u);
   }
 }
@@ -338,15 +341,15 @@ DG_KERNEL void __launch_bounds__(256) k_kscan_add(uint32_t nkeys, const uint32_t
   chunk_off[i] += tot[nblocks + b];
 }
 
-DG_KERNEL void __launch_bounds__(256) k_kmsm_scatter(uint32_t N, uint32_t k, uint32_t nsets, uint64_t seed,
+DG_KERNEL void __launch_bounds__(256) k_kmsm_scatter(uint32_t N, uint32_t k, uint32_t nsets, uint32_t nwin, uint64_t seed,
                                                      const uint32_t* item_slot, const uint8_t* status,
                                                      const uint8_t* isolate, uint32_t* cursor, uint32_t* list) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N || status[i] != DG_ST_OK_ || isolate[i]) return;
-  uint64_t a = rlc_alpha(seed, i / k);
+  const MsmDigits dg(seed, i / k, nwin);
   uint32_t s = item_slot[i];
-  for (uint32_t w = 0; w < MSM_WIN; ++w) {
-    uint32_t d = (uint32_t)(a >> (MSM_C * w)) & (MSM_NB - 1);
+  for (uint32_t w = 0; w < nwin; ++w) {
+    uint32_t d = dg(w);
     if (d) list[atomicAdd(&cursor[kmsm_key(w, d, s, nsets)], 1u)] = i;
   }
 }
@@ -388,10 +391,11 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_buckets(uint32_t nke
 }
 
 // lane (set, w, k, c < 16): 8 of the buckets of (set, w) whose digit has bit k set; rows (set, w, k)
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_slices(uint32_t nsets, const G2JStore* B, G2JStore* P1) {
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_slices(uint32_t nsets, uint32_t nwin, const G2JStore* B,
+                                                                   G2JStore* P1) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nsets * MSM_WIN * MSM_C * 16) return;
-  uint32_t c = g % 16, k = (g / 16) % MSM_C, w = (g / (16 * MSM_C)) % MSM_WIN, set = g / (16 * MSM_C * MSM_WIN);
+  if (g >= nsets * nwin * MSM_C * 16) return;
+  uint32_t c = g % 16, k = (g / 16) % MSM_C, w = (g / (16 * MSM_C)) % nwin, set = g / (16 * MSM_C * nwin);
   G2J acc = jac_infinity<Fp2>();
   for (uint32_t i = 8 * c; i < 8 * c + 8; ++i) {
     uint32_t d = ((i >> k) << (k + 1)) | (1u << k) | (i & ((1u << k) - 1));
@@ -400,11 +404,25 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_slices(uint32_t nset
   store_g2j(P1[g], acc);
 }
 
-// lane s: beta_s T_s
-DG_KERNEL void __launch_bounds__(64) k_kmsm_beta(uint32_t nsets, uint64_t seed, const G2JStore* Tset, G2JStore* out) {
-  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nsets) return;
-  store_g2j(out[s], jac_mul_u64(load_g2j(Tset[s]), rlc_beta(seed, s)));
+// one 128-lane workgroup per set s: beta_s T_s by cooperative double-and-add (coop.h; beta is odd, so
+// non-zero)
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_kmsm_beta(uint64_t seed, const G2JStore* Tset, G2JStore* out) {
+  __shared__ CoG2Tmp tmp;
+  __shared__ CoG2 acc, p;
+  const uint32_t s = blockIdx.x;
+  const uint64_t beta = rlc_beta(seed, s);
+  CO_SERIAL({
+    G2J a = load_g2j(Tset[s]);
+    p = CoG2{a.x, a.y, a.z};
+    acc = p;
+  });
+  int top = 63;
+  while (!((beta >> top) & 1)) --top;
+  for (int b = top - 1; b >= 0; --b) {
+    co_g2_dbl(&acc, &tmp);
+    if ((beta >> b) & 1) co_g2_add(&acc, &acc, &p, &tmp);
+  }
+  CO_SERIAL(store_g2j(out[s], G2J{acc.x, acc.y, acc.z}));
 }
 
 #endif
