@@ -123,6 +123,26 @@ def recover_bench(L, tbls, chain_sigs, first_round, R, t, n, steps):
                     "recovered signatures equal the chain's" % (R * n * 98 // 10**6)}
 
 
+def sync_bench(chain_sigs, R, batch=25000):
+    """syncFrom catch-up (drand_amd/bulk.sync_from) of R linked chain rounds from the
+    genesis seed, as Beacon objects streamed by one peer, `batch` rounds per GPU call (links + one RLC
+    multi-pairing per batch); host objects, PCIe and the per-batch blocking calls inside the timed
+    region.  Every round must be stored."""
+    from drand_amd import bulk
+
+    pk = S.GROUP_PK
+    bs = [bulk.Beacon(r - 1, S.GENESIS_SEED if r == 1 else bytes(chain_sigs[r - 2]), r, bytes(chain_sigs[r - 1]))
+          for r in range(1, R + 1)]
+    got = []
+    t0 = time.perf_counter()
+    res = bulk.sync_from(pk, 0, S.GENESIS_SEED, [bs], put=got.append, batch=batch)
+    dt = time.perf_counter() - t0
+    assert res.stored == R and got[-1].round == R, "sync_from did not store the whole chain"
+    return {"metric": "syncFrom catch-up rounds/s (bulk.sync_from, beacon/beacon.go:529-607)", "value": R / dt,
+            "unit": "rounds/s", "rounds": R, "batch": batch, "s": dt,
+            "note": "host Beacon objects -> dg_check_links + dg_verify_beacons per batch (host-buffer API, blocking)"}
+
+
 def adversarial_bench(L, tbls, chain_sigs, R, t=129, n=256, frac=0.10, n_short=3):
     """BASELINE configs C5: n = 256, t = 129, R rounds, ~10% of the (round, share) cells
     corrupted with the six cycling modes of tools/corrupt.py, plus `n_short` rounds with more than n - t
@@ -191,6 +211,7 @@ def main():
                     help="no per-kernel HIP events in the timed region (no roofline)")
     ap.add_argument("--recover-rounds", type=int, default=20000, help="0 disables the Recover line")
     ap.add_argument("--c5-rounds", type=int, default=10000, help="0 disables the adversarial (C5) line")
+    ap.add_argument("--sync-rounds", type=int, default=100000, help="0 disables the syncFrom catch-up line")
     args = ap.parse_args()
 
     import torch
@@ -354,6 +375,9 @@ def main():
         adv = None
         if args.c5_rounds and chain is not None:
             adv = adversarial_bench(L, tbls, chain, min(args.c5_rounds, len(chain) - 1))
+        syn = None
+        if args.sync_rounds and chain is not None:
+            syn = sync_bench(chain, min(args.sync_rounds, len(chain)))
         cpu = None
         if not args.no_cpu_baseline:
             ns = min(n, 40000)  # the sampler stops at ~10 s of 16-thread CPU work
@@ -365,7 +389,7 @@ def main():
                "config": {"workload": "batch bls.Verify / beacon.VerifyBeacon of %d linked chain rounds per GPU, one "
                                       "shared group key (BASELINE configs[1]; configs[3] at N>1)" % n,
                           "rounds_per_gpu": n, "global_rounds": world * n, "parallelism": "rounds sharded dp%d" % world},
-               "roofline": roof, "cpu_baseline": cpu, "recover": rec, "adversarial": adv,
+               "roofline": roof, "cpu_baseline": cpu, "recover": rec, "adversarial": adv, "sync": syn,
                "batch_fallbacks": fallbacks,
                "kernel_time_share": share,
                "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},

@@ -17,3 +17,4 @@ for k in ("recover", "adversarial"):
     x = d.get(k) or {}
     print(k, x.get("value"), x.get("s_per_step"))
 PY
+python -c "import json; d=json.loads(open('gpurun_out/bench.json').read().strip().splitlines()[-1]); print('sync', d.get('sync'))"
