@@ -215,6 +215,51 @@ DGI Fp fp_small(uint32_t v) {
   return fp_to_mont(a);
 }
 
+// The digit-form chain is used in the hot translation unit only (hash-to-G2 -8%, decode -13% per launch):
+// built into the library TU as well, the overlapped batches ran 3-5x slower on MI355X although every
+// kernel was as fast or faster alone (measured, cause not isolated), so the library keeps the per-step
+// form below.
+#if DG_TU_HOT
+// x^e for a fixed exponent given as a width-3 sliding-window schedule (tools/gen_constants.py).
+// The schedule is wave-uniform (scalar loads); the odd-power table is selected with v_cndmask.  The chain
+// runs in the radix-2^28 digit form (fp28.h): one unpack of the table, one pack and one conditional
+// subtraction at the end instead of per step.
+template <int NSTEPS>
+DGI Fp fp_pow_sched(const Fp& x, int first, const int8_t (&steps)[NSTEPS][2]) {
+  Fp x2 = fp_sqr(x);
+  Fp t1f = fp_mul(x, x2);
+  Fp t2f = fp_mul(t1f, x2);
+  Fp t3f = fp_mul(t2f, x2);
+  uint32_t t0[14], t1[14], t2[14], t3[14], acc[14], nxt[14], m[14];
+  fp28_unpack(x.l, t0);
+  fp28_unpack(t1f.l, t1);
+  fp28_unpack(t2f.l, t2);
+  fp28_unpack(t3f.l, t3);
+#pragma unroll
+  for (int d = 0; d < 14; ++d) acc[d] = first == 0 ? t0[d] : first == 1 ? t1[d] : first == 2 ? t2[d] : t3[d];
+  for (int s = 0; s < NSTEPS; ++s) {
+    int k = steps[s][0];
+    int idx = steps[s][1];
+    for (int j = 0; j < k; ++j) {
+      DG_COUNT_SQR();
+      fp28_mont_sqr_d(acc, nxt);
+#pragma unroll
+      for (int d = 0; d < 14; ++d) acc[d] = nxt[d];
+    }
+    if (idx >= 0) {
+#pragma unroll
+      for (int d = 0; d < 14; ++d) m[d] = idx == 0 ? t0[d] : idx == 1 ? t1[d] : idx == 2 ? t2[d] : t3[d];
+      DG_COUNT_MUL();
+      fp28_mont_mul_d(acc, m, nxt);
+#pragma unroll
+      for (int d = 0; d < 14; ++d) acc[d] = nxt[d];
+    }
+  }
+  Fp r;
+  fp28_pack(acc, r.l);
+  return fp_reduce_once(r);
+}
+#else
 // x^e for a fixed exponent given as a width-3 sliding-window schedule (tools/gen_constants.py).
 // The schedule is wave-uniform (scalar loads); the odd-power table is selected with v_cndmask.
 template <int NSTEPS>
@@ -238,6 +283,7 @@ DGI Fp fp_pow_sched(const Fp& x, int first, const int8_t (&steps)[NSTEPS][2]) {
   }
   return acc;
 }
+#endif
 // a^(p-2): Fermat inversion (~455 multiplications); kept as the cross-check of fp_inv
 DGH Fp fp_inv_fermat(const Fp& a) { return fp_pow_sched(a, EXP_PM2_FIRST, EXP_PM2_STEPS); }
 

@@ -55,11 +55,13 @@ DGI void fp28_mont_tail(uint64_t& acc, int k, uint32_t (&m)[14], uint32_t (&r)[1
   acc >>= 28;
 }
 
-// r = a b / 2^392 mod p, r < 2p (a, b < p)
-DGI void fp28_mont_mul(const uint32_t (&a)[12], const uint32_t (&b)[12], uint32_t (&out)[12]) {
-  uint32_t x[14], y[14], m[14], r[14];
-  fp28_unpack(a, x);
-  fp28_unpack(b, y);
+// Digit form: 14 digits, digits 0..12 below 2^28, the top one below 2^20 (values < 2^384).  The
+// products below take and return digit form, so an exponentiation chain stays in it between steps (no
+// unpack / pack, no conditional subtraction: inputs < 2p give an output < 2p because 4p < R).
+
+// r = x y / 2^392 mod p in digit form, r < 2p (x, y < 2p)
+DGI void fp28_mont_mul_d(const uint32_t (&x)[14], const uint32_t (&y)[14], uint32_t (&r)[14]) {
+  uint32_t m[14];
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 27; ++k) {
@@ -71,13 +73,11 @@ DGI void fp28_mont_mul(const uint32_t (&a)[12], const uint32_t (&b)[12], uint32_
     fp28_mont_tail(acc, k, m, r);
   }
   r[13] = (uint32_t)acc;
-  fp28_pack(r, out);
 }
 
-// r = a^2 / 2^392 mod p: the off-diagonal products once, doubled per column
-DGI void fp28_mont_sqr(const uint32_t (&a)[12], uint32_t (&out)[12]) {
-  uint32_t x[14], m[14], r[14];
-  fp28_unpack(a, x);
+// r = x^2 / 2^392 mod p in digit form: the off-diagonal products once, doubled per column
+DGI void fp28_mont_sqr_d(const uint32_t (&x)[14], uint32_t (&r)[14]) {
+  uint32_t m[14];
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 27; ++k) {
@@ -92,6 +92,22 @@ DGI void fp28_mont_sqr(const uint32_t (&a)[12], uint32_t (&out)[12]) {
     fp28_mont_tail(acc, k, m, r);
   }
   r[13] = (uint32_t)acc;
+}
+
+// r = a b / 2^392 mod p, r < 2p (a, b < p)
+DGI void fp28_mont_mul(const uint32_t (&a)[12], const uint32_t (&b)[12], uint32_t (&out)[12]) {
+  uint32_t x[14], y[14], r[14];
+  fp28_unpack(a, x);
+  fp28_unpack(b, y);
+  fp28_mont_mul_d(x, y, r);
+  fp28_pack(r, out);
+}
+
+// r = a^2 / 2^392 mod p
+DGI void fp28_mont_sqr(const uint32_t (&a)[12], uint32_t (&out)[12]) {
+  uint32_t x[14], r[14];
+  fp28_unpack(a, x);
+  fp28_mont_sqr_d(x, r);
   fp28_pack(r, out);
 }
 
