@@ -550,8 +550,9 @@ DG_KERNEL void __launch_bounds__(128) k_recover_select(uint32_t R, uint32_t k, u
 // selected indices).  A wave covers 64 rounds of the same position m, so while the rounds select the same
 // index set (every round with no bad share among its first t) its lanes share lambda_m and the scalar
 // multiplication's digit-dependent branches are uniform across the wave.
-#if !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(64) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
+// hot translation unit (kernels_hot.hip: flat, 2 waves/SIMD; measured -27% / -36%)
+#if DG_TU_HOT
+DG_KERNEL void __launch_bounds__(64, DG_HOT_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
                                                      const uint32_t* selidx, const uint8_t* round_status,
                                                      const G2AStore* S, G2JStore* terms) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -565,6 +566,10 @@ DG_KERNEL void __launch_bounds__(64) k_recover_terms(uint32_t R, uint32_t k, uin
   Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, m);
   store_g2j(terms[o], g2_mul_u256_psi(load_g2a(S[(size_t)r * k + sel[o]]), lam.l));
 }
+#else
+DG_KERNEL void __launch_bounds__(64, DG_HOT_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
+                                                     const uint32_t* selidx, const uint8_t* round_status,
+                                                     const G2AStore* S, G2JStore* terms);
 #endif
 
 // compress points (zeros where status != OK)

@@ -34,6 +34,8 @@ namespace dg {
 constexpr uint32_t MSM_C = 8, MSM_WIN = 8, MSM_NB = 256, MSM_NBK = MSM_WIN * MSM_NB;  // 2048 bucket slots
 constexpr uint32_t MSM_TWIN = 10, MSM_WT = MSM_WIN + MSM_TWIN;  // test windows of the batched subgroup check
 constexpr uint32_t MSM_NBT = MSM_WT * MSM_NB;                   // 4608 bucket slots with the test windows
+// keyed MSM bucket key: (window, digit, key set), the set fastest
+DGI uint32_t kmsm_key(uint32_t w, uint32_t d, uint32_t set, uint32_t nsets) { return (w * MSM_NB + d) * nsets + set; }
 constexpr uint32_t MSM_CHUNK = 8;   // points per first-level lane
 constexpr uint32_t MSM_BSPLIT = 8;  // lanes per bucket at the second level
 
@@ -268,7 +270,6 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_subgroup(const G2JSto
 //   k_kmsm_beta                                 beta_s T_s, then a row sum
 constexpr uint32_t KSCAN_B = 1024;  // keys per scan block
 
-DGI uint32_t kmsm_key(uint32_t w, uint32_t d, uint32_t set, uint32_t nsets) { return (w * MSM_NB + d) * nsets + set; }
 
 DG_KERNEL void __launch_bounds__(256) k_kmsm_count(uint32_t N, uint32_t k, uint32_t nsets, uint32_t nwin, uint64_t seed,
                                                    const uint32_t* item_slot, const uint8_t* status,
@@ -355,7 +356,10 @@ DG_KERNEL void __launch_bounds__(256) k_kmsm_scatter(uint32_t N, uint32_t k, uin
 }
 
 // lane c: the c-th chunk (<= MSM_CHUNK affine points of one bucket)
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_chunks(uint32_t max_chunks, uint32_t nkeys,
+#endif
+// hot translation unit (kernels_hot.hip: flat, 2 waves/SIMD; measured -27% / -36%)
+#if defined(__HIP__) && DG_TU_HOT
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_kmsm_chunks(uint32_t max_chunks, uint32_t nkeys,
                                                                    const uint32_t* count, const uint32_t* offset,
                                                                    const uint32_t* chunk_off, const uint32_t* list,
                                                                    const G2AStore* S, G2JStore* out) {
@@ -379,6 +383,13 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_chunks(uint32_t max_
   }
   store_g2j(out[c], acc);
 }
+#elif defined(__HIP__)
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_kmsm_chunks(uint32_t max_chunks, uint32_t nkeys,
+                                                                   const uint32_t* count, const uint32_t* offset,
+                                                                   const uint32_t* chunk_off, const uint32_t* list,
+                                                                   const G2AStore* S, G2JStore* out);
+#endif
+#if defined(__HIP__) && !DG_TU_HOT
 
 // lane = bucket key: sum of its chunks (identity when empty)
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_buckets(uint32_t nkeys, const uint32_t* chunk_off,
