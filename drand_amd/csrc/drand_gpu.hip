@@ -88,7 +88,7 @@ int fail(int code, const std::string& msg) {
 
 // workspace slots
 enum Slot {
-  S_MSGS, S_DST, S_Q, S_S, S_U, S_STATUS, S_ISO, S_CELL, S_W, S_A, S_TMP, S_KP, S_F, S_H, S_FLAG, S_KEYS, S_KEYST, S_XC,
+  S_MSGS, S_DST, S_Q, S_S, S_U, S_STATUS, S_ISO, S_CELL, S_W, S_A, S_TMP, S_KP, S_F, S_H, S_FLAG, S_KEYS, S_KEYST, S_XC, S_FIN, S_LIST,
   S_COMMITS, S_COMMITST, S_SLOTIDX, S_ITEMSLOT, S_SEL, S_SELIDX, S_RST, S_SST, S_TERMS, S_IN0, S_IN1, S_IN2, S_IN3,
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
@@ -248,6 +248,7 @@ struct Batch {
   uint32_t stride, offset;
   G2AStore* S;
   uint8_t* status;
+  uint32_t prefix_t = 0;  // Recover: after a failed batch, check items only up to each round's t-th valid one
 };
 
 // Pippenger MSM (msm.h): out[0] = sum_r alpha_r PA_r, out[1] = sum_r alpha_r PB_r (PB may be null),
@@ -405,8 +406,28 @@ int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
   G2AStore* H;
   RET(wsT(S_H, b.R, &H));
   RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, (const uint32_t*)flag, b.Q, H));
-  RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
-             (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status, batched_sub));
+  if (b.prefix_t == 0) {
+    RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
+               (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status, batched_sub));
+  } else {
+    // Recover: per-item checks over the examined prefix only, in passes that grow it by each round's deficit;
+    // the last pass takes every unverified item before the t-th valid one, so the statuses Recover reads
+    // are exact.  A passed batch marks nothing (only isolated items can be pending).
+    uint8_t* fin;
+    uint32_t* list;
+    RET(wsT(S_FIN, N, &fin));
+    RET(wsT(S_LIST, (size_t)N + 1, &list));
+    RET(launch("k_prefix_init", k_prefix_init, N, 256, st, N, (const uint32_t*)flag, (const uint8_t*)iso,
+               (const uint8_t*)b.status, fin));
+    constexpr int kPasses = 4;
+    for (int pass = 0; pass <= kPasses; ++pass) {
+      HIPCHK(hipMemsetAsync(list, 0, 4, st));
+      RET(launch("k_prefix_mark", k_prefix_mark, b.R, 128, st, b.R, b.k, b.prefix_t, pass == kPasses ? 1u : 0u,
+                 (const uint8_t*)b.status, (const uint8_t*)fin, list));
+      RET(launch("k_verify_list", k_verify_list, N, 64, st, b.k, (const uint32_t*)list, b.keys, b.item_slot,
+                 (const G2AStore*)H, (const G2AStore*)b.S, b.status, fin, batched_sub));
+    }
+  }
   RET(launch("k_count_fallback", k_count_fallback, 1, 64, st, (const uint32_t*)flag, g_ctx.fallbacks));
   return 0;
 }
@@ -512,7 +533,7 @@ int poly_keys(const uint8_t* commits48, uint32_t t, const std::vector<uint32_t>&
 // VerifyPartial over R rounds x k partials: keys X_i = PubPoly.Eval(i) for every distinct index
 int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const uint8_t* msgs, uint32_t msg_len,
                         uint32_t k, const uint8_t* partials98, uint64_t seed, hipStream_t st, uint8_t** d_status,
-                        uint8_t** d_partials, G2AStore** d_S) {
+                        uint8_t** d_partials, G2AStore** d_S, uint32_t prefix_t = 0) {
   const size_t N = (size_t)R * k;
   // distinct indices (host bookkeeping over the 2-byte index fields only)
   std::vector<int32_t> slot_of(65536, -1);
@@ -538,6 +559,7 @@ int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const 
   RET(wsT(S_S, N, d_S));
   RET(wsT(S_STATUS, N, d_status));
   Batch b{R, k, nslots, Q, keys, kst, d_itemslot, d_p, 98, 2, *d_S, *d_status};
+  b.prefix_t = prefix_t;
   RET(batch_verify(b, seed, st));
   *d_partials = d_p;
   return 0;
@@ -953,7 +975,7 @@ int dg_recover(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t ro
   uint8_t *d_st, *d_p, *d_rst, *d_sst, *d_out;
   G2AStore* d_S;
   RET(verify_partials_dev(commits48, t, R, msgs, (uint32_t)msg_len, k, partials98, fresh_seed(seed), st, &d_st, &d_p,
-                          &d_S));
+                          &d_S, t));
   uint32_t *d_sel, *d_selidx;
   G2JStore *terms, *tmp;
   RET(wsT(S_SEL, (size_t)R * t, &d_sel));

@@ -451,18 +451,12 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_clear_rounds(uint32_t R, 
 }
 #endif
 
-// individual bls.Verify of item i: e(X_slot, H_{i/k}) == e(g1, S_i): every decoded item after a failed
-// batch (flag[0] == 0), only the isolated ones after a passed batch; with `subgroup` the decode skipped
+// individual bls.Verify of item i: e(X_slot, H_{i/k}) == e(g1, S_i); with `subgroup` the decode skipped
 // the per-item G2 subgroup check (batched on the MSM windows), so it is done here: a sigma outside G2
 // is a decode error, as in g2_decompress
 #if !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
-                                                    const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
-                                                    const uint8_t* isolate, uint8_t* status, uint32_t subgroup) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (status[i] != DG_ST_OK_) return;
-  if (flag[0] && !isolate[i]) return;
+DGN void verify_item(size_t i, uint32_t k, const G1AStore* keys, const uint32_t* item_slot, const G2AStore* H,
+                     const G2AStore* S, uint8_t* status, uint32_t subgroup) {
   G1A key = load_g1a(keys[item_slot ? item_slot[i] : 0u]);
   G2A h = load_g2a(H[i / k]);
   G2A s = load_g2a(S[i]);
@@ -485,6 +479,57 @@ DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, cons
   }
   bool good = np == 0 ? true : fp12_is_one(final_exp_cubed(miller_loop<2>(P, Qa, np)));
   status[i] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
+}
+
+// every decoded item after a failed batch (flag[0] == 0), only the isolated ones after a passed batch
+DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
+                                                    const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
+                                                    const uint8_t* isolate, uint8_t* status, uint32_t subgroup) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (status[i] != DG_ST_OK_) return;
+  if (flag[0] && !isolate[i]) return;
+  verify_item(i, k, keys, item_slot, H, S, status, subgroup);
+}
+
+// ---- Recover's per-item pass over the examined prefix only.  Recover (kyber tbls.Recover) checks the
+// partials of a round in input order and stops at the t-th valid one, so after a failed batch only the
+// items up to that point need their own pairing check: about t / (1 - corrupted fraction) of the k.
+// fin[i] = the verdict of item i is final (decode failure, or a passed batch and not isolated).
+DG_KERNEL void __launch_bounds__(256) k_prefix_init(uint32_t n, const uint32_t* flag, const uint8_t* isolate,
+                                                   const uint8_t* status, uint8_t* fin) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fin[i] = (status[i] != DG_ST_OK_ || (flag[0] && !isolate[i])) ? 1 : 0;
+}
+// per round: scanning in input order, the unverified items that could be among the first t valid ones if
+// every unverified item were valid (`all`: every unverified item before the t-th verified valid one) are
+// appended to list[1 + ...] (list[0] = count)
+DG_KERNEL void __launch_bounds__(128) k_prefix_mark(uint32_t R, uint32_t k, uint32_t t, uint32_t all,
+                                                   const uint8_t* status, const uint8_t* fin, uint32_t* list) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  uint32_t valid = 0, pending = 0;
+  for (uint32_t j = 0; j < k; ++j) {
+    size_t i = (size_t)r * k + j;
+    if (valid >= t || (!all && valid + pending >= t)) break;
+    if (fin[i]) {
+      if (status[i] == DG_ST_OK_) ++valid;
+    } else {
+      ++pending;
+      list[1 + atomicAdd(&list[0], 1u)] = (uint32_t)i;
+    }
+  }
+}
+// lane g < list[0]: the per-item check of item list[1 + g]
+DG_KERNEL void __launch_bounds__(64) k_verify_list(uint32_t k, const uint32_t* list, const G1AStore* keys,
+                                                   const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
+                                                   uint8_t* status, uint8_t* fin, uint32_t subgroup) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= list[0]) return;
+  uint32_t i = list[1 + g];
+  verify_item(i, k, keys, item_slot, H, S, status, subgroup);
+  fin[i] = 1;
 }
 #endif
 
