@@ -590,6 +590,21 @@ int dg_init(int device) {
     HIPCHK(hipMalloc(&g_ctx.fallbacks, sizeof(unsigned long long)));
     HIPCHK(hipMemset(g_ctx.fallbacks, 0, sizeof(unsigned long long)));
   }
+  // A hardware queue's scratch (private segment) grows on the first dispatch that needs more.  On MI355X
+  // that growth, when it first happened inside an overlapped batch (the per-item kernels: ~14 KB per
+  // lane), stalled every queue for ~0.5 s (rocprofv3 trace).  Dispatch the largest-scratch kernels once per
+  // workspace stream here, with zero items (every lane returns at once), so the growth happens now.
+  for (Set& x : g_ctx.sets) {
+    hipLaunchKernelGGL(k_verify_items, dim3(1), dim3(64), 0, x.stream, 0u, 1u, (const uint32_t*)nullptr,
+                       (const G1AStore*)nullptr, (const uint32_t*)nullptr, (const G2AStore*)nullptr,
+                       (const G2AStore*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, 0u);
+    // list[0] = 0 (the zeroed fallback counter): no items
+    hipLaunchKernelGGL(k_verify_list, dim3(1), dim3(64), 0, x.stream, 1u, (const uint32_t*)g_ctx.fallbacks,
+                       (const G1AStore*)nullptr, (const uint32_t*)nullptr, (const G2AStore*)nullptr,
+                       (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr, 0u);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipDeviceSynchronize());
   g_ctx.device = device;
   g_ctx.ready = true;
   return 0;
