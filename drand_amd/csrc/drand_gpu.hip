@@ -277,9 +277,11 @@ int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA
              (const uint32_t*)offset, (const uint32_t*)chunk_off, (const uint32_t*)list, PA, PB, chunks));
   RET(launch("k_msm_buckets", k_msm_buckets, nbk * MSM_BSPLIT * nsides, 128, st, max_chunks, nsides, nbk,
              (const uint32_t*)chunk_off, (const G2JStore*)chunks, BP));
-  RET(reduce_rows(BP, tmp, nbk * nsides, MSM_BSPLIT, st));  // B[side][b] = BP[side * nbk + b]
+  // pairwise levels (one dependent addition per lane per launch): these launches run on a nearly empty chip,
+  // so their time is the depth of the addition chain, not the number of additions
+  RET(reduce_rows(BP, tmp, nbk * nsides, MSM_BSPLIT, st, 2));  // B[side][b] = BP[side * nbk + b]
   RET(launch("k_msm_slices", k_msm_slices, nsides * nwin * MSM_C * 16, 128, st, nsides, nwin, (const G2JStore*)BP, P1));
-  RET(reduce_rows(P1, tmp, nsides * nwin * MSM_C, 16, st, 4));  // S[side][w][k] = P1[...]
+  RET(reduce_rows(P1, tmp, nsides * nwin * MSM_C, 16, st, 2));  // S[side][w][k] = P1[...]
   RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * nwin * nsides, 128, st, nwin, 1u, (const G2JStore*)P1, W));
   RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsides, 128, st, nwin, (const G2JStore*)W, *out));
   if (win) *win = W;
