@@ -266,7 +266,7 @@ int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA
   RET(wsT(S_MSM_CHUNKS, (size_t)max_chunks * nsides, &chunks));
   RET(wsT(S_MSM_B, (size_t)nbk * MSM_BSPLIT * nsides, &BP));
   RET(wsT(S_MSM_G, (size_t)nbk * MSM_BSPLIT * nsides, &tmp));
-  RET(wsT(S_MSM_P1, (size_t)nwin * MSM_C * 16 * nsides, &P1));
+  RET(wsT(S_MSM_P1, (size_t)nwin * MSM_C * MSM_SLICE_LANES * nsides, &P1));
   RET(wsT(S_MSM_W, (size_t)nwin * nsides, &W));
   RET(wsT(S_MSM_OUT, 2, out));
   HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * nbk, st));
@@ -280,8 +280,8 @@ int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA
   // pairwise levels (one dependent addition per lane per launch): these launches run on a nearly empty chip,
   // so their time is the depth of the addition chain, not the number of additions
   RET(reduce_rows(BP, tmp, nbk * nsides, MSM_BSPLIT, st, 2));  // B[side][b] = BP[side * nbk + b]
-  RET(launch("k_msm_slices", k_msm_slices, nsides * nwin * MSM_C * 16, 128, st, nsides, nwin, (const G2JStore*)BP, P1));
-  RET(reduce_rows(P1, tmp, nsides * nwin * MSM_C, 16, st, 2));  // S[side][w][k] = P1[...]
+  RET(launch("k_msm_slices", k_msm_slices, nsides * nwin * MSM_C * MSM_SLICE_LANES, 128, st, nsides, nwin, (const G2JStore*)BP, P1));
+  RET(reduce_rows(P1, tmp, nsides * nwin * MSM_C, MSM_SLICE_LANES, st, 2));  // S[side][w][k] = P1[...]
   RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * nwin * nsides, 128, st, nwin, 1u, (const G2JStore*)P1, W));
   RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsides, 128, st, nwin, (const G2JStore*)W, *out));
   if (win) *win = W;

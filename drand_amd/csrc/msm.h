@@ -38,6 +38,7 @@ constexpr uint32_t MSM_NBT = MSM_WT * MSM_NB;                   // 4608 bucket s
 DGI uint32_t kmsm_key(uint32_t w, uint32_t d, uint32_t set, uint32_t nsets) { return (w * MSM_NB + d) * nsets + set; }
 constexpr uint32_t MSM_CHUNK = 8;   // points per first-level lane
 constexpr uint32_t MSM_BSPLIT = 8;  // lanes per bucket at the second level
+constexpr uint32_t MSM_SLICE_LANES = 64;  // lanes per (side, window, bit slice) in k_msm_slices
 
 #if defined(__HIP__) && !DG_TU_HOT
 // digits of round r in windows 0..nwin-1: the bytes of alpha_r, then (nwin > MSM_WIN) the first
@@ -178,15 +179,17 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_buckets(uint32_t max_
 }
 
 // Bucket aggregation by bit slices: sum_b b B_b = sum_k 2^k S_k with S_k = sum of the buckets whose
-// digit b has bit k set (128 of the 255).  Level 1: lane (side, w, k, c < 16) sums 8 of those buckets.
+// digit b has bit k set (128 of the 255).  Level 1: lane (side, w, k, c < MSM_SLICE_LANES) sums 2 of those
+// buckets; the pairwise row sums that follow keep the dependent-addition depth at 1 + log2(lanes).
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_slices(uint32_t nsides, uint32_t nwin, const G2JStore* B,
                                                                   G2JStore* P1) {
+  constexpr uint32_t L = MSM_SLICE_LANES, PER = 128 / MSM_SLICE_LANES;
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nsides * nwin * MSM_C * 16) return;
-  uint32_t c = g % 16, k = (g / 16) % MSM_C, w = (g / (16 * MSM_C)) % nwin, side = g / (16 * MSM_C * nwin);
+  if (g >= nsides * nwin * MSM_C * L) return;
+  uint32_t c = g % L, k = (g / L) % MSM_C, w = (g / (L * MSM_C)) % nwin, side = g / (L * MSM_C * nwin);
   const G2JStore* Bw = B + (side * nwin + w) * MSM_NB;
   G2J acc = jac_infinity<Fp2>();
-  for (uint32_t i = 8 * c; i < (side && w >= MSM_WIN ? 0 : 8 * c + 8); ++i) {
+  for (uint32_t i = PER * c; i < (side && w >= MSM_WIN ? 0 : PER * c + PER); ++i) {
     // i-th digit in 0..255 with bit k set: insert a 1 at bit k of i
     uint32_t b = ((i >> k) << (k + 1)) | (1u << k) | (i & ((1u << k) - 1));
     acc = jac_add(acc, load_g2j(Bw[b]));
