@@ -9,7 +9,7 @@
 //                     sums are exact group elements, so the result does not depend on it)
 //   4. k_msm_chunks       each lane sums one chunk of <= MSM_CHUNK points of one bucket (mixed additions
 //                         for Z = 1 inputs)
-//   5. k_msm_buckets      MSM_BSPLIT lanes per bucket sum its chunks strided; k_sum_rows folds the partials
+//   5. k_msm_buckets      MSM_BSPLIT (32) lanes per bucket sum its chunks strided; pairwise k_sum_rows fold them
 //   6. k_msm_slices       bucket aggregation by bit slices: sum_b b B_b = sum_k 2^k S_k, S_k = sum of the
 //                         buckets whose digit has bit k set (16 lanes per (window, k), then k_sum_rows)
 //   7. k_msm_horner_coop  per window, cooperatively (coop.h): W_w = sum_k 2^k S_k, times 2^(8w)
@@ -37,7 +37,7 @@ constexpr uint32_t MSM_NBT = MSM_WT * MSM_NB;                   // 4608 bucket s
 // keyed MSM bucket key: (window, digit, key set), the set fastest
 DGI uint32_t kmsm_key(uint32_t w, uint32_t d, uint32_t set, uint32_t nsets) { return (w * MSM_NB + d) * nsets + set; }
 constexpr uint32_t MSM_CHUNK = 8;   // points per first-level lane
-constexpr uint32_t MSM_BSPLIT = 8;  // lanes per bucket at the second level
+constexpr uint32_t MSM_BSPLIT = 32;  // lanes per bucket at the second level
 constexpr uint32_t MSM_SLICE_LANES = 64;  // lanes per (side, window, bit slice) in k_msm_slices
 
 #if defined(__HIP__) && !DG_TU_HOT
