@@ -221,7 +221,9 @@ int wsT(Slot s, size_t count, T** out) {
 }
 
 // Collapse each of `rows` rows of `cols` Jacobian points (row-major in buf) to its sum, left in buf[row].
-int reduce_rows(G2JStore* buf, G2JStore* tmp, uint32_t rows, uint32_t cols, hipStream_t st, uint32_t max_chunk = 32) {
+// Pairwise levels by default (one dependent addition per lane per launch): these launches run on a nearly
+// empty chip, so their time is the depth of the addition chain, not the number of additions.
+int reduce_rows(G2JStore* buf, G2JStore* tmp, uint32_t rows, uint32_t cols, hipStream_t st, uint32_t max_chunk = 2) {
   G2JStore* src = buf;
   G2JStore* dst = tmp;
   while (cols > 1) {
@@ -277,11 +279,9 @@ int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA
              (const uint32_t*)offset, (const uint32_t*)chunk_off, (const uint32_t*)list, PA, PB, chunks));
   RET(launch("k_msm_buckets", k_msm_buckets, nbk * MSM_BSPLIT * nsides, 128, st, max_chunks, nsides, nbk,
              (const uint32_t*)chunk_off, (const G2JStore*)chunks, BP));
-  // pairwise levels (one dependent addition per lane per launch): these launches run on a nearly empty chip,
-  // so their time is the depth of the addition chain, not the number of additions
-  RET(reduce_rows(BP, tmp, nbk * nsides, MSM_BSPLIT, st, 2));  // B[side][b] = BP[side * nbk + b]
+  RET(reduce_rows(BP, tmp, nbk * nsides, MSM_BSPLIT, st));  // B[side][b] = BP[side * nbk + b]
   RET(launch("k_msm_slices", k_msm_slices, nsides * nwin * MSM_C * MSM_SLICE_LANES, 128, st, nsides, nwin, (const G2JStore*)BP, P1));
-  RET(reduce_rows(P1, tmp, nsides * nwin * MSM_C, MSM_SLICE_LANES, st, 2));  // S[side][w][k] = P1[...]
+  RET(reduce_rows(P1, tmp, nsides * nwin * MSM_C, MSM_SLICE_LANES, st));  // S[side][w][k] = P1[...]
   RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * nwin * nsides, 128, st, nwin, 1u, (const G2JStore*)P1, W));
   RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsides, 128, st, nwin, (const G2JStore*)W, *out));
   if (win) *win = W;
@@ -325,7 +325,7 @@ int msm_run_keyed(const Batch& b, uint64_t seed, const uint8_t* iso, bool test_w
   RET(launch("k_kmsm_buckets", k_kmsm_buckets, nkeys, 128, st, nkeys, (const uint32_t*)chunk_off,
              (const G2JStore*)chunks, B));
   RET(launch("k_kmsm_slices", k_kmsm_slices, nsets * nwin * MSM_C * 16, 128, st, nsets, nwin, (const G2JStore*)B, P1));
-  RET(reduce_rows(P1, tmp, nsets * nwin * MSM_C, 16, st, 4));  // S[set][w][k] = P1[...]
+  RET(reduce_rows(P1, tmp, nsets * nwin * MSM_C, 16, st));  // S[set][w][k] = P1[...]
   RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * nwin * nsets, 128, st, nwin, nsets, (const G2JStore*)P1, W));
   RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsets, 128, st, nwin, (const G2JStore*)W, Ts));
   if (win) *win = W;
