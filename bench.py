@@ -199,7 +199,7 @@ def adversarial_bench(L, tbls, chain_sigs, R, t=129, n=256, frac=0.10, n_short=3
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--rounds", type=int, default=100000, help="rounds per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
