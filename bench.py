@@ -1,21 +1,31 @@
-"""Benchmark of the threshold-BLS hot path (BASELINE.json): verified beacon rounds/s.
+"""Benchmark of the threshold-BLS hot path (BASELINE.json): verified beacon rounds/s, Recover/s at n = 64.
 
-A step = one dg_verify_beacons_dev pass over this rank's contiguous range of the synthetic linked chain
-(beacon.Message on the device, hash-to-G2, sigma decode + subgroup check, RLC multi-pairing with one
-shared final exponentiation; BASELINE configs[1] at N = 1: 100k rounds, one shared group key), inputs
-resident in HBM, followed by the RCCL all-gather of the per-round verdict bitmaps (configs[3] at N > 1,
-one contiguous round range per GPU, weak scaling).
+A step = one pass of beacon.VerifyBeacon (beacon/chain.go:65-71) over this rank's contiguous range of the
+synthetic linked chain, in device-resident batches of at most --batch rounds (beacon.Message on the device,
+hash-to-G2, sigma decode with a batched subgroup check, RLC multi-pairing with one shared final
+exponentiation; asynchronous, so one batch's latency-bound tail overlaps the next batch's head), then the
+RCCL all-gather of the per-round verdict bitmaps.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--rounds R] [--no-cpu-baseline]
+    N = 1 (default): BASELINE configs[1], 100k rounds per step, one shared group key.
+    N > 1:           BASELINE configs[3], the 1M-round chain per step sharded into N contiguous ranges
+                     (strong scaling; --global-rounds overrides the total at any N).
 
-Rank 0 prints ONE JSON line (contract in the task statement); the roofline object is the integer
-multiply-add rate of the dominant kernel (algorithmic MACs from profiles/opcounts.json / its average
-HIP-event duration measured live on the launch stream) against the measured v_mad_u64_u32 peak.
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--global-rounds R] [--no-cpu-baseline]
+
+--gpus N without a torchrun environment starts the N ranks itself (torch.distributed.run as a child
+process, before anything touches the GPU) and exits with their status; a rank whose WORLD_SIZE differs
+from --gpus exits non-zero.  Rank 0 prints ONE JSON line (contract in the task statement).  Beside the
+headline it carries the Recover lines (configs[2] C3 and configs[4] C5, sharded the same way, their
+outputs all-gathered), the live-round latency lines, the syncFrom catch-up line, the
+CPU baselines (rank 0 at N = 1 only) and the roofline objects: algorithmic multiply-adds of the dominant
+kernel (profiles/opcounts.json) over its HIP-event launch time, against the measured v_mad_u64_u32 peak.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,6 +43,16 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def cpu_threads():
+    """Host threads for the CPU baselines: the CPUs this process may run on, capped by OMP_NUM_THREADS (the
+    GPU box sets it to this GPU's CPU share; nproc there counts the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def traffic_of(kernel):
     """HBM-side bytes per launch of `kernel` from the committed PMC passes (profiles/traffic.json, made by
     tools/traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench): 2 x
@@ -45,7 +65,7 @@ def traffic_of(kernel):
 
 
 def load_chain(total):
-    """(sigs (total, 96), prev_sig of round 1) for rounds 1..total of the synthetic chain."""
+    """sigs (total, 96) of rounds 1..total of the synthetic chain (the smallest chain file that holds them)."""
     best = None
     d = os.path.join(ROOT, "data")
     if os.path.isdir(d):
@@ -73,12 +93,32 @@ def gpu_signed_rounds(lib_tbls, first, n, x):
     return prev, sigs
 
 
-def cpu_baseline(pk, msgs, sigs, seconds=10.0, threads=16):
-    """The CPU twin (C port of the reference algorithm: one full pairing check per beacon) on a bounded
-    sample of the same rounds, `threads` POSIX threads."""
+def roofline_of(kt, kernel_units, peak, extra=None):
+    """Roofline object of the dominant kernel of a timing table {name: (avg us, launches)}: the kernel with
+    the largest total time among those profiles/opcounts.json prices; kernel_units[name] = units per launch."""
+    oc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["per_unit"]
+    cands = [(us * n, name, us) for name, (us, n) in kt.items() if name in oc and name in kernel_units]
+    if not cands:
+        return None
+    _, name, us = max(cands)
+    macs = oc[name]["macs"]
+    units = kernel_units[name]
+    achieved = macs * units / (us * 1e-6) / 1e12
+    out = {"bound": "valu-int", "achieved": achieved, "peak": peak["tmac_s"], "unit": "TMAC/s",
+           "frac": achieved / peak["tmac_s"], "traffic": traffic_of(name), "kernel": name, "kernel_avg_us": us,
+           "units_per_launch": units, "macs_per_unit": macs, "peak_source": peak["source"]}
+    if extra:
+        out.update(extra)
+    return out
+
+
+# ------------------------------------------------------------------------------------------ CPU baselines
+def cpu_verify(pk, msgs, sigs, threads, seconds=8.0):
+    """C2 on the host: the CPU twin (C port of the reference algorithm: one full pairing check per beacon)
+    on a bounded sample of the same rounds."""
     from oracle import twin
 
-    n0 = 64
+    n0 = 32
     t0 = time.time()
     twin.verify_batch(pk, msgs[:n0], sigs[:n0], threads=1)
     per = (time.time() - t0) / n0
@@ -92,35 +132,267 @@ def cpu_baseline(pk, msgs, sigs, seconds=10.0, threads=16):
                       "bls.Verify: 2 Miller loops + final exp per round), %d threads, %.1f s" % (n, threads, dt)}
 
 
-def recover_bench(L, tbls, chain_sigs, first_round, R, t, n, steps):
-    """BASELINE configs[2]: VerifyPartial on every share + Lagrange Recover for an (n, t) group
-    over R rounds of the chain, through dg_recover (host-buffer API: the 98 B partials cross PCIe inside the
-    timed region).  Partials are produced on the GPU by dg_sign (untimed); every recovered signature must
-    equal the chain's signature byte for byte."""
+def cpu_c1(threads, rounds=1000):
+    """BASELINE configs[0] (C1) on the host: n = 5, t = 3; per round 5 tbls.Sign, Recover (re-verifying each
+    examined share) and VerifyRecovered (beacon/beacon_test.go:41-93, beacon/beacon.go:433-494)."""
+    from oracle import twin
+
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "groups.json")))["t3"]
+    coeffs = S.poly_coeffs(3)
+    shares = [S.share_value(coeffs, i) for i in range(5)]
+    commits = [bytes.fromhex(c) for c in g]
+    import hashlib
+
+    msgs = np.frombuffer(b"".join(hashlib.sha256(b"c1/%d" % r).digest() for r in range(rounds)),
+                         np.uint8).reshape(rounds, 32)
+    t0 = time.time()
+    _, ok = twin.c1_batch(commits, 3, 5, shares, msgs, threads=threads)
+    dt = time.time() - t0
+    assert ok == rounds, "CPU twin C1 round failed"
+    return {"value": rounds / dt, "unit": "rounds/s", "cores": threads, "kind": "port",
+            "sample": "%d rounds, n=5 t=3: 5 Signs + Recover + VerifyRecovered per round, CPU twin, %d threads, "
+                      "%.1f s" % (rounds, threads, dt)}
+
+
+def cpu_recover(commits, t, n, msgs, parts, threads, seconds=8.0, label=""):
+    """Recover (the kyber algorithm: VerifyPartial of each examined share in input order, Lagrange over the
+    first t valid) on the host over a bounded sample of the same rounds."""
+    from oracle import twin
+
+    t0 = time.time()
+    twin.recover_batch(commits, t, n, msgs[:1], parts[:1], threads=1)
+    per = time.time() - t0
+    R = int(min(len(msgs), max(threads, seconds * threads / per)))
+    t0 = time.time()
+    _, rs, ss = twin.recover_batch(commits, t, n, msgs[:R], parts[:R], threads=threads)
+    dt = time.time() - t0
+    return {"value": R / dt, "unit": "recovers/s", "cores": threads, "kind": "port",
+            "statuses_per_s": int((ss != 255).sum()) / dt,
+            "sample": "%d rounds of the same %s partials, CPU twin tbls.Recover, %d threads, %.1f s"
+                      % (R, label, threads, dt)}, (rs, ss, R)
+
+
+# --------------------------------------------------------------------------------------- Recover lines
+def make_group_rounds(tbls, chain_sigs, first, R, t, n):
+    """Partials sigma_{i,r} = x_i H(m_r) of an (n, t) group for chain rounds first..first+R-1, signed on the
+    GPU (untimed).  Returns (pub, commits, shares, msgs (R, 32), parts (R, n, 98))."""
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "groups.json")))["t%d" % t]
-    pub = tbls.PubPoly([bytes.fromhex(c) for c in g])
+    commits = [bytes.fromhex(c) for c in g]
+    pub = tbls.PubPoly(commits)
     coeffs = S.poly_coeffs(t)
     shares = [S.share_value(coeffs, i) for i in range(n)]
-    rounds = np.arange(first_round, first_round + R, dtype=np.uint64)
+    rounds = np.arange(first, first + R, dtype=np.uint64)
     prev = [bytes(chain_sigs[r - 2]) if r >= 2 else S.GENESIS_SEED for r in rounds.tolist()]
     msgs = tbls.beacon_messages(rounds - 1, rounds, prev)
-    sc = [shares[i] for _ in range(R) for i in range(n)]
-    idx = [i for _ in range(R) for i in range(n)]
+    parts = np.empty((R, n, 98), np.uint8)
+    step = max(1, 2000000 // n)
+    for a in range(0, R, step):
+        b = min(R, a + step)
+        sc = [shares[i] for _ in range(a, b) for i in range(n)]
+        idx = [i for _ in range(a, b) for i in range(n)]
+        parts[a:b] = tbls.sign_batch(sc, np.repeat(msgs[a:b], n, axis=0), idx).reshape(b - a, n, 98)
+    return pub, commits, shares, msgs, parts
+
+
+def gather_recover(sigs, rs, ss, world, total):
+    """All-gather of the Recover outputs of every rank's contiguous range (RCCL) -> numpy (total, ...)."""
+    import torch
+
+    from drand_amd import shard
+
+    if world == 1:
+        return sigs, rs, ss
+    dev = torch.device("cuda", torch.cuda.current_device())
+    out = [shard.allgather_rows(torch.from_numpy(np.ascontiguousarray(x)).to(dev), world, total).cpu().numpy()
+           for x in (sigs, rs, ss)]
+    return out[0], out[1].reshape(-1), out[2]
+
+
+def timed_ranks(fn, world):
+    """fn() between barriers; the max over ranks of its wall time."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    parts = tbls.sign_batch(sc, np.repeat(msgs, n, axis=0), idx).reshape(R, n, 98)
+    res = fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return res, dt
+
+
+def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps=2):
+    """BASELINE configs[2]: VerifyPartial on every share + Lagrange Recover for an (n, t) group over
+    R_total rounds of the chain, each rank its contiguous range through dg_recover (host-buffer API: the 98 B
+    partials cross PCIe inside the timed region), then the RCCL all-gather of the recovered signatures, round
+    statuses and share statuses.  Every recovered signature must equal the chain's byte for byte."""
+    a, b = shard.round_range(R_total, world, rank)
+    R = b - a
+    t0 = time.perf_counter()
+    pub, commits, shares, msgs, parts = make_group_rounds(tbls, chain, a + 1, R, t, n)
     gen_s = time.perf_counter() - t0
-    sigs, rs, ss = tbls.recover_batch(pub, msgs, parts, t, n, seed=5)  # warmup + check
-    want = chain_sigs[first_round - 1:first_round - 1 + R]
-    assert not rs.any() and np.array_equal(sigs, want), "recovered signatures differ from the chain"
-    t0 = time.perf_counter()
+    tbls.recover_batch(pub, msgs, parts, t, n, seed=5)  # warmup (workspace growth)
+    dts = []
     for s in range(steps):
-        tbls.recover_batch(pub, msgs, parts, t, n, seed=6 + s)
-    dt = (time.perf_counter() - t0) / steps
-    return {"metric": "Recover/s at n=%d t=%d (all %d shares VerifyPartial'd, first t valid interpolated)" % (n, t, n),
-            "value": R / dt, "unit": "recovers/s", "rounds": R, "partials_per_round": n, "s_per_step": dt,
-            "partials_verified_per_s": R * n / dt, "partials_generated_s": gen_s,
-            "note": "host-buffer C-ABI (dg_recover): PCIe transfer of %d MB of partials inside the timed region; "
-                    "recovered signatures equal the chain's" % (R * n * 98 // 10**6)}
+        (sigs, rs, ss), dt = timed_ranks(lambda: tbls.recover_batch(pub, msgs, parts, t, n, seed=6 + s), world)
+        dts.append(dt)
+    (gs, grs, gss), gdt = timed_ranks(lambda: gather_recover(sigs, rs, ss, world, R_total), world)
+    assert not grs.any() and np.array_equal(gs, chain[:R_total]), "recovered signatures differ from the chain"
+    assert (gss[:, :t] == 0).all() and (gss[:, t:] == 255).all(), "share statuses"
+    dt = min(dts)
+    # per-kernel timing of one more call: the dominant kernel's roofline
+    L.check(L.lib().dg_set_timing(1))
+    tbls.recover_batch(pub, msgs, parts, t, n, seed=9)
+    kt = L.timings()
+    L.check(L.lib().dg_set_timing(0))
+    units = {"k_decode_items": R * n, "k_recover_terms": R * t, "k_h2c_uncleared": R,
+             "k_kmsm_chunks": None}
+    units = {k: v for k, v in units.items() if v}
+    roof = roofline_of(kt, units, peak, {"timing": "HIP events on the launch stream, one dg_recover call"})
+    out = {"metric": "Recover/s at n=%d t=%d (all %d shares VerifyPartial'd, first t valid interpolated)" % (n, t, n),
+           "value": R_total / (dt + gdt), "unit": "recovers/s", "n_gpus": world, "rounds": R_total,
+           "rounds_per_gpu": R, "partials_per_round": n, "s_per_step": dt, "allgather_s": gdt,
+           "partials_verified_per_s": R_total * n / (dt + gdt), "partials_generated_s": gen_s,
+           "roofline": roof, "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
+           "note": "host-buffer C-ABI (dg_recover): PCIe transfer of %d MB of partials per GPU inside the timed "
+                   "region; outputs all-gathered (RCCL) and equal to the chain's signatures"
+                   % (R * n * 98 // 10**6)}
+    return out, (commits, msgs, parts)
+
+
+def adversarial_bench(L, tbls, shard, chain, R_total, world, rank, t=129, n=256, frac=0.10, n_short=3):
+    """BASELINE configs[4]: n = 256, t = 129, ~10% of the (round, share) cells corrupted with the six
+    cycling modes of tools/corrupt.py, plus `n_short` rounds with more than n - t corrupted shares (-> "not
+    enough shares"); each rank its contiguous range of R_total rounds through dg_recover (the batch equation
+    fails, so the examined prefix of every round takes the exact per-item check), then the all-gather of the
+    outputs.  Checked without the CPU: recovered signatures equal the chain's, exactly the short rounds
+    report NOT_ENOUGH, every examined corrupted share is rejected and every examined clean one accepted
+    (per-share parity with the CPU twin is tests/test_gpu_parity.py's job)."""
+    from tools import corrupt
+
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "groups.json")))["t%d" % t]
+    commits = [bytes.fromhex(c) for c in g]
+    pub = tbls.PubPoly(commits)
+    coeffs = S.poly_coeffs(t)
+    shares = [S.share_value(coeffs, i) for i in range(n)]
+    a, b = shard.round_range(R_total, world, rank)
+    R = b - a
+    rounds = np.arange(a + 1, b + 2, dtype=np.uint64)  # one extra round for the "other_round" mode
+    prev = [bytes(chain[r - 2]) if r >= 2 else S.GENESIS_SEED for r in rounds.tolist()]
+    msgs_all = tbls.beacon_messages(rounds - 1, rounds, prev)
+    msgs = msgs_all[:R]
+    t0 = time.perf_counter()
+    parts = tbls.sign_batch([shares[i] for _ in range(R) for i in range(n)], np.repeat(msgs, n, axis=0),
+                            [i for _ in range(R) for i in range(n)]).reshape(R, n, 98)
+    # corruption pattern of the GLOBAL round numbers, so it does not depend on the rank count
+    items = [it for it in corrupt.pick(R_total, n, frac) if a <= it[0] < b]
+    items = [(r - a, j, m) for r, j, m in items]
+    short = set(r - a for r in range(n_short) if a <= r < b)
+    items = [it for it in items if it[0] not in short] + [(r, j, "random_bytes") for r in sorted(short)
+                                                           for j in range(n - t + 2)]
+
+    def resign(reqs):
+        sc = [shares[idx] + ds for _, idx, ds, _ in reqs]
+        return tbls.sign_batch(sc, np.stack([msgs_all[r + dr] for r, _, _, dr in reqs]))
+
+    corrupt.corrupt_batch(parts, items, n, resign)
+    gen_s = time.perf_counter() - t0
+    bad = np.zeros((R, n), dtype=bool)
+    for r, j, _ in items:
+        bad[r, j] = True
+    tbls.recover_batch(pub, msgs, parts, t, n, seed=11)  # warmup
+    (sigs, rs, ss), dt = timed_ranks(lambda: tbls.recover_batch(pub, msgs, parts, t, n, seed=12), world)
+    ok_r = np.array([r not in short for r in range(R)], dtype=bool)
+    assert np.array_equal(rs != 0, ~ok_r) and (rs[~ok_r] == 5).all(), "round statuses"
+    assert np.array_equal(sigs[ok_r], chain[a:b][ok_r]), "recovered signatures differ from the chain"
+    examined = ss != 255
+    assert (ss[examined & bad] != 0).all() and (ss[examined & ~bad] == 0).all(), "share statuses"
+    (gs, grs, gss), gdt = timed_ranks(lambda: gather_recover(sigs, rs, ss, world, R_total), world)
+    assert gs.shape == (R_total, 96) and gss.shape == (R_total, n)
+    L.check(L.lib().dg_set_timing(1))
+    tbls.recover_batch(pub, msgs, parts, t, n, seed=13)
+    kt = L.timings()
+    L.check(L.lib().dg_set_timing(0))
+    ncorrupt = np.array([len(items)], np.int64)
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        c = torch.from_numpy(ncorrupt).cuda()
+        dist.all_reduce(c)
+        ncorrupt = c.cpu().numpy()
+    return {"metric": "adversarial Recover/s at n=%d t=%d, %.0f%% of shares corrupted (C5)" % (n, t, 100 * frac),
+            "value": R_total / (dt + gdt), "unit": "recovers/s", "n_gpus": world, "rounds": R_total,
+            "rounds_per_gpu": R, "partials_per_round": n, "corrupted_shares": int(ncorrupt[0]),
+            "short_rounds": n_short, "s_per_step": dt, "allgather_s": gdt,
+            "statuses_per_s": int((gss != 255).sum()) / (dt + gdt), "setup_s": gen_s,
+            "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
+            "note": "host-buffer C-ABI (dg_recover), PCIe transfer of %d MB of partials per GPU inside the timed "
+                    "region; the batch equation fails, so the examined prefix of every round takes the per-item "
+                    "pairing check; outputs all-gathered (RCCL)" % (R * n * 98 // 10**6)}, (commits, msgs, parts,
+                                                                                             ss, rs)
+
+
+def c1_gpu(L, tbls, reps=3, rounds=1000):
+    """BASELINE configs[0] (C1) on the GPU, the same work as cpu_c1: 5 tbls.Sign per round (dg_sign), Recover
+    (dg_recover: VerifyPartial of the shares + Lagrange) and VerifyRecovered (dg_verify) of 1000 rounds."""
+    import hashlib
+
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "groups.json")))["t3"]
+    pub = tbls.PubPoly([bytes.fromhex(c) for c in g])
+    coeffs = S.poly_coeffs(3)
+    shares = [S.share_value(coeffs, i) for i in range(5)]
+    msgs = np.frombuffer(b"".join(hashlib.sha256(b"c1/%d" % r).digest() for r in range(rounds)),
+                         np.uint8).reshape(rounds, 32)
+
+    def run():
+        parts = tbls.sign_batch([shares[i] for _ in range(rounds) for i in range(5)], np.repeat(msgs, 5, axis=0),
+                                [i for _ in range(rounds) for i in range(5)]).reshape(rounds, 5, 98)
+        sigs, rs, _ = tbls.recover_batch(pub, msgs, parts, 3, 5)
+        st = tbls.verify_recovered_batch(pub.commit(), msgs, sigs)
+        assert not rs.any() and not st.any()
+        return sigs
+
+    run()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    dt = (time.perf_counter() - t0) / reps
+    return {"metric": "C1: n=5 t=3, 5 Signs + Recover + VerifyRecovered per round (BASELINE configs[0])",
+            "value": rounds / dt, "unit": "rounds/s", "rounds": rounds, "s_per_step": dt,
+            "note": "three blocking host-buffer calls per 1000 rounds (dg_sign, dg_recover, dg_verify)"}
+
+
+def live_latency(L, tbls, commits, msgs, parts, t, n, reps=20):
+    """SURVEY §8(f) row 4, the live round (beacon/beacon.go:472-494): one round's Recover with the
+    VerifyPartial verdicts ProcessBeacon already holds (dg_recover_verified: no re-verification) and the
+    VerifyRecovered of its output, per call; plus the full dg_recover of one round for comparison."""
+    pub = tbls.PubPoly(commits)
+    m1, p1 = msgs[:1], parts[:1]
+    st = np.zeros((1, n), np.uint8)
+    sig, rs, _ = tbls.recover_verified_batch(pub, m1, p1, st, t, n)
+    assert not rs.any()
+    out = {}
+    for name, fn in (("recover_verified_ms", lambda: tbls.recover_verified_batch(pub, m1, p1, st, t, n)),
+                     ("recover_full_ms", lambda: tbls.recover_batch(pub, m1, p1, t, n)),
+                     ("verify_recovered_ms", lambda: tbls.verify_recovered_batch(pub.commit(), m1, sig))):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        out[name] = (time.perf_counter() - t0) / reps * 1e3
+    out.update({"metric": "live-round latency, one round at n=%d t=%d (ms per call)" % (n, t),
+                "note": "host-buffer blocking calls; recover_verified takes the ProcessBeacon verdicts "
+                        "(beacon/beacon.go:148) instead of re-verifying the shares (:488)"})
+    return out
 
 
 def sync_bench(chain_sigs, R, batch=25000):
@@ -143,57 +415,12 @@ def sync_bench(chain_sigs, R, batch=25000):
             "note": "host Beacon objects -> dg_check_links + dg_verify_beacons per batch (host-buffer API, blocking)"}
 
 
-def adversarial_bench(L, tbls, chain_sigs, R, t=129, n=256, frac=0.10, n_short=3):
-    """BASELINE configs C5: n = 256, t = 129, R rounds, ~10% of the (round, share) cells
-    corrupted with the six cycling modes of tools/corrupt.py, plus `n_short` rounds with more than n - t
-    corrupted shares (-> "not enough shares").  One dg_recover over all R x n partials (VerifyPartial on
-    every share -- the batch equation fails, so every share takes the exact per-item check -- then
-    Recover).  Checked without the CPU: recovered signatures equal the chain's, exactly the short rounds
-    report NOT_ENOUGH, every examined corrupted share is rejected and every examined clean one accepted
-    (per-share parity with the CPU twin is tests/test_gpu_parity.py's job)."""
-    from tools import corrupt
-
-    g = json.load(open(os.path.join(ROOT, "tests", "golden", "groups.json")))["t%d" % t]
-    pub = tbls.PubPoly([bytes.fromhex(c) for c in g])
-    coeffs = S.poly_coeffs(t)
-    shares = [S.share_value(coeffs, i) for i in range(n)]
-    rounds = np.arange(1, R + 2, dtype=np.uint64)  # one extra round for the "other_round" mode
-    prev = [S.GENESIS_SEED] + [bytes(chain_sigs[r - 2]) for r in rounds.tolist()[1:]]
-    msgs_all = tbls.beacon_messages(rounds - 1, rounds, prev)
-    msgs = msgs_all[:R]
-    t0 = time.perf_counter()
-    parts = tbls.sign_batch([shares[i] for _ in range(R) for i in range(n)], np.repeat(msgs, n, axis=0),
-                            [i for _ in range(R) for i in range(n)]).reshape(R, n, 98)
-    items = corrupt.pick(R, n, frac)
-    short = set(range(n_short))
-    items = [it for it in items if it[0] not in short] + [(r, j, "random_bytes") for r in short
-                                                           for j in range(n - t + 2)]
-
-    def resign(reqs):
-        sc = [shares[idx] + ds for _, idx, ds, _ in reqs]
-        return tbls.sign_batch(sc, np.stack([msgs_all[r + dr] for r, _, _, dr in reqs]))
-
-    corrupt.corrupt_batch(parts, items, n, resign)
-    gen_s = time.perf_counter() - t0
-    bad = np.zeros((R, n), dtype=bool)
-    for r, j, _ in items:
-        bad[r, j] = True
-    sigs, rs, ss = tbls.recover_batch(pub, msgs, parts, t, n, seed=11)  # warmup + check
-    ok_r = np.array([r not in short for r in range(R)])
-    assert np.array_equal(rs != 0, ~ok_r) and (rs[~ok_r] == 5).all(), "round statuses"
-    assert np.array_equal(sigs[ok_r], chain_sigs[:R][ok_r]), "recovered signatures differ from the chain"
-    examined = ss != 255
-    assert (ss[examined & bad] != 0).all() and (ss[examined & ~bad] == 0).all(), "share statuses"
-    t0 = time.perf_counter()
-    tbls.recover_batch(pub, msgs, parts, t, n, seed=12)
-    dt = time.perf_counter() - t0
-    return {"metric": "adversarial Recover/s at n=%d t=%d, %.0f%% of shares corrupted (C5)" % (n, t, 100 * frac),
-            "value": R / dt, "unit": "recovers/s", "rounds": R, "partials_per_round": n,
-            "corrupted_shares": int(bad.sum()), "short_rounds": n_short, "s_per_step": dt,
-            "partials_verified_per_s": R * n / dt, "setup_s": gen_s,
-            "note": "host-buffer C-ABI (dg_recover), PCIe transfer of %d MB of partials inside the timed region; "
-                    "every batch fails its RLC check, so all shares take the per-item pairing check"
-                    % (R * n * 98 // 10**6)}
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
 def main():
@@ -201,25 +428,38 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--rounds", type=int, default=100000, help="rounds per GPU per step")
+    ap.add_argument("--global-rounds", type=int, default=0,
+                    help="rounds per step over all GPUs (default 100k at N = 1, the 1M chain at N > 1)")
+    ap.add_argument("--batch", type=int, default=100000, help="max rounds per device batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--sync", dest="use_sync", action="store_true",
-                    help="blocking dg_verify_beacons_dev per step (default: dg_verify_beacons_dev_async, so the "
+                    help="blocking dg_verify_beacons_dev per batch (default: dg_verify_beacons_dev_async, so the "
                          "latency-bound tail of one batch overlaps the head of the next)")
     ap.add_argument("--no-kernel-timing", action="store_true",
-                    help="no per-kernel HIP events in the timed region (no roofline)")
-    ap.add_argument("--recover-rounds", type=int, default=20000, help="0 disables the Recover line")
-    ap.add_argument("--c5-rounds", type=int, default=10000, help="0 disables the adversarial (C5) line")
+                    help="no per-kernel HIP events after the timed region (no roofline)")
+    ap.add_argument("--recover-rounds", type=int, default=100000, help="C3 rounds (all GPUs); 0 disables")
+    ap.add_argument("--c5-rounds", type=int, default=10000, help="C5 rounds (all GPUs); 0 disables")
     ap.add_argument("--sync-rounds", type=int, default=100000, help="0 disables the syncFrom catch-up line")
+    ap.add_argument("--no-c1", action="store_true", help="no C1 / live-latency lines")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # start the N ranks (one process per GPU) before anything in this process touches the GPU
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+        cmd += sys.argv[1:]
+        log("launching", " ".join(cmd))
+        sys.exit(subprocess.call(cmd))
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("world size %d != --gpus %d" % (world, args.gpus))
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -229,22 +469,24 @@ def main():
     from drand_amd import tbls, shard
 
     lib = L.lib(local)
-    R = args.rounds
+    G = args.global_rounds or (100000 if world == 1 else 1000000)
     x = S.master_secret()
     pk = S.GROUP_PK  # x * g1, the chain's group key (public fixture constant)
-    a, b = shard.round_range(world * R, world, rank)
-    chain = load_chain(world * R)
+    a, b = shard.round_range(G, world, rank)
+    n = b - a
+    chain = load_chain(G)
     if chain is not None:
         sigs = chain[a:b]
         prev = chain[a - 1:b - 1] if a > 0 else np.concatenate([np.zeros((1, 96), np.uint8), chain[:b - 1]])
         data = "synthetic linked chain data/chain_v1 (CPU-twin generated, seed tools/synthetic.py)"
         linked = True
     else:
-        prev, sigs = gpu_signed_rounds(tbls, a + 1, b - a, x)
+        prev, sigs = gpu_signed_rounds(tbls, a + 1, n, x)
         data = "synthetic rounds, GPU-signed (no chain file: prev_sig pseudo-random, links not checked)"
         linked = False
-    n = b - a
-    mbytes = (max(y - x for x, y in (shard.round_range(world * R, world, q) for q in range(world))) + 7) // 8
+    nb = max(1, -(-n // args.batch))
+    bounds = [(n * i // nb, n * (i + 1) // nb) for i in range(nb)]
+    mbytes = (max(y - x_ for x_, y in (shard.round_range(G, world, q) for q in range(world))) + 7) // 8
     rounds = np.arange(a + 1, b + 1, dtype=np.uint64)
     prev_sigs = [bytes(p) for p in prev]
     if a == 0 and linked:
@@ -255,30 +497,35 @@ def main():
     d_ps = torch.from_numpy(psb).to(dev)
     d_off = torch.from_numpy(off.astype(np.int32)).to(dev)
     d_sig = torch.from_numpy(np.ascontiguousarray(sigs)).to(dev)
-    # one status buffer per in-flight batch (the library rotates over DG_SETS = 4 workspace sets)
-    nbuf = 4
+    # status buffers rotate over the steps in flight (the library itself keeps at most DG_SETS = 4 batches
+    # in flight); a buffer is reused once the all-gather that read it has finished
+    nbuf = 3
     d_sts = [torch.full((n,), 99, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
     gathered = [None] * nbuf
     side = torch.cuda.Stream(dev)
     pkb = ctypes.c_char_p(pk)
     counter = [0]
 
+    def enqueue(lo, hi, d_st, seed, blocking):
+        args_ = (pkb, hi - lo, L.ptr(d_pr[lo:]), L.ptr(d_r[lo:]), L.ptr(d_ps), L.ptr(d_off[lo:]), L.ptr(d_sig[lo:]),
+                 L.ptr(d_st[lo:]), seed)
+        if blocking:
+            L.check(lib.dg_verify_beacons_dev(*args_, None))
+        else:
+            L.check(lib.dg_verify_beacons_dev_async(*args_, None, ctypes.c_void_p(side.cuda_stream)))
+
     def step(seed):
-        """Enqueue one batch (asynchronously: consecutive batches overlap) and the all-gather of its verdict
-        bitmap on a side stream that waits for the batch; returns the gathered bitmap tensor."""
+        """Enqueue this rank's batches (asynchronously: consecutive batches overlap) and the all-gather of the
+        rank's verdict bitmap on a side stream that waits for them; returns the gathered bitmap tensor."""
         i = counter[0] % nbuf
         counter[0] += 1
         if gathered[i] is not None:
             gathered[i][1].synchronize()  # the all-gather that read this status buffer has finished
         d_st = d_sts[i]
+        for j, (lo, hi) in enumerate(bounds):
+            enqueue(lo, hi, d_st, seed * 64 + j, args.use_sync)
         if args.use_sync:
-            L.check(lib.dg_verify_beacons_dev(pkb, n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off),
-                                              L.ptr(d_sig), L.ptr(d_st), seed, None))
             side.wait_stream(torch.cuda.current_stream(dev))
-        else:
-            L.check(lib.dg_verify_beacons_dev_async(pkb, n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off),
-                                                    L.ptr(d_sig), L.ptr(d_st), seed, None,
-                                                    ctypes.c_void_p(side.cuda_stream)))
         with torch.cuda.stream(side):
             bits = shard.allgather_verdicts(d_st, world, m=mbytes)
             ev = torch.cuda.Event()
@@ -292,7 +539,7 @@ def main():
 
     # prime every workspace set once (its grow-only buffers are allocated on first use), then the W warmup
     # steps: no allocation or first-dispatch cost falls inside the timed region
-    for w in range(nbuf):
+    for w in range(max(1, 4 // nb + 1)):
         step(500 + w)
     drain()
     for w in range(args.warmup):
@@ -300,8 +547,7 @@ def main():
     drain()
     bitmap = step(7)
     drain()
-    used = min(counter[0], nbuf)
-    assert all(int(d.max().item()) == 0 for d in d_sts[:used]), "valid chain rounds rejected"
+    assert all(int(d.max().item()) == 0 for d in d_sts[:min(counter[0], nbuf)]), "valid chain rounds rejected"
     assert bitmap.sum().item() == 0
     if world > 1:
         dist.barrier()
@@ -316,87 +562,100 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    used = min(counter[0], nbuf)
-    assert all(int(b.sum().item()) == 0 for b in bits) and all(int(d.max().item()) == 0 for d in d_sts[:used])
+    assert all(int(bt.sum().item()) == 0 for bt in bits) and all(int(d.max().item()) == 0 for d in d_sts)
     fallbacks = L.fallback_count() - fb0  # timed batches that ran the per-item pass (0 for valid chains)
-    # instrumented replay of the timed region (same steps, same seeds) with HIP events around every
-    # launch on its stream: per-kernel averages while the batches overlap
+    # instrumented replay of the timed region (same steps, same seeds) with HIP events around every launch on
+    # its stream: per-kernel averages while the batches overlap; then one batch through the blocking entry
+    # point, so each kernel runs alone on the chip
     kt, kt_iso = {}, {}
     if not args.no_kernel_timing:
         L.check(lib.dg_set_timing(1))
         [step(17 + s) for s in range(args.steps)]
         drain()
         kt = L.timings()
-        # the same batch through the blocking entry point, so each kernel runs alone on the chip
         L.check(lib.dg_set_timing(0))
         L.check(lib.dg_set_timing(1))
+        lo, hi = bounds[0]
         for s in range(2):
-            L.check(lib.dg_verify_beacons_dev(pkb, n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off),
-                                              L.ptr(d_sig), L.ptr(d_sts[0]), 900 + s, None))
+            enqueue(lo, hi, d_sts[0], 900 + s, True)
         kt_iso = L.timings()
-        assert int(d_sts[0].max().item()) == 0
+        assert int(d_sts[0][lo:hi].max().item()) == 0
         L.check(lib.dg_set_timing(0))
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
-    total = world * n * args.steps
-    if rank == 0:
+    peak = shard.mad_peak(local) if rank == 0 else None
+    roof = None
+    if rank == 0 and kt_iso:
         oc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["per_unit"]
-        # dominant kernel by its isolated time (blocking batches after the timed region, one kernel on the
-        # chip at a time -- the launches rocprofv3 --stats of `bench.py --sync` averages); the same kernel's
-        # average inside the overlapped timed region is reported beside it
-        src = kt_iso if kt_iso else kt
-        name, (us, launches) = max(src.items(), key=lambda kv: kv[1][0] * kv[1][1]) if src else (None, (0, 0))
-        per_launch_units = n
-        macs = oc.get(name, {}).get("macs") if name else None
-        peak = shard.mad_peak()
-        roof = None
-        if macs is not None:
-            achieved = macs * per_launch_units / (us * 1e-6) / 1e12
-            roof = {"bound": "valu-int", "achieved": achieved, "peak": peak["tmac_s"], "unit": "TMAC/s",
-                    "frac": achieved / peak["tmac_s"], "traffic": traffic_of(name), "kernel": name,
-                    "kernel_avg_us": us, "units_per_launch": per_launch_units, "macs_per_unit": macs,
-                    "peak_source": peak["source"],
-                    "timing": "HIP events on the launch stream, blocking batches right after the timed region "
-                              "(the kernel alone on the chip)"}
-            if name in kt:
-                o_us = kt[name][0]
-                a_o = macs * per_launch_units / (o_us * 1e-6) / 1e12
-                roof["overlapped"] = {"kernel_avg_us": o_us, "achieved": a_o, "frac": a_o / peak["tmac_s"],
-                                      "note": "instrumented replay of the timed region: the launch shares the "
-                                              "chip with the other batches in flight"}
-            # whole chip: algorithmic multiply-adds of the per-round work (hash, decode, 16 bucket additions
-            # of the two MSMs + 10 of the subgroup-check test windows, mixed: signatures and hashes are
-            # stored with Z = 1) over the step time; per-batch fixed work not counted
+        per = bounds[0][1] - bounds[0][0]
+        roof = roofline_of(kt_iso, {"k_h2c_uncleared": per, "k_decode_items": per}, peak,
+                           {"timing": "HIP events on the launch stream, blocking batches right after the timed "
+                                      "region (the kernel alone on the chip)"})
+        if roof and roof["kernel"] in kt:
+            o_us = kt[roof["kernel"]][0]
+            a_o = roof["macs_per_unit"] * per / (o_us * 1e-6) / 1e12
+            roof["overlapped"] = {"kernel_avg_us": o_us, "achieved": a_o, "frac": a_o / peak["tmac_s"],
+                                  "note": "instrumented replay of the timed region: the launch shares the chip "
+                                          "with the other batches in flight"}
+        if roof:
+            # whole chip: algorithmic multiply-adds of the per-round work (hash, decode, 16 bucket additions of
+            # the two MSMs + 10 of the subgroup-check test windows, mixed: signatures and hashes are stored with
+            # Z = 1) over the step time; per-batch fixed work not counted
             per_round = (sum(oc[k]["macs"] for k in ("k_h2c_uncleared", "k_decode_items")) +
                          26 * oc["k_msm_chunks[mixed add]"]["macs"])
-            chip = per_round * n * args.steps / dt / 1e12
-            roof["chip"] = {"macs_per_round": per_round, "achieved": chip, "frac": chip / peak["tmac_s"]}
-        share = {k: round(v[0] * v[1] / (dt * 1e6 / 1.0), 4) for k, v in kt.items()}
-        rec = None
-        if args.recover_rounds and chain is not None:
-            rec = recover_bench(L, tbls, chain, 1, min(args.recover_rounds, len(chain)), 33, 64, 1)
-        adv = None
-        if args.c5_rounds and chain is not None:
-            adv = adversarial_bench(L, tbls, chain, min(args.c5_rounds, len(chain) - 1))
-        syn = None
-        if args.sync_rounds and chain is not None:
-            syn = sync_bench(chain, min(args.sync_rounds, len(chain)))
-        cpu = None
-        if not args.no_cpu_baseline:
-            ns = min(n, 40000)  # the sampler stops at ~10 s of 16-thread CPU work
-            m = tbls.beacon_messages(rounds[:ns] - 1, rounds[:ns], prev_sigs[:ns])
-            cpu = cpu_baseline(pk, m, np.ascontiguousarray(sigs[:ns]), threads=args.cpu_threads)
-        out = {"metric": METRIC, "value": total / dt, "unit": "rounds/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "u32 (381-bit Fp, 12x32-bit limbs)", "data": data,
-               "config": {"workload": "batch bls.Verify / beacon.VerifyBeacon of %d linked chain rounds per GPU, one "
-                                      "shared group key (BASELINE configs[1]; configs[3] at N>1)" % n,
-                          "rounds_per_gpu": n, "global_rounds": world * n, "parallelism": "rounds sharded dp%d" % world},
-               "roofline": roof, "cpu_baseline": cpu, "recover": rec, "adversarial": adv, "sync": syn,
-               "batch_fallbacks": fallbacks,
-               "kernel_time_share": share,
+            chip = per_round * G * args.steps / world / dt / 1e12
+            roof["chip"] = {"macs_per_round": per_round, "achieved": chip, "frac": chip / peak["tmac_s"],
+                            "note": "per GPU"}
+    share = {k: round(v[0] * v[1] / (dt * 1e6), 4) for k, v in kt.items()}
+    del d_sts, d_sig, d_ps
+    torch.cuda.empty_cache()
+
+    # Recover lines (sharded like the headline; chain rounds 1..R)
+    rec_chain = load_chain(max(args.recover_rounds, args.c5_rounds + 1, args.sync_rounds, 1000))
+    rec = adv = syn = c1 = lat = None
+    rec_in = adv_in = None
+    if args.recover_rounds and rec_chain is not None:
+        rec, rec_in = recover_bench(L, tbls, shard, rec_chain, args.recover_rounds, 33, 64, world, rank, peak)
+    if args.c5_rounds and rec_chain is not None:
+        adv, adv_in = adversarial_bench(L, tbls, shard, rec_chain, args.c5_rounds, world, rank)
+    if rank == 0:
+        if args.sync_rounds and rec_chain is not None:
+            syn = sync_bench(rec_chain, args.sync_rounds)
+        if not args.no_c1:
+            c1 = c1_gpu(L, tbls)
+            if rec_in is not None:
+                lat = live_latency(L, tbls, rec_in[0], rec_in[1], rec_in[2], 33, 64)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        th = cpu_threads()
+        ns = min(n, 40000)
+        m = tbls.beacon_messages(rounds[:ns] - 1, rounds[:ns], prev_sigs[:ns])
+        cpu = cpu_verify(pk, m, np.ascontiguousarray(sigs[:ns]), th)
+        if c1 is not None:
+            c1["cpu_baseline"] = cpu_c1(th)
+        if rec_in is not None:
+            rec["cpu_baseline"], _ = cpu_recover(rec_in[0], 33, 64, rec_in[1], rec_in[2], th, label="C3 n=64 t=33")
+        if adv_in is not None:
+            cb, (trs, tss, Rs) = cpu_recover(adv_in[0], 129, 256, adv_in[1], adv_in[2], th, seconds=6.0,
+                                             label="C5 n=256 t=129 corrupted")
+            # the GPU's statuses on the same rounds are the twin's (bit-exact sample check)
+            cb["statuses_match_gpu"] = bool(np.array_equal(tss, adv_in[3][:Rs]) and np.array_equal(trs, adv_in[4][:Rs]))
+            adv["cpu_baseline"] = cb
+    if rank == 0:
+        out = {"metric": METRIC, "value": G * args.steps / dt, "unit": "rounds/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+               "higher_is_better": True, "scaling": "strong" if (world > 1 or args.global_rounds) else "weak",
+               "vs_baseline": None, "dtype": "u32 (381-bit Fp, 12x32-bit limbs)", "data": data,
+               "config": {"workload": ("batch bls.Verify / beacon.VerifyBeacon of the %d-round linked chain per "
+                                       "step, %d contiguous range(s) of <= %d rounds per GPU in batches of <= %d, "
+                                       "one shared group key (BASELINE configs[%d])"
+                                       % (G, world, -(-G // world), args.batch, 1 if G <= 100000 else 3)),
+                          "global_rounds": G, "rounds_per_gpu": n, "batches_per_gpu": nb,
+                          "parallelism": "rounds sharded dp%d" % world},
+               "roofline": roof, "cpu_baseline": cpu, "recover": rec, "adversarial": adv, "c1": c1,
+               "live_latency": lat, "sync": syn, "batch_fallbacks": fallbacks, "kernel_time_share": share,
                "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
                "kernel_avg_us_isolated": {k: round(v[0], 1) for k, v in kt_iso.items()}}
         print(json.dumps(out), flush=True)

@@ -43,6 +43,9 @@ SIGNATURES = {
     "dg_pubpoly_eval": ([_P, _U32, _SZ, _P, _P], _I),
     "dg_verify_partials": ([_P, _U32, _SZ, _P, _SZ, _U32, _P, _P, _U64], _I),
     "dg_recover": ([_P, _U32, _U32, _SZ, _P, _SZ, _U32, _P, _P, _P, _P, _U64], _I),
+    "dg_recover_verified": ([_U32, _U32, _SZ, _U32, _P, _P, _P, _P, _P], _I),
+    "dg_set_hash_dst": ([_P, _SZ], _I),
+    "dg_get_hash_dst": ([_P, _SZ, _P], _I),
     "dg_verify_beacons_dev": ([_P, _SZ, _P, _P, _P, _P, _P, _P, _U64, _P], _I),
     "dg_verify_beacons_dev_async": ([_P, _SZ, _P, _P, _P, _P, _P, _P, _U64, _P, _P], _I),
     "dg_wait_all": ([], _I),

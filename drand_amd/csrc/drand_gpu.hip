@@ -5,6 +5,7 @@
 
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <random>
 #include <string>
@@ -69,6 +70,8 @@ struct Ctx {
   std::vector<uint8_t> poly_commits;
   std::vector<uint32_t> poly_idx;
   bool poly_valid = false;
+  // hash-to-G2 DST of sign / verify / recover (dg_set_hash_dst; default the NUL DST)
+  std::vector<uint8_t> dst = std::vector<uint8_t>(kDstNul, kDstNul + kDstNulLen);
 };
 
 std::mutex g_mu;
@@ -92,7 +95,7 @@ enum Slot {
   S_COMMITS, S_COMMITST, S_SLOTIDX, S_ITEMSLOT, S_SEL, S_SELIDX, S_RST, S_SST, S_TERMS, S_IN0, S_IN1, S_IN2, S_IN3,
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
-  S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_COUNT
+  S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -241,22 +244,53 @@ int reduce_rows(G2JStore* buf, G2JStore* tmp, uint32_t rows, uint32_t cols, hipS
 // nslots keys.  Fills S / status / isolate for the N = R*k items; status ends as the exact per-item
 // bls.Verify verdict.
 struct Batch {
-  uint32_t R, k, nslots;
+  uint32_t R, k, nslots;      // nslots: key slots in the batch equation; items of slots >= nslots are checked alone
   const G2JStore* Q;
-  const G1AStore* keys;
+  const G1AStore* keys;       // every item's key (slots >= nslots included)
   const uint8_t* key_status;
   const uint32_t* item_slot;  // N entries, or null when nslots == 1
   const uint8_t* sigs;        // N records of `stride` bytes, sigma at `offset`
   uint32_t stride, offset;
   G2AStore* S;
   uint8_t* status;
+  const uint8_t* msgs;        // R messages of msg_len bytes (device): bound into the batch coefficients
+  uint32_t msg_len;
+  const uint8_t* key_bytes;   // host: the key encoding(s) (48 B pk, or t x 48 B commits)
+  size_t key_len;
   uint32_t prefix_t = 0;  // Recover: after a failed batch, check items only up to each round's t-th valid one
 };
+
+// The batch's coefficient seed (kernels.h k_digest_*): seed' = SHA-256(SHA-256(BE64 seed || key bytes) || D),
+// D = a SHA-256 tree over every (message, signature record) of the batch, left on the device.
+int bind_seed(const Batch& b, uint64_t seed, hipStream_t st, uint64_t** d_seed) {
+  const uint32_t N = b.R * b.k;
+  Sha256 h;
+  sha256_init(h);
+  for (int i = 7; i >= 0; --i) sha256_byte(h, (uint8_t)(seed >> (8 * i)));
+  sha256_update(h, b.key_bytes, (uint32_t)b.key_len);
+  uint8_t seed0[32];
+  sha256_final(h, seed0);
+  uint8_t *d0, *d1, *d_s0;
+  RET(wsT(S_DIG0, (size_t)32 * N, &d0));
+  RET(wsT(S_DIG1, (size_t)32 * ((N + 63) / 64) + 64, &d1));
+  RET(wsT(S_SEED, 48, d_seed));
+  d_s0 = (uint8_t*)(*d_seed + 2);
+  HIPCHK(hipMemcpyAsync(d_s0, seed0, 32, hipMemcpyHostToDevice, st));
+  RET(launch("k_digest_items", k_digest_items, N, 128, st, N, b.k, b.msgs, b.msg_len, b.sigs, b.stride, d0));
+  uint32_t n = N;
+  while (n > 1) {
+    uint32_t m = (n + 63) / 64;
+    RET(launch("k_digest_level", k_digest_level, m, 128, st, n, (const uint8_t*)d0, d1));
+    std::swap(d0, d1);
+    n = m;
+  }
+  return launch("k_digest_seed", k_digest_seed, 1, 64, st, (const uint8_t*)d_s0, (const uint8_t*)d0, *d_seed);
+}
 
 // Pippenger MSM (msm.h): out[0] = sum_r alpha_r PA_r, out[1] = sum_r alpha_r PB_r (PB may be null),
 // over the rounds with active[r] != 0.  With `test_windows` side A also gets the MSM_TWIN test windows of
 // the batched subgroup check; *win = its MSM_WT window sums (checked by k_msm_subgroup).
-int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA, const G2JStore* PB, bool test_windows,
+int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JStore* PA, const G2JStore* PB, bool test_windows,
             G2JStore** out, G2JStore** win, hipStream_t st) {
   const uint32_t nsides = PB ? 2 : 1, nwin = test_windows ? MSM_WT : MSM_WIN, nbk = nwin * MSM_NB;
   uint32_t *cnt, *list;
@@ -264,7 +298,9 @@ int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA
   RET(wsT(S_MSM_CNT, 4 * nbk + 1, &cnt));
   uint32_t *offset = cnt + nbk, *cursor = offset + nbk, *chunk_off = cursor + nbk;
   RET(wsT(S_MSM_LIST, (size_t)nwin * R + 1, &list));
-  const uint32_t max_chunks = (nwin * R) / MSM_CHUNK + nbk;
+  const size_t max_chunks_sz = ((size_t)nwin * R) / MSM_CHUNK + nbk;
+  if (max_chunks_sz * nsides > 0xffffffffull) return fail(DG_E_ARG, "batch too large for the MSM");
+  const uint32_t max_chunks = (uint32_t)max_chunks_sz;
   RET(wsT(S_MSM_CHUNKS, (size_t)max_chunks * nsides, &chunks));
   RET(wsT(S_MSM_B, (size_t)nbk * MSM_BSPLIT * nsides, &BP));
   RET(wsT(S_MSM_G, (size_t)nbk * MSM_BSPLIT * nsides, &tmp));
@@ -291,10 +327,12 @@ int msm_run(uint32_t R, uint64_t seed, const uint8_t* active, const G2JStore* PA
 // Keyed MSM (msm.h) of the multi-key batch: T = sum_s beta_s sum_{items i of slot s} alpha_{r(i)} S_i.
 // With `test_windows` every key set also gets the MSM_TWIN test windows; *win = the nsets x MSM_WT window
 // sums of the batched subgroup check.
-int msm_run_keyed(const Batch& b, uint64_t seed, const uint8_t* iso, bool test_windows, G2JStore** T, G2JStore** win,
+int msm_run_keyed(const Batch& b, const uint64_t* seed, const uint8_t* iso, bool test_windows, G2JStore** T, G2JStore** win,
                   hipStream_t st) {
   const uint32_t nwin = test_windows ? MSM_WT : MSM_WIN;
-  const uint32_t N = b.R * b.k, nsets = b.nslots, nkeys = nwin * MSM_NB * nsets;
+  const uint32_t N = b.R * b.k, nsets = b.nslots;
+  if ((size_t)nwin * MSM_NB * nsets > 0x7fffffffull) return fail(DG_E_ARG, "too many key sets");
+  const uint32_t nkeys = nwin * MSM_NB * nsets;
   const uint32_t nblocks = (nkeys + KSCAN_B - 1) / KSCAN_B;
   uint32_t *cnt, *tot, *list;
   G2JStore *chunks, *B, *P1, *tmp, *W, *Ts, *BT;
@@ -302,7 +340,10 @@ int msm_run_keyed(const Batch& b, uint64_t seed, const uint8_t* iso, bool test_w
   uint32_t *offset = cnt + nkeys, *cursor = offset + nkeys, *chunk_off = cursor + nkeys;  // chunk_off: nkeys + 1
   RET(wsT(S_KMSM_TOT, (size_t)2 * nblocks, &tot));
   RET(wsT(S_KMSM_LIST, (size_t)nwin * N + 1, &list));
-  const uint32_t max_chunks = (nwin * N) / MSM_CHUNK + 1 + nkeys;  // sum of ceil(count / 8) <= nwin N / 8 + nkeys
+  // sum of ceil(count / 8) <= nwin N / 8 + nkeys
+  const size_t max_chunks_sz = ((size_t)nwin * N) / MSM_CHUNK + 1 + nkeys;
+  if (max_chunks_sz > 0xffffffffull) return fail(DG_E_ARG, "batch too large for the keyed MSM");
+  const uint32_t max_chunks = (uint32_t)max_chunks_sz;
   RET(wsT(S_KMSM_CHUNKS, max_chunks, &chunks));
   RET(wsT(S_KMSM_B, nkeys, &B));
   RET(wsT(S_KMSM_P1, (size_t)nsets * nwin * MSM_C * 16, &P1));
@@ -335,8 +376,11 @@ int msm_run_keyed(const Batch& b, uint64_t seed, const uint8_t* iso, bool test_w
   return 0;
 }
 
-int batch_verify(const Batch& b, uint64_t seed, hipStream_t st) {
+int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
   const uint32_t N = b.R * b.k;
+  uint64_t* d_seed;
+  RET(bind_seed(b, seed_in, st, &d_seed));
+  const uint64_t* seed = d_seed;
   uint8_t *iso, *active;
   uint32_t *cell, *flag;
   G2JStore *U, *V, *A = nullptr, *tmp, *Kp, *msm;
@@ -466,9 +510,10 @@ int decode_key(const uint8_t* pk48_host, hipStream_t st, G1AStore** keys, uint8_
 
 int hash_rounds(uint32_t R, const uint8_t* d_msgs, uint32_t msg_len, hipStream_t st, G2JStore** Q) {
   uint8_t* d_dst;
-  RET(upload(S_DST, kDstNul, kDstNulLen, &d_dst, st));
+  const std::vector<uint8_t>& dst = g_ctx.dst;
+  RET(upload(S_DST, dst.data(), dst.size(), &d_dst, st));
   RET(wsT(S_Q, R, Q));
-  return launch("k_h2c_uncleared", k_h2c_uncleared, R, 128, st, R, d_msgs, msg_len, (const uint8_t*)d_dst, kDstNulLen,
+  return launch("k_h2c_uncleared", k_h2c_uncleared, R, 128, st, R, d_msgs, msg_len, (const uint8_t*)d_dst, (uint32_t)dst.size(),
                 *Q);
 }
 
@@ -482,7 +527,7 @@ int verify_single_key(const uint8_t* pk48_host, uint32_t n, const uint8_t* d_msg
   RET(decode_key(pk48_host, st, &keys, &kst));
   RET(hash_rounds(n, d_msgs, msg_len, st, &Q));
   RET(wsT(S_S, n, &S));
-  Batch b{n, 1, 1, Q, keys, kst, nullptr, d_sigs, 96, 0, S, d_status};
+  Batch b{n, 1, 1, Q, keys, kst, nullptr, d_sigs, 96, 0, S, d_status, d_msgs, msg_len, pk48_host, 48};
   RET(batch_verify(b, seed, st));
   return 0;
 }
@@ -537,18 +582,36 @@ int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const 
                         uint32_t k, const uint8_t* partials98, uint64_t seed, hipStream_t st, uint8_t** d_status,
                         uint8_t** d_partials, G2AStore** d_S, uint32_t prefix_t = 0) {
   const size_t N = (size_t)R * k;
-  // distinct indices (host bookkeeping over the 2-byte index fields only)
+  // Key slots (host bookkeeping over the 2-byte index fields only).  An index enters the batch equation
+  // as its own key set only if it occurs in at least 1/8 of the rounds, and at most kMaxSlots of them
+  // (most frequent first): each set costs an MSM bucket array, a column of the (round, key) cell map and
+  // possibly a correction pairing, so a signer that sends a fresh index every round must not get one
+  // per index.  Items of the other indices are checked on their own (their verdicts stay exact).
+  std::vector<uint32_t> count(65536, 0);
+  for (size_t i = 0; i < N; ++i) ++count[(uint32_t)partials98[98 * i] << 8 | partials98[98 * i + 1]];
+  std::vector<uint32_t> distinct;
+  for (uint32_t idx = 0; idx < 65536; ++idx)
+    if (count[idx]) distinct.push_back(idx);
+  std::stable_sort(distinct.begin(), distinct.end(), [&](uint32_t a, uint32_t b) { return count[a] > count[b]; });
+  constexpr uint32_t kMaxSlots = 1024;
+  uint32_t nslots = 0;
+  while (nslots < distinct.size() && nslots < kMaxSlots && (nslots == 0 || (size_t)count[distinct[nslots]] * 8 >= R))
+    ++nslots;
+  // slots in first-occurrence order within each class (batched, alone), so the usual batch keeps the
+  // input's index order
   std::vector<int32_t> slot_of(65536, -1);
+  std::vector<uint8_t> batched(65536, 0);
+  for (uint32_t q = 0; q < nslots; ++q) batched[distinct[q]] = 1;
   std::vector<uint32_t> slot_idx, item_slot(N);
-  for (size_t i = 0; i < N; ++i) {
-    uint32_t idx = (uint32_t)partials98[98 * i] << 8 | partials98[98 * i + 1];
-    if (slot_of[idx] < 0) {
-      slot_of[idx] = (int32_t)slot_idx.size();
-      slot_idx.push_back(idx);
+  for (int pass = 0; pass < 2; ++pass)
+    for (size_t i = 0; i < N; ++i) {
+      uint32_t idx = (uint32_t)partials98[98 * i] << 8 | partials98[98 * i + 1];
+      if (slot_of[idx] < 0 && batched[idx] == (pass == 0 ? 1 : 0)) {
+        slot_of[idx] = (int32_t)slot_idx.size();
+        slot_idx.push_back(idx);
+      }
     }
-    item_slot[i] = (uint32_t)slot_of[idx];
-  }
-  uint32_t nslots = (uint32_t)slot_idx.size();
+  for (size_t i = 0; i < N; ++i) item_slot[i] = (uint32_t)slot_of[(uint32_t)partials98[98 * i] << 8 | partials98[98 * i + 1]];
   uint8_t *d_m, *d_p, *kst;
   G1AStore* keys;
   uint32_t* d_itemslot;
@@ -560,10 +623,37 @@ int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const 
   RET(hash_rounds(R, d_m, msg_len, st, &Q));
   RET(wsT(S_S, N, d_S));
   RET(wsT(S_STATUS, N, d_status));
-  Batch b{R, k, nslots, Q, keys, kst, d_itemslot, d_p, 98, 2, *d_S, *d_status};
+  Batch b{R, k, nslots, Q, keys, kst, d_itemslot, d_p, 98, 2, *d_S, *d_status, d_m, msg_len, commits48, (size_t)t * 48};
   b.prefix_t = prefix_t;
   RET(batch_verify(b, seed, st));
   *d_partials = d_p;
+  return 0;
+}
+
+// Recover after the VerifyPartial statuses are known (d_st): per round the first t valid partials, xyCommit
+// dedupe, Lagrange terms lambda_j S_j, row sums, compression; results copied to the host buffers.
+int recover_tail(uint32_t R, uint32_t k, uint32_t t, const uint8_t* d_p, const uint8_t* d_st, const G2AStore* d_S,
+                 uint8_t* out_sig96, uint8_t* round_status, uint8_t* share_status, hipStream_t st) {
+  uint8_t *d_rst, *d_sst, *d_out;
+  uint32_t *d_sel, *d_selidx;
+  G2JStore *terms, *tmp;
+  RET(wsT(S_SEL, (size_t)R * t, &d_sel));
+  RET(wsT(S_SELIDX, (size_t)R * t, &d_selidx));
+  RET(wsT(S_RST, R, &d_rst));
+  RET(wsT(S_SST, (size_t)R * k, &d_sst));
+  RET(launch("k_recover_select", k_recover_select, R, 128, st, R, k, t, d_p, d_st, d_sel, d_selidx, d_rst, d_sst));
+  RET(wsT(S_TERMS, (size_t)R * t, &terms));
+  RET(wsT(S_TMP, (size_t)R * t, &tmp));
+  RET(launch("k_recover_terms", k_recover_terms, R * t, 64, st, R, k, t, (const uint32_t*)d_sel,
+             (const uint32_t*)d_selidx, (const uint8_t*)d_rst, d_S, terms));
+  RET(reduce_rows(terms, tmp, R, t, st));
+  RET(wsT(S_OUT0, (size_t)R * 96, &d_out));
+  RET(launch("k_compress_g2", k_compress_g2, R, 128, st, R, (const G2JStore*)terms, (const uint8_t*)d_rst, d_out));
+  HIPCHK(hipMemcpyAsync(out_sig96, d_out, (size_t)R * 96, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(round_status, d_rst, R, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(share_status, d_sst, (size_t)R * k, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (g_ctx.timing) collect_timings();
   return 0;
 }
 
@@ -651,6 +741,25 @@ void dg_shutdown(void) {
 
 const char* dg_last_error(void) { return g_err.c_str(); }
 
+int dg_set_hash_dst(const uint8_t* dst, size_t dst_len) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (dst_len > 255 || (dst_len > 0 && !dst)) return fail(DG_E_ARG, "DST longer than 255 bytes");
+  // batches in flight hash with the DST they were enqueued with (uploaded into their own workspace set)
+  if (dst_len == 0)
+    g_ctx.dst.assign(kDstNul, kDstNul + kDstNulLen);
+  else
+    g_ctx.dst.assign(dst, dst + dst_len);
+  return 0;
+}
+
+int dg_get_hash_dst(uint8_t* out, size_t cap, size_t* len) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!len) return fail(DG_E_ARG, "bad arguments");
+  *len = g_ctx.dst.size();
+  if (out && cap) memcpy(out, g_ctx.dst.data(), cap < g_ctx.dst.size() ? cap : g_ctx.dst.size());
+  return 0;
+}
+
 int dg_device_ready(void) { return g_ctx.ready ? 1 : 0; }
 
 int dg_set_timing(int on) {
@@ -706,12 +815,12 @@ int dg_sign(size_t n, const uint8_t* scalars32, const uint16_t* index, const uin
   uint16_t* d_idx = nullptr;
   RET(upload(S_IN0, scalars32, n * 32, &d_sc, st));
   RET(upload(S_MSGS, msgs, n * msg_len, &d_m, st));
-  RET(upload(S_DST, kDstNul, kDstNulLen, &d_dst, st));
+  RET(upload(S_DST, g_ctx.dst.data(), g_ctx.dst.size(), &d_dst, st));
   if (index) RET(upload(S_IN1, index, n, &d_idx, st));
   size_t rec = index ? 98 : 96;
   RET(wsT(S_OUT0, n * rec, &d_out));
   RET(launch("k_sign", k_sign, (uint32_t)n, 128, st, (uint32_t)n, (const uint8_t*)d_sc, (const uint16_t*)d_idx,
-             (const uint8_t*)d_m, (uint32_t)msg_len, (const uint8_t*)d_dst, kDstNulLen, d_out));
+             (const uint8_t*)d_m, (uint32_t)msg_len, (const uint8_t*)d_dst, (uint32_t)g_ctx.dst.size(), d_out));
   HIPCHK(hipMemcpyAsync(out, d_out, n * rec, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if (g_ctx.timing) collect_timings();
@@ -989,31 +1098,36 @@ int dg_recover(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t ro
   hipStream_t st;
   RET(acquire_set(&st));
   const uint32_t R = (uint32_t)rounds;
-  uint8_t *d_st, *d_p, *d_rst, *d_sst, *d_out;
+  uint8_t *d_st, *d_p;
   G2AStore* d_S;
   RET(verify_partials_dev(commits48, t, R, msgs, (uint32_t)msg_len, k, partials98, fresh_seed(seed), st, &d_st, &d_p,
                           &d_S, t));
-  uint32_t *d_sel, *d_selidx;
-  G2JStore *terms, *tmp;
-  RET(wsT(S_SEL, (size_t)R * t, &d_sel));
-  RET(wsT(S_SELIDX, (size_t)R * t, &d_selidx));
-  RET(wsT(S_RST, R, &d_rst));
-  RET(wsT(S_SST, (size_t)R * k, &d_sst));
-  RET(launch("k_recover_select", k_recover_select, R, 128, st, R, k, t, (const uint8_t*)d_p, (const uint8_t*)d_st,
-             d_sel, d_selidx, d_rst, d_sst));
-  RET(wsT(S_TERMS, (size_t)R * t, &terms));
-  RET(wsT(S_TMP, (size_t)R * t, &tmp));
-  RET(launch("k_recover_terms", k_recover_terms, R * t, 64, st, R, k, t, (const uint32_t*)d_sel,
-             (const uint32_t*)d_selidx, (const uint8_t*)d_rst, (const G2AStore*)d_S, terms));
-  RET(reduce_rows(terms, tmp, R, t, st));
-  RET(wsT(S_OUT0, (size_t)R * 96, &d_out));
-  RET(launch("k_compress_g2", k_compress_g2, R, 128, st, R, (const G2JStore*)terms, (const uint8_t*)d_rst, d_out));
-  HIPCHK(hipMemcpyAsync(out_sig96, d_out, (size_t)R * 96, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(round_status, d_rst, R, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(share_status, d_sst, (size_t)R * k, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  if (g_ctx.timing) collect_timings();
-  return 0;
+  return recover_tail(R, k, t, d_p, d_st, d_S, out_sig96, round_status, share_status, st);
+}
+
+int dg_recover_verified(uint32_t t, uint32_t nshares, size_t rounds, uint32_t k, const uint8_t* partials98,
+                        const uint8_t* verified_status, uint8_t* out_sig96, uint8_t* round_status,
+                        uint8_t* share_status) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  (void)nshares;
+  if (rounds == 0) return 0;
+  if (t == 0 || k == 0 || !partials98 || !verified_status || !out_sig96 || !round_status || !share_status)
+    return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(rounds * (size_t)(k > t ? k : t)));
+  hipStream_t st;
+  RET(acquire_set(&st));
+  const uint32_t R = (uint32_t)rounds;
+  const size_t N = (size_t)R * k;
+  uint8_t *d_p, *d_vst, *d_st;
+  G2AStore* d_S;
+  RET(upload(S_IN1, partials98, N * 98, &d_p, st));
+  RET(upload(S_VST, verified_status, N, &d_vst, st));
+  RET(wsT(S_STATUS, N, &d_st));
+  RET(wsT(S_S, N, &d_S));
+  RET(launch("k_decode_verified", k_decode_verified, (uint32_t)N, 128, st, (uint32_t)N, (const uint8_t*)d_p,
+             (const uint8_t*)d_vst, d_S, d_st));
+  return recover_tail(R, k, t, d_p, d_st, d_S, out_sig96, round_status, share_status, st);
 }
 
 }  // extern "C"

@@ -248,7 +248,8 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_decode_items(uint32_t n, u
   store_g2a(S[i], a);
   status[i] = ok ? DG_ST_OK_ : DG_ST_SIG_DECODE_;
   if (ok) {
-    uint32_t old = atomicExch(&cell[(size_t)(i / k) * nslots + slot], 1u);
+    // a key outside the batch equation (a rare index, drand_gpu.hip verify_partials_dev) is checked alone
+    uint32_t old = slot < nslots ? atomicExch(&cell[(size_t)(i / k) * nslots + slot], 1u) : 1u;
     isolate[i] = old ? 1 : 0;
   }
 }
@@ -261,9 +262,10 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_decode_items(uint32_t n, u
 
 // U_i = beta_slot S_i for batch items, O otherwise
 #if !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_scale_items(uint32_t n, uint32_t nslots, uint64_t seed,
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_scale_items(uint32_t n, uint32_t nslots, const uint64_t* seedp,
                                                     const uint32_t* item_slot, const G2AStore* S,
                                                     const uint8_t* status, const uint8_t* isolate, G2JStore* U) {
+  const uint64_t seed = *seedp;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   G2J u = jac_infinity<Fp2>();
@@ -281,10 +283,11 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_scale_items(uint32_t n, u
 // and C_s = sum of A_r over the active rounds without an item of s (k_key_accum) -- nothing when every
 // share is present in every round
 #if !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_round_combine(uint32_t R, uint32_t k, uint32_t nslots, uint64_t seed,
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_round_combine(uint32_t R, uint32_t k, uint32_t nslots, const uint64_t* seedp,
                                                       const G2JStore* U, const uint8_t* status,
                                                       const uint8_t* isolate, const G2JStore* Q, const uint32_t* cell,
                                                       G2JStore* V, G2JStore* A, uint8_t* active) {
+  const uint64_t seed = *seedp;
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   bool any = false;
@@ -323,8 +326,9 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_key_accum(uint32_t R, uin
 }
 
 // Xc = sum_s beta_s X_s over the key slots with a decoded key: per-lane 64-bit products, LDS tree sum
-DG_KERNEL void __launch_bounds__(256) k_key_combine(uint32_t nslots, uint64_t seed, const G1AStore* keys,
+DG_KERNEL void __launch_bounds__(256) k_key_combine(uint32_t nslots, const uint64_t* seedp, const G1AStore* keys,
                                                    const uint8_t* key_status, G1AStore* out) {
+  const uint64_t seed = *seedp;
   __shared__ G1J part[256];
   const uint32_t t = threadIdx.x;
   G1J acc = jac_infinity<Fp>();
@@ -365,9 +369,10 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_sum_rows(uint32_t rows, u
 // K_s = -C_s and one more pair (Xc, h_eff Kc), Xc = sum_s beta_s X_s: prod_s e(beta_s X_s, h(Kc - C_s)).
 // f[s] = 1 when a side is the identity (every correction pair when all shares are present).
 #if !DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_pair_miller_coop(uint32_t nslots, uint64_t seed, const G1AStore* keys,
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_pair_miller_coop(uint32_t nslots, const uint64_t* seedp, const G1AStore* keys,
                                                          const G2JStore* K, const G2JStore* T, const G1AStore* Xc,
                                                          const G2JStore* Kc, Fp12* f) {
+  const uint64_t seed = *seedp;
   __shared__ CoGT gt;
   __shared__ CoML ml;
   __shared__ CoG2Tmp g2t;
@@ -544,6 +549,76 @@ DG_KERNEL void __launch_bounds__(256) k_any(uint32_t n, const uint8_t* v, uint32
 DG_KERNEL void __launch_bounds__(64) k_count_fallback(const uint32_t* flag, unsigned long long* counter) {
   if (threadIdx.x == 0 && (!flag[0] || flag[1])) atomicAdd(counter, 1ull);
 }
+
+// ---- Binding the batch coefficients to the batch (Fiat-Shamir).  alpha_r, beta_s and the test-window
+// digits of the batched subgroup check are keyed by seed' = SHA-256(seed0 || D)[0..8), where seed0 =
+// SHA-256(BE64 seed || key bytes) (host) and D is a SHA-256 tree over every item (message and signature
+// record).  A caller-known seed therefore does not let anyone choose items whose errors cancel in the
+// batch equation: changing any item changes every coefficient.
+// d_i = SHA-256(BE32 i || msg_{i / k} || record_i), record_i = the `stride` bytes at recs + stride * i
+DG_KERNEL void __launch_bounds__(128) k_digest_items(uint32_t n, uint32_t k, const uint8_t* msgs, uint32_t msg_len,
+                                                     const uint8_t* recs, uint32_t stride, uint8_t* out32) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Sha256 s;
+  sha256_init(s);
+  for (int b = 3; b >= 0; --b) sha256_byte(s, (uint8_t)(i >> (8 * b)));
+  sha256_update(s, msgs + (size_t)msg_len * (i / k), msg_len);
+  sha256_update(s, recs + (size_t)stride * i, stride);
+  sha256_final(s, out32 + 32ull * i);
+}
+// one tree level: out_j = SHA-256(in_{64 j} || ... || in_{min(64 j + 63, n - 1)}) (32 B digests, word-wise:
+// two digests per block, then the padding)
+DGI uint32_t ld_be32(const uint8_t* p) {
+  return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+}
+DG_KERNEL void __launch_bounds__(128) k_digest_level(uint32_t n, const uint8_t* in32, uint8_t* out32) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t a = 64 * j;
+  if (a >= n) return;
+  uint32_t b = a + 64 < n ? a + 64 : n;
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint32_t w[16];
+  uint32_t q = a;
+  for (; q + 1 < b; q += 2) {
+    const uint8_t* p = in32 + 32ull * q;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w[t] = ld_be32(p + 4 * t);
+    sha256_compress(h, w);
+  }
+  const bool odd = q < b;
+  const uint8_t* p = in32 + 32ull * q;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) w[t] = odd ? ld_be32(p + 4 * t) : 0u;
+  w[odd ? 8 : 0] = 0x80000000u;
+#pragma unroll
+  for (int t = 1; t < 15; ++t)
+    if (t != 8) w[t] = (odd && t < 8) ? w[t] : 0u;
+  if (!odd) w[8] = 0u;
+  w[15] = 256u * (b - a);
+  sha256_compress(h, w);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    uint8_t* o = out32 + 32ull * j + 4 * t;
+    o[0] = (uint8_t)(h[t] >> 24);
+    o[1] = (uint8_t)(h[t] >> 16);
+    o[2] = (uint8_t)(h[t] >> 8);
+    o[3] = (uint8_t)h[t];
+  }
+}
+// *seed_out = the first 8 bytes of SHA-256(seed0 || D), forced non-zero
+DG_KERNEL void __launch_bounds__(64) k_digest_seed(const uint8_t* seed0, const uint8_t* d32, uint64_t* seed_out) {
+  if (threadIdx.x != 0) return;
+  Sha256 s;
+  uint8_t d[32];
+  sha256_init(s);
+  sha256_update(s, seed0, 32);
+  sha256_update(s, d32, 32);
+  sha256_final(s, d);
+  uint64_t v = 0;
+  for (int b = 0; b < 8; ++b) v = (v << 8) | d[b];
+  *seed_out = v ? v : 1ull;
+}
 #endif
 
 // ------------------------------------------------------------------ Recover (A6)
@@ -588,6 +663,25 @@ DG_KERNEL void __launch_bounds__(128) k_recover_select(uint32_t R, uint32_t k, u
     ++distinct;
   }
   round_status[r] = distinct >= t ? DG_ST_OK_ : DG_ST_NOT_ENOUGH_;
+}
+#endif
+
+// Recover with known VerifyPartial verdicts (dg_recover_verified, the live round: beacon/beacon.go:148 has
+// already verified every partial the round cache holds, :488 would re-verify them): decode the sigma of
+// the partials whose verdict is OK (already subgroup-checked by that VerifyPartial), carry the others' verdicts
+#if !DG_TU_HOT
+DG_KERNEL void __launch_bounds__(128) k_decode_verified(uint32_t n, const uint8_t* partials, const uint8_t* vst,
+                                                        G2AStore* S, uint8_t* status) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t st = vst[i];
+  G2A a{fp2_zero(), fp2_zero(), true};
+  if (st == DG_ST_OK_ && !g2_decompress(a, partials + 98ull * i + 2, false)) {
+    a = G2A{fp2_zero(), fp2_zero(), true};
+    st = DG_ST_SIG_DECODE_;
+  }
+  store_g2a(S[i], a);
+  status[i] = st;
 }
 #endif
 

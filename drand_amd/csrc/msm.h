@@ -54,8 +54,9 @@ struct MsmDigits {
   }
 };
 
-DG_KERNEL void __launch_bounds__(256) k_msm_count(uint32_t R, uint32_t nwin, uint64_t seed, const uint8_t* active,
+DG_KERNEL void __launch_bounds__(256) k_msm_count(uint32_t R, uint32_t nwin, const uint64_t* seedp, const uint8_t* active,
                                                   uint32_t* count) {
+  const uint64_t seed = *seedp;
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R || !active[r]) return;
   const MsmDigits dg(seed, r, nwin);
@@ -103,8 +104,9 @@ DG_KERNEL void __launch_bounds__(256) k_msm_scan(uint32_t nbk, const uint32_t* c
   }
 }
 
-DG_KERNEL void __launch_bounds__(256) k_msm_scatter(uint32_t R, uint32_t nwin, uint64_t seed, const uint8_t* active,
+DG_KERNEL void __launch_bounds__(256) k_msm_scatter(uint32_t R, uint32_t nwin, const uint64_t* seedp, const uint8_t* active,
                                                     uint32_t* cursor, uint32_t* list) {
+  const uint64_t seed = *seedp;
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R || !active[r]) return;
   const MsmDigits dg(seed, r, nwin);
@@ -274,9 +276,10 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_subgroup(const G2JSto
 constexpr uint32_t KSCAN_B = 1024;  // keys per scan block
 
 
-DG_KERNEL void __launch_bounds__(256) k_kmsm_count(uint32_t N, uint32_t k, uint32_t nsets, uint32_t nwin, uint64_t seed,
+DG_KERNEL void __launch_bounds__(256) k_kmsm_count(uint32_t N, uint32_t k, uint32_t nsets, uint32_t nwin, const uint64_t* seedp,
                                                    const uint32_t* item_slot, const uint8_t* status,
                                                    const uint8_t* isolate, uint32_t* count) {
+  const uint64_t seed = *seedp;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N || status[i] != DG_ST_OK_ || isolate[i]) return;
   const MsmDigits dg(seed, i / k, nwin);
@@ -345,9 +348,10 @@ DG_KERNEL void __launch_bounds__(256) k_kscan_add(uint32_t nkeys, const uint32_t
   chunk_off[i] += tot[nblocks + b];
 }
 
-DG_KERNEL void __launch_bounds__(256) k_kmsm_scatter(uint32_t N, uint32_t k, uint32_t nsets, uint32_t nwin, uint64_t seed,
+DG_KERNEL void __launch_bounds__(256) k_kmsm_scatter(uint32_t N, uint32_t k, uint32_t nsets, uint32_t nwin, const uint64_t* seedp,
                                                      const uint32_t* item_slot, const uint8_t* status,
                                                      const uint8_t* isolate, uint32_t* cursor, uint32_t* list) {
+  const uint64_t seed = *seedp;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N || status[i] != DG_ST_OK_ || isolate[i]) return;
   const MsmDigits dg(seed, i / k, nwin);
@@ -420,7 +424,8 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_slices(uint32_t nset
 
 // one 128-lane workgroup per set s: beta_s T_s by cooperative double-and-add (coop.h; beta is odd, so
 // non-zero)
-DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_kmsm_beta(uint64_t seed, const G2JStore* Tset, G2JStore* out) {
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_kmsm_beta(const uint64_t* seedp, const G2JStore* Tset, G2JStore* out) {
+  const uint64_t seed = *seedp;
   __shared__ CoG2Tmp tmp;
   __shared__ CoG2 acc, p;
   const uint32_t s = blockIdx.x;

@@ -1,6 +1,7 @@
 """Multi-GPU layout of the verify path: one process per GPU, one contiguous round range
-per rank, no data-path collective; the only exchange is the all-gather of per-round verdict bitmaps
-(RCCL over xGMI on the GPU node, gloo in the CPU tests)."""
+per rank, no data-path collective; the only exchange is the all-gather of the per-round results --
+verdict bitmaps (VerifyBeacon), recovered signatures, round statuses and per-share statuses (Recover)
+-- over RCCL/xGMI on the GPU node, gloo in the CPU tests."""
 import ctypes
 import os
 
@@ -55,6 +56,36 @@ def allgather_verdicts(status, world, group=None, m=None):
     parts = [torch.empty(m, dtype=torch.uint8, device=bits.device) for _ in range(world)]
     dist.all_gather(parts, bits, group=group)  # gloo (CPU tests)
     return torch.cat(parts)
+
+
+def allgather_rows(rows, world, total, group=None):
+    """All-gather a rank's contiguous block of per-round records (a (n_rank, w) uint8 tensor, rank r holding
+    rounds round_range(total, world, r)) into the (total, w) array of every round, in round order.
+
+    Shards are padded to the largest one (its size is a function of `total`, so no size exchange and no host
+    round trip); one all_gather_into_tensor on RCCL, list all_gather on gloo.  Used for the Recover outputs:
+    96 B recovered signatures, the round status byte and the k share-status bytes of every round."""
+    import torch
+    import torch.distributed as dist
+
+    if rows.dim() == 1:
+        rows = rows.view(-1, 1)
+    w = rows.shape[1]
+    sizes = [b - a for a, b in (round_range(total, world, q) for q in range(world))]
+    if world == 1:
+        return rows
+    m = max(sizes)
+    if rows.shape[0] < m:
+        rows = torch.cat([rows, torch.zeros((m - rows.shape[0], w), dtype=rows.dtype, device=rows.device)])
+    rows = rows.contiguous()
+    if dist.get_backend(group) == "nccl":  # RCCL on ROCm
+        out = torch.empty((world * m, w), dtype=rows.dtype, device=rows.device)
+        dist.all_gather_into_tensor(out, rows, group=group)
+    else:
+        parts = [torch.empty((m, w), dtype=rows.dtype, device=rows.device) for _ in range(world)]
+        dist.all_gather(parts, rows, group=group)
+        out = torch.cat(parts)
+    return torch.cat([out[q * m:q * m + sizes[q]] for q in range(world)])
 
 
 def unpack_bits(bitmap, sizes):

@@ -140,6 +140,39 @@ def recover_batch(pub: PubPoly, msgs, partials, t, n, seed=0):
     return out, rs, ss
 
 
+def recover_verified_batch(pub: PubPoly, msgs, partials, verified_status, t, n):
+    """The live round's Recover (beacon/beacon.go:472-494) with the VerifyPartial verdicts ProcessBeacon
+    already holds (beacon/beacon.go:148): partials (R, k, 98), verified_status (R, k) DG_ST_* ->
+    (sigs (R, 96), round_status (R,), share_status (R, k)); no pairing is recomputed.  `pub` and `msgs`
+    are what kyber's Recover takes; the verdicts stand in for the re-verification they would feed."""
+    del pub, msgs  # only the re-verification reads them
+    p = L.u8(partials)
+    st_in = np.ascontiguousarray(verified_status, dtype=np.uint8)
+    R = st_in.shape[0]
+    p = p.reshape(R, -1, 98)
+    k = p.shape[1]
+    out = np.zeros((R, 96), dtype=np.uint8)
+    rs = np.zeros(R, dtype=np.uint8)
+    ss = np.zeros((R, k), dtype=np.uint8)
+    L.check(L.lib().dg_recover_verified(t, n, R, k, L.ptr(p), L.ptr(st_in), L.ptr(out), L.ptr(rs), L.ptr(ss)))
+    return out, rs, ss
+
+
+def set_hash_dst(dst=None):
+    """Switch the hash-to-G2 DST of every sign / verify / recover entry point (None: the NUL default)."""
+    d = b"" if dst is None else bytes(dst)
+    L.check(L.lib().dg_set_hash_dst(L.ptr(d) if d else None, len(d)))
+
+
+def hash_dst():
+    import ctypes
+
+    buf = np.zeros(256, np.uint8)
+    n = ctypes.c_size_t()
+    L.check(L.lib().dg_get_hash_dst(L.ptr(buf), 256, ctypes.cast(ctypes.pointer(n), ctypes.c_void_p)))
+    return bytes(buf[:n.value])
+
+
 def _beacon_arrays(prev_rounds, rounds, prev_sigs):
     pr = np.ascontiguousarray(prev_rounds, dtype=np.uint64)
     rr = np.ascontiguousarray(rounds, dtype=np.uint64)

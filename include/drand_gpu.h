@@ -50,6 +50,15 @@ const char* dg_last_error(void);
 /* 1 if the library runs on a gfx950 device after dg_init, else 0 */
 int dg_device_ready(void);
 
+/* The hash-to-G2 domain-separation tag of every signing / verifying entry point (dg_sign, dg_verify*,
+ * dg_verify_partials, dg_recover).  The suite's hash lives in github.com/drand/bls12-381 v0.2.0 (key/curve.go:4,12),
+ * whose DST / draft version no file in the reference pins; it defaults to the RFC 9380
+ * "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_" and a maintainer can switch it at run time, without a rebuild.
+ * dst_len 0 restores the default; at most 255 bytes.  Process-wide; batches already enqueued keep theirs. */
+int dg_set_hash_dst(const uint8_t* dst, size_t dst_len);
+/* The current DST: *len = its length, min(cap, len) bytes copied to out (out may be NULL). */
+int dg_get_hash_dst(uint8_t* out, size_t cap, size_t* len);
+
 /* A9 -- hash-to-G2 (RFC 9380 XMD:SHA-256_SSWU_RO_ with `dst`), compressed 96 B per message.
  * Replaces kyber's hashablePoint.Hash used inside bls.Sign / bls.Verify [UPSTREAM]. */
 int dg_hash_to_g2(size_t n, const uint8_t* msgs, size_t msg_len, const uint8_t* dst, size_t dst_len, uint8_t* out96);
@@ -101,6 +110,16 @@ int dg_verify_partials(const uint8_t* commits48, uint32_t t, size_t rounds, cons
 int dg_recover(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t rounds, const uint8_t* msgs,
                size_t msg_len, uint32_t k, const uint8_t* partials98, uint8_t* out_sig96, uint8_t* round_status,
                uint8_t* share_status, uint64_t seed);
+
+/* A6 on the live round (beacon/beacon.go:472-494): tbls.Recover for partials whose VerifyPartial verdicts the
+ * caller already holds -- ProcessBeacon verified every partial at beacon/beacon.go:148 before the round cache
+ * (beacon/round_cache.go:113-119) kept it, and kyber's Recover (:488) verifies each again.  verified_status[r*k + j]
+ * is that verdict (DG_ST_OK = valid); a non-OK partial is skipped exactly as Recover skips a failing one.
+ * Per round: the first t partials with an OK verdict (input order), deduplicated by index, Lagrange-interpolated
+ * at 0 on G2; no pairing is computed.  Outputs as dg_recover.  The caller vouches for the verdicts. */
+int dg_recover_verified(uint32_t t, uint32_t nshares, size_t rounds, uint32_t k, const uint8_t* partials98,
+                        const uint8_t* verified_status, uint8_t* out_sig96, uint8_t* round_status,
+                        uint8_t* share_status);
 
 /* ---- device-resident variants (bench / multi-GPU path): pointers are device memory on the current
  * device, work is enqueued on `stream` (a hipStream_t; NULL = the library's stream) and completes before

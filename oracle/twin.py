@@ -35,6 +35,9 @@ def lib():
         L.twin_recover.argtypes = [P, c.c_uint32, c.c_uint32, P, c.c_size_t, P, c.c_uint32, P, P]
         L.twin_recover_batch.argtypes = [P, c.c_uint32, c.c_uint32, c.c_size_t, P, P, c.c_uint32, P, P, P, c.c_int]
         L.twin_pairing_cubed.argtypes = [P, P, P]
+        L.twin_set_dst.argtypes = [P, c.c_size_t]
+        L.twin_c1_batch.argtypes = [P, c.c_uint32, c.c_uint32, P, c.c_size_t, P, P, c.c_int]
+        L.twin_c1_batch.restype = c.c_size_t
         L.twin_opcount.restype = c.c_uint64
         L.twin_opcount_enable.argtypes = [c.c_int]
         L.twin_init()
@@ -127,6 +130,25 @@ def recover_batch(commits, t, n, msgs32, partials98, threads=1):
     lib().twin_recover_batch(_buf(cb), t, n, R_, _np_ptr(msgs32), _np_ptr(partials98), k, _np_ptr(out), _np_ptr(rs),
                              _np_ptr(ss), threads)
     return out, rs, ss
+
+
+def set_dst(dst=None):
+    """The DST of twin sign / verify / recover (None: BLS_SIG_..._NUL_)."""
+    if dst is None:
+        lib().twin_set_dst(None, 0)
+    else:
+        lib().twin_set_dst(_buf(dst), len(dst))
+
+
+def c1_batch(commits, t, n, shares, msgs32, threads=1):
+    """BASELINE configs[0] per round: n Signs + Recover + VerifyRecovered -> (sigs (R, 96), rounds verified)."""
+    cb = b"".join(commits)
+    sb = b"".join(int(v).to_bytes(32, "big") for v in shares)
+    msgs32 = np.ascontiguousarray(msgs32, dtype=np.uint8)
+    R_ = msgs32.shape[0]
+    out = np.zeros((R_, 96), dtype=np.uint8)
+    ok = lib().twin_c1_batch(_buf(cb), t, n, _buf(sb), R_, _np_ptr(msgs32), _np_ptr(out), threads)
+    return out, int(ok)
 
 
 def pairing_cubed(g1_48, g2_96):

@@ -941,6 +941,18 @@ static void hash_to_g2_point(g2j* out, const uint8_t* msg, size_t msg_len, const
 }
 static const uint8_t DST_NUL[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_";
 #define DST_NUL_LEN 43
+/* the hash-to-G2 DST of sign / verify (the one unpinned parameter of the suite):
+ * NUL by default, switchable with twin_set_dst like the library's dg_set_hash_dst */
+static uint8_t g_dst[255];
+static size_t g_dst_len = 0;
+static const uint8_t* cur_dst(size_t* len) {
+  if (g_dst_len == 0) {
+    *len = DST_NUL_LEN;
+    return DST_NUL;
+  }
+  *len = g_dst_len;
+  return g_dst;
+}
 
 /* ------------------------------------------------------------------------------------------ pairing */
 typedef struct { fp2 x, y, z; } g2p; /* homogeneous projective */
@@ -1299,14 +1311,18 @@ void twin_sign(const uint8_t sk32[32], const uint8_t* msg, size_t msg_len, uint8
   scalar_from_be32(k, sk32);
   fr_reduce(k);
   g2j h, s;
-  hash_to_g2_point(&h, msg, msg_len, DST_NUL, DST_NUL_LEN);
+  size_t dl;
+  const uint8_t* dst = cur_dst(&dl);
+  hash_to_g2_point(&h, msg, msg_len, dst, dl);
   g2_mul(&s, &h, k, 4);
   g2_compress(out96, &s);
 }
 static int verify_point(const g1j* pk, const uint8_t* msg, size_t msg_len, const uint8_t sig96[96]) {
   g2j s, h;
   if (!g2_decompress(&s, sig96)) return 2;
-  hash_to_g2_point(&h, msg, msg_len, DST_NUL, DST_NUL_LEN);
+  size_t dl;
+  const uint8_t* dst = cur_dst(&dl);
+  hash_to_g2_point(&h, msg, msg_len, dst, dl);
   /* e(pk, H) * e(-g1, sig) == 1 */
   fp px[2], py[2];
   fp2 qx[2], qy[2];
@@ -1551,6 +1567,61 @@ int twin_pairing_cubed(const uint8_t g1_48[48], const uint8_t g2_96[96], uint8_t
     fp_to_be(out576 + 96 * i + 48, &slots[i]->c1);
   }
   return 0;
+}
+int twin_set_dst(const uint8_t* dst, size_t dst_len) {
+  if (dst_len > 255) return -1;
+  if (dst == NULL || dst_len == 0) {
+    g_dst_len = 0;
+    return 0;
+  }
+  memcpy(g_dst, dst, dst_len);
+  g_dst_len = dst_len;
+  return 0;
+}
+typedef struct {
+  const uint8_t *commits, *shares, *msgs;
+  uint32_t t, n;
+  uint8_t* out;
+  size_t lo, hi, ok;
+} c1job;
+static void* c1_worker(void* arg) {
+  c1job* j = (c1job*)arg;
+  uint8_t* parts = (uint8_t*)malloc(98 * (size_t)j->n);
+  uint8_t* ss = (uint8_t*)malloc(j->n);
+  for (size_t r = j->lo; r < j->hi; ++r) {
+    const uint8_t* msg = j->msgs + 32 * r;
+    for (uint32_t i = 0; i < j->n; ++i) { /* tbls.Sign of every node (beacon/beacon.go:433) */
+      parts[98 * i] = (uint8_t)(i >> 8);
+      parts[98 * i + 1] = (uint8_t)i;
+      twin_sign(j->shares + 32 * i, msg, 32, parts + 98 * i + 2);
+    }
+    /* Recover (beacon/beacon.go:488) then VerifyRecovered against pub.Commit() (:494) */
+    if (twin_recover(j->commits, j->t, j->n, msg, 32, parts, j->n, j->out + 96 * r, ss) == 0 &&
+        twin_verify(j->commits, msg, 32, j->out + 96 * r) == 0)
+      ++j->ok;
+  }
+  free(parts);
+  free(ss);
+  return NULL;
+}
+size_t twin_c1_batch(const uint8_t* commits48, uint32_t t, uint32_t n, const uint8_t* shares32, size_t rounds,
+                     const uint8_t* msgs32, uint8_t* out96, int threads) {
+  twin_init();
+  if (threads < 1) threads = 1;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+  c1job* jobs = (c1job*)malloc(sizeof(c1job) * threads);
+  for (int q = 0; q < threads; ++q) {
+    jobs[q] = (c1job){commits48, shares32, msgs32, t, n, out96, rounds * q / threads, rounds * (q + 1) / threads, 0};
+    pthread_create(&th[q], NULL, c1_worker, &jobs[q]);
+  }
+  size_t ok = 0;
+  for (int q = 0; q < threads; ++q) {
+    pthread_join(th[q], NULL);
+    ok += jobs[q].ok;
+  }
+  free(th);
+  free(jobs);
+  return ok;
 }
 void twin_opcount_reset(void) { g_count = 0; }
 uint64_t twin_opcount(void) { return g_count; }

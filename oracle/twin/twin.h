@@ -52,6 +52,13 @@ void twin_recover_batch(const uint8_t* commits48, uint32_t t, uint32_t n, size_t
 /* Full pairing e(P, Q) cubed (the twin's final exponentiation computes f^(3(p^12-1)/r)), as 12 Fp2
  * coefficients c[i] (tower slot i = c0.c0,c0.c1,c0.c2,c1.c0,c1.c1,c1.c2), each Fp2 as c0||c1, 48 B BE each. */
 int twin_pairing_cubed(const uint8_t g1_48[48], const uint8_t g2_96[96], uint8_t out576[576]);
+/* The hash-to-G2 DST used by twin_sign / twin_verify* / twin_recover* (NULL or 0 length: the NUL DST). */
+int twin_set_dst(const uint8_t* dst, size_t dst_len);
+/* BASELINE configs[0] (C1, beacon/beacon_test.go:41-93) per round: n tbls.Sign partials (share i has index i,
+ * shares32 = n x 32 B), Recover over them, VerifyRecovered of the result against commits48[0]; returns the
+ * number of rounds that recovered and verified. */
+size_t twin_c1_batch(const uint8_t* commits48, uint32_t t, uint32_t n, const uint8_t* shares32, size_t rounds,
+                     const uint8_t* msgs32, uint8_t* out96, int threads);
 /* instrumented op counter: number of Fp Montgomery multiplications (squarings included) since reset */
 void twin_opcount_reset(void);
 uint64_t twin_opcount(void);
