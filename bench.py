@@ -441,6 +441,7 @@ def main():
     ap.add_argument("--c5-rounds", type=int, default=10000, help="C5 rounds (all GPUs); 0 disables")
     ap.add_argument("--sync-rounds", type=int, default=100000, help="0 disables the syncFrom catch-up line")
     ap.add_argument("--no-c1", action="store_true", help="no C1 / live-latency lines")
+    ap.add_argument("--status-bufs", type=int, default=4, help="steps whose verdicts may be in flight")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -499,7 +500,7 @@ def main():
     d_sig = torch.from_numpy(np.ascontiguousarray(sigs)).to(dev)
     # status buffers rotate over the steps in flight (the library itself keeps at most DG_SETS = 4 batches
     # in flight); a buffer is reused once the all-gather that read it has finished
-    nbuf = 3
+    nbuf = args.status_bufs
     d_sts = [torch.full((n,), 99, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
     gathered = [None] * nbuf
     side = torch.cuda.Stream(dev)

@@ -3,6 +3,7 @@
 // runs on the device.  No CPU fallback exists: without a gfx950 device the API returns DG_E_NODEV.
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -72,6 +73,13 @@ struct Ctx {
   bool poly_valid = false;
   // hash-to-G2 DST of sign / verify / recover (dg_set_hash_dst; default the NUL DST)
   std::vector<uint8_t> dst = std::vector<uint8_t>(kDstNul, kDstNul + kDstNulLen);
+  // the DST and its word-wise expand_message_xmd tail, resident on the device (uploaded once per DST, never
+  // inside a batch: a pageable host-to-device copy blocks the host until the stream reaches it, which would
+  // serialise the asynchronous batches)
+  XmdTail xmd;
+  uint8_t* d_dst = nullptr;
+  XmdTail* d_xmd = nullptr;
+  bool dst_dev_valid = false;
 };
 
 std::mutex g_mu;
@@ -95,7 +103,7 @@ enum Slot {
   S_COMMITS, S_COMMITST, S_SLOTIDX, S_ITEMSLOT, S_SEL, S_SELIDX, S_RST, S_SST, S_TERMS, S_IN0, S_IN1, S_IN2, S_IN3,
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
-  S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_COUNT
+  S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -264,18 +272,25 @@ struct Batch {
 // D = a SHA-256 tree over every (message, signature record) of the batch, left on the device.
 int bind_seed(const Batch& b, uint64_t seed, hipStream_t st, uint64_t** d_seed) {
   const uint32_t N = b.R * b.k;
+  static const bool no_bind = getenv("DG_NO_BIND") != nullptr;  // A/B diagnostics of the binding's cost only
+  if (no_bind) {
+    RET(wsT(S_SEED, 16, d_seed));
+    return launch("k_store_seed", k_store_seed, 1, 64, st, seed, *d_seed);
+  }
   Sha256 h;
   sha256_init(h);
   for (int i = 7; i >= 0; --i) sha256_byte(h, (uint8_t)(seed >> (8 * i)));
   sha256_update(h, b.key_bytes, (uint32_t)b.key_len);
   uint8_t seed0[32];
   sha256_final(h, seed0);
-  uint8_t *d0, *d1, *d_s0;
+  // seed0 travels as a kernel argument: a host-to-device copy here would block the host (see ensure_dst)
+  Seed0 s0;
+  for (int i = 0; i < 8; ++i)
+    s0.w[i] = (uint32_t)seed0[4 * i] << 24 | (uint32_t)seed0[4 * i + 1] << 16 | (uint32_t)seed0[4 * i + 2] << 8 | seed0[4 * i + 3];
+  uint8_t *d0, *d1;
   RET(wsT(S_DIG0, (size_t)32 * N, &d0));
   RET(wsT(S_DIG1, (size_t)32 * ((N + 63) / 64) + 64, &d1));
-  RET(wsT(S_SEED, 48, d_seed));
-  d_s0 = (uint8_t*)(*d_seed + 2);
-  HIPCHK(hipMemcpyAsync(d_s0, seed0, 32, hipMemcpyHostToDevice, st));
+  RET(wsT(S_SEED, 16, d_seed));
   RET(launch("k_digest_items", k_digest_items, N, 128, st, N, b.k, b.msgs, b.msg_len, b.sigs, b.stride, d0));
   uint32_t n = N;
   while (n > 1) {
@@ -284,7 +299,7 @@ int bind_seed(const Batch& b, uint64_t seed, hipStream_t st, uint64_t** d_seed) 
     std::swap(d0, d1);
     n = m;
   }
-  return launch("k_digest_seed", k_digest_seed, 1, 64, st, (const uint8_t*)d_s0, (const uint8_t*)d0, *d_seed);
+  return launch("k_digest_seed", k_digest_seed, 1, 64, st, s0, (const uint8_t*)d0, *d_seed);
 }
 
 // Pippenger MSM (msm.h): out[0] = sum_r alpha_r PA_r, out[1] = sum_r alpha_r PB_r (PB may be null),
@@ -508,13 +523,32 @@ int decode_key(const uint8_t* pk48_host, hipStream_t st, G1AStore** keys, uint8_
   return 0;
 }
 
+// The current DST and its expand_message_xmd tail on the device (blocking upload after a DST change: batches
+// in flight keep reading the old bytes until they finish, so they are waited for first).
+int ensure_dst() {
+  Ctx& c = g_ctx;
+  if (c.dst_dev_valid) return 0;
+  for (Set& x : c.sets)
+    if (x.busy) {
+      HIPCHK(hipEventSynchronize(x.done));
+      x.busy = false;
+    }
+  if (!c.d_dst) HIPCHK(hipMalloc(&c.d_dst, 256));
+  if (!c.d_xmd) HIPCHK(hipMalloc(&c.d_xmd, sizeof(XmdTail)));
+  xmd_tail_build(c.xmd, c.dst.data(), (uint32_t)c.dst.size());
+  HIPCHK(hipMemcpy(c.d_dst, c.dst.data(), c.dst.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(c.d_xmd, &c.xmd, sizeof(XmdTail), hipMemcpyHostToDevice));
+  c.dst_dev_valid = true;
+  return 0;
+}
+
 int hash_rounds(uint32_t R, const uint8_t* d_msgs, uint32_t msg_len, hipStream_t st, G2JStore** Q) {
   uint8_t* d_dst;
-  const std::vector<uint8_t>& dst = g_ctx.dst;
-  RET(upload(S_DST, dst.data(), dst.size(), &d_dst, st));
+  RET(ensure_dst());
+  d_dst = g_ctx.d_dst;
   RET(wsT(S_Q, R, Q));
-  return launch("k_h2c_uncleared", k_h2c_uncleared, R, 128, st, R, d_msgs, msg_len, (const uint8_t*)d_dst, (uint32_t)dst.size(),
-                *Q);
+  return launch("k_h2c_uncleared", k_h2c_uncleared, R, 128, st, R, d_msgs, msg_len, (const uint8_t*)d_dst,
+                (uint32_t)g_ctx.dst.size(), (const XmdTail*)g_ctx.d_xmd, *Q);
 }
 
 // bls.Verify batch against one key, everything device-resident
@@ -722,6 +756,11 @@ void dg_shutdown(void) {
   if (g_ctx.pk_raw) (void)hipFree(g_ctx.pk_raw);
   if (g_ctx.pk_ready) (void)hipEventDestroy(g_ctx.pk_ready);
   if (g_ctx.fallbacks) (void)hipFree(g_ctx.fallbacks);
+  if (g_ctx.d_dst) (void)hipFree(g_ctx.d_dst);
+  if (g_ctx.d_xmd) (void)hipFree(g_ctx.d_xmd);
+  g_ctx.d_dst = nullptr;
+  g_ctx.d_xmd = nullptr;
+  g_ctx.dst_dev_valid = false;
   g_ctx.fallbacks = nullptr;
   if (g_ctx.poly_keys) (void)hipFree(g_ctx.poly_keys);
   if (g_ctx.poly_kst) (void)hipFree(g_ctx.poly_kst);
@@ -749,6 +788,7 @@ int dg_set_hash_dst(const uint8_t* dst, size_t dst_len) {
     g_ctx.dst.assign(kDstNul, kDstNul + kDstNulLen);
   else
     g_ctx.dst.assign(dst, dst + dst_len);
+  g_ctx.dst_dev_valid = false;
   return 0;
 }
 
@@ -815,7 +855,8 @@ int dg_sign(size_t n, const uint8_t* scalars32, const uint16_t* index, const uin
   uint16_t* d_idx = nullptr;
   RET(upload(S_IN0, scalars32, n * 32, &d_sc, st));
   RET(upload(S_MSGS, msgs, n * msg_len, &d_m, st));
-  RET(upload(S_DST, g_ctx.dst.data(), g_ctx.dst.size(), &d_dst, st));
+  RET(ensure_dst());
+  d_dst = g_ctx.d_dst;
   if (index) RET(upload(S_IN1, index, n, &d_idx, st));
   size_t rec = index ? 98 : 96;
   RET(wsT(S_OUT0, n * rec, &d_out));

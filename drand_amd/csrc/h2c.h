@@ -151,6 +151,126 @@ DGH void hash_to_field_fp2x2(Fp2 u[2], const uint8_t* msg, uint32_t msg_len, con
   }
 }
 
+// ---- expand_message_xmd for 32-byte messages, word-wise (drand hashes 32 B SHA-256 outputs).  The host
+// builds the message-independent words of every SHA-256 block (xmd_tail_build: the state after b_0's
+// all-zero first block, then the padded DST tails); the device streams 32-bit words with static indices,
+// no byte arrays.  Same bytes as hash_to_field_fp2x2 (RFC 9380 §5.3.1, L = 64, count 2, m 2).
+constexpr int XMD_MAXB = 5;  // SHA-256 blocks per hash for DST lengths up to 255
+struct XmdTail {
+  uint32_t nb0, nbi;                // blocks of b_0 after its zero block; blocks of each b_i
+  uint32_t h_zero[8];               // state after the 64-byte zero block of b_0
+  uint32_t w0[XMD_MAXB * 16];       // b_0's blocks: words 0..7 of the first one are the message
+  uint32_t wi[8][XMD_MAXB * 16];    // b_i's blocks: words 0..7 of the first one are b_0 ^ b_{i-1}
+};
+
+static inline void xmd_tail_build(XmdTail& T, const uint8_t* dst, uint32_t dst_len) {
+  const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint8_t buf[XMD_MAXB * 64 + 64];
+  auto words = [](const uint8_t* b, uint32_t* w, int n) {
+    for (int t = 0; t < n; ++t)
+      w[t] = (uint32_t)b[4 * t] << 24 | (uint32_t)b[4 * t + 1] << 16 | (uint32_t)b[4 * t + 2] << 8 | b[4 * t + 3];
+  };
+  // padded message of `len` bytes already in buf -> number of blocks
+  auto pad = [&](uint32_t len) {
+    uint32_t nb = (len + 9 + 63) / 64;
+    for (uint32_t k = len; k < nb * 64; ++k) buf[k] = 0;
+    buf[len] = 0x80;
+    uint64_t bits = (uint64_t)len * 8;
+    for (int k = 0; k < 8; ++k) buf[nb * 64 - 1 - k] = (uint8_t)(bits >> (8 * k));
+    return nb;
+  };
+  for (int k = 0; k < 8; ++k) T.h_zero[k] = iv[k];
+  uint32_t zw[16] = {0};
+  sha256_compress(T.h_zero, zw);
+  // b_0 = H(Z_pad || msg || I2OSP(256, 2) || I2OSP(0, 1) || DST || I2OSP(len(DST), 1)), after the zero block
+  uint32_t len = 0;
+  for (int k = 0; k < 32; ++k) buf[len++] = 0;  // the message's place
+  buf[len++] = 1;
+  buf[len++] = 0;
+  buf[len++] = 0;
+  for (uint32_t k = 0; k < dst_len; ++k) buf[len++] = dst[k];
+  buf[len++] = (uint8_t)dst_len;
+  // the length field counts the zero block too: pad as if 64 bytes preceded
+  uint32_t nb = (len + 64 + 9 + 63) / 64 - 1;
+  for (uint32_t k = len; k < nb * 64; ++k) buf[k] = 0;
+  buf[len] = 0x80;
+  uint64_t bits = (uint64_t)(len + 64) * 8;
+  for (int k = 0; k < 8; ++k) buf[nb * 64 - 1 - k] = (uint8_t)(bits >> (8 * k));
+  T.nb0 = nb;
+  for (uint32_t k = 0; k < XMD_MAXB * 16; ++k) T.w0[k] = 0;
+  words(buf, T.w0, (int)nb * 16);
+  // b_i = H((b_0 xor b_{i-1}) || I2OSP(i, 1) || DST || I2OSP(len(DST), 1))
+  for (int i = 1; i <= 8; ++i) {
+    len = 0;
+    for (int k = 0; k < 32; ++k) buf[len++] = 0;
+    buf[len++] = (uint8_t)i;
+    for (uint32_t k = 0; k < dst_len; ++k) buf[len++] = dst[k];
+    buf[len++] = (uint8_t)dst_len;
+    nb = pad(len);
+    T.nbi = nb;
+    for (uint32_t k = 0; k < XMD_MAXB * 16; ++k) T.wi[i - 1][k] = 0;
+    words(buf, T.wi[i - 1], (int)nb * 16);
+  }
+}
+
+// nb SHA-256 blocks into h: words 0..7 of the first block from `head`, the rest from the host-built tail
+DGI void xmd_blocks(uint32_t (&h)[8], const uint32_t (&head)[8], const uint32_t* tail, uint32_t nb) {
+  uint32_t w[16];
+  for (uint32_t blk = 0; blk < nb; ++blk) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w[t] = (blk == 0 && t < 8) ? head[t] : tail[blk * 16 + t];
+    sha256_compress(h, w);
+  }
+}
+
+// 64 uniform bytes (big-endian words b_{2e+1} || b_{2e+2}) -> Fp: hi 2^256 + lo mod p, in Montgomery form
+DGI Fp fp_from_words64(const uint32_t (&hi)[8], const uint32_t (&lo)[8]) {
+  Fp a = fp_zero(), b = fp_zero();
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    a.l[k] = hi[7 - k];
+    b.l[k] = lo[7 - k];
+  }
+  return fp_add(fp_mul(a, fp_const(FP_R2_2POW256)), fp_mul(b, fp_const(FP_R2)));
+}
+
+DGH void hash_to_field_xmd32(Fp2 u[2], const uint8_t* msg, const XmdTail* T) {
+  const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint32_t m[8], h[8], b0[8], bp[8], v[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    m[t] = (uint32_t)msg[4 * t] << 24 | (uint32_t)msg[4 * t + 1] << 16 | (uint32_t)msg[4 * t + 2] << 8 | msg[4 * t + 3];
+    h[t] = T->h_zero[t];
+  }
+  xmd_blocks(h, m, T->w0, T->nb0);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    b0[t] = h[t];
+    bp[t] = 0;
+  }
+  Fp e0 = fp_zero(), e1 = fp_zero(), e2 = fp_zero(), e3 = fp_zero();
+#pragma unroll 1
+  for (uint32_t i = 1; i <= 8; ++i) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      v[t] = b0[t] ^ bp[t];  // b_0 xor b_{i-1} (b_0 alone for i = 1: bp = 0)
+      h[t] = iv[t];
+    }
+    xmd_blocks(h, v, T->wi[i - 1], T->nbi);
+    if ((i & 1) == 0) {
+      Fp e = fp_from_words64(bp, h);
+      e0 = fp_sel(i == 2, e0, e);
+      e1 = fp_sel(i == 4, e1, e);
+      e2 = fp_sel(i == 6, e2, e);
+      e3 = fp_sel(i == 8, e3, e);
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) bp[t] = h[t];
+  }
+  u[0] = Fp2{e0, e1};
+  u[1] = Fp2{e2, e3};
+}
+
 // RFC 9380 §6.6.2 simplified SWU onto E2': y^2 = x^3 + A'x + B', A' = 240u, B' = 1012(1+u), Z = -(2+u).
 // One Fp inversion, one Fp sqrt of the norm and one (p-3)/4 exponentiation; the gx2 branch reuses the
 // first norm root through sqrt(norm(gx2)) = norm(u)^3 * 5 * sqrt(-5) * sqrt(-norm(gx1)).

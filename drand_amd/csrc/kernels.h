@@ -135,19 +135,32 @@ DG_KERNEL void __launch_bounds__(128) k_hash_to_g2(uint32_t n, const uint8_t* ms
 }
 #endif
 
-// hash-to-curve without cofactor clearing (RLC path)
+// hash-to-curve without cofactor clearing (RLC path); 32 B messages take the word-wise expand_message_xmd
 #if DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_h2c_uncleared(uint32_t n, const uint8_t* msgs, uint32_t msg_len,
-                                                      const uint8_t* dst, uint32_t dst_len, G2JStore* outQ) {
+                                                      const uint8_t* dst, uint32_t dst_len, const XmdTail* xmd,
+                                                      G2JStore* outQ) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  Fp2 u[2];
+  if (msg_len == 32 && xmd)
+    hash_to_field_xmd32(u, msgs + 32ull * i, xmd);
+  else
+    hash_to_field_fp2x2(u, msgs + (size_t)msg_len * i, msg_len, dst, dst_len);
+  G2J q[2];
+  for (int h = 0; h < 2; ++h) {
+    Fp2 x, y;
+    sswu_g2(x, y, u[h], fp_zero(), false);
+    q[h] = iso_map_g2(x, y);
+  }
   // normalised to Z = 1 (one safegcd inversion): the MSM and the scalar multiplications downstream
   // then use mixed additions
-  store_g2j(outQ[i], jac_from_aff(g2_to_aff(hash_to_g2_uncleared(msgs + (size_t)msg_len * i, msg_len, dst, dst_len))));
+  store_g2j(outQ[i], jac_from_aff(g2_to_aff(jac_add(q[0], q[1]))));
 }
 #else
 DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_h2c_uncleared(uint32_t n, const uint8_t* msgs, uint32_t msg_len,
-                                                      const uint8_t* dst, uint32_t dst_len, G2JStore* outQ);
+                                                      const uint8_t* dst, uint32_t dst_len, const XmdTail* xmd,
+                                                      G2JStore* outQ);
 #endif
 
 // sigma decode + subgroup check (A10)
@@ -550,6 +563,13 @@ DG_KERNEL void __launch_bounds__(64) k_count_fallback(const uint32_t* flag, unsi
   if (threadIdx.x == 0 && (!flag[0] || flag[1])) atomicAdd(counter, 1ull);
 }
 
+struct Seed0 {
+  uint32_t w[8];
+};
+// diagnostics only (DG_NO_BIND=1): the caller's seed as is
+DG_KERNEL void __launch_bounds__(64) k_store_seed(uint64_t seed, uint64_t* out) {
+  if (threadIdx.x == 0) *out = seed;
+}
 // ---- Binding the batch coefficients to the batch (Fiat-Shamir).  alpha_r, beta_s and the test-window
 // digits of the batched subgroup check are keyed by seed' = SHA-256(seed0 || D)[0..8), where seed0 =
 // SHA-256(BE64 seed || key bytes) (host) and D is a SHA-256 tree over every item (message and signature
@@ -606,17 +626,24 @@ DG_KERNEL void __launch_bounds__(128) k_digest_level(uint32_t n, const uint8_t* 
     o[3] = (uint8_t)h[t];
   }
 }
-// *seed_out = the first 8 bytes of SHA-256(seed0 || D), forced non-zero
-DG_KERNEL void __launch_bounds__(64) k_digest_seed(const uint8_t* seed0, const uint8_t* d32, uint64_t* seed_out) {
+// *seed_out = the first 8 bytes of SHA-256(seed0 || D), forced non-zero (seed0 as 8 big-endian words, passed by
+// value; one block of 64 bytes plus the padding block)
+DG_KERNEL void __launch_bounds__(64) k_digest_seed(Seed0 s0, const uint8_t* d32, uint64_t* seed_out) {
   if (threadIdx.x != 0) return;
-  Sha256 s;
-  uint8_t d[32];
-  sha256_init(s);
-  sha256_update(s, seed0, 32);
-  sha256_update(s, d32, 32);
-  sha256_final(s, d);
-  uint64_t v = 0;
-  for (int b = 0; b < 8; ++b) v = (v << 8) | d[b];
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint32_t w[16];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    w[t] = s0.w[t];
+    w[8 + t] = ld_be32(d32 + 4 * t);
+  }
+  sha256_compress(h, w);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) w[t] = 0;
+  w[0] = 0x80000000u;
+  w[15] = 512u;
+  sha256_compress(h, w);
+  const uint64_t v = (uint64_t)h[0] << 32 | h[1];
   *seed_out = v ? v : 1ull;
 }
 #endif

@@ -111,3 +111,14 @@ extern "C" int hc_g2_mul_psi_check(const uint8_t* sig96, const uint32_t* k8) {
   G2J v = jac_mul_u256(jac_from_aff(a), k8);
   return jac_eq(u, v) ? 1 : 0;
 }
+
+// word-wise expand_message_xmd (32 B messages, host-built DST tail) against the byte-wise RFC 9380 path:
+// 1 if the four hash_to_field elements agree
+extern "C" int hc_h2f_xmd32_check(const uint8_t* msg32, const uint8_t* dst, uint32_t dl) {
+  static XmdTail T;
+  xmd_tail_build(T, dst, dl);
+  Fp2 a[2], b[2];
+  hash_to_field_xmd32(a, msg32, &T);
+  hash_to_field_fp2x2(b, msg32, 32, dst, dl);
+  return fp2_eq(a[0], b[0]) && fp2_eq(a[1], b[1]) ? 1 : 0;
+}

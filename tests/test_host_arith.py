@@ -75,3 +75,15 @@ def test_g2_mul_psi_decomposition_host_build(hc):
     for k in ks:
         k8 = (ctypes.c_uint32 * 8)(*[(k >> (32 * w)) & 0xFFFFFFFF for w in range(8)])
         assert hc.hc_g2_mul_psi_check(sig, k8) == 1, hex(k)
+
+
+def test_wordwise_xmd_matches_bytewise(hc):
+    """hash_to_field_xmd32 (k_h2c_uncleared's word-wise expand_message_xmd for 32-byte messages) gives the
+    byte-wise RFC 9380 path's field elements, for DST lengths across every SHA-256 block boundary."""
+    import hashlib
+
+    for dl in (0, 1, 19, 20, 43, 83, 84, 147, 148, 200, 211, 212, 255):
+        dst = bytes((7 * k + dl) % 256 for k in range(dl)) if dl != 43 else b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"
+        for j in range(3):
+            msg = hashlib.sha256(b"xmd/%d/%d" % (dl, j)).digest()
+            assert hc.hc_h2f_xmd32_check(msg, dst, dl) == 1, (dl, j)

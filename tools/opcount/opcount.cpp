@@ -21,9 +21,24 @@ static void take(uint64_t* out) {
 extern "C" {
 // out[0..1] = (mul, sqr) of hash_to_g2_uncleared(msg) -- k_h2c_uncleared per round
 void oc_h2c_uncleared(const uint8_t* msg, uint32_t len, const uint8_t* dst, uint32_t dl, uint64_t* out) {
+  // as k_h2c_uncleared computes one round (word-wise expand_message_xmd for 32 B messages; the two-lane
+  // kernel repeats the final addition and normalisation in both lanes: not counted, the algorithm needs one)
+  static XmdTail T;
+  xmd_tail_build(T, dst, dl);
   reset();
-  G2J q = jac_from_aff(g2_to_aff(hash_to_g2_uncleared(msg, len, dst, dl)));  // as k_h2c_uncleared stores it
-  (void)q;
+  Fp2 u[2];
+  if (len == 32)
+    hash_to_field_xmd32(u, msg, &T);
+  else
+    hash_to_field_fp2x2(u, msg, len, dst, dl);
+  G2J q[2];
+  for (int h = 0; h < 2; ++h) {
+    Fp2 x, y;
+    sswu_g2(x, y, u[h], fp_zero(), false);
+    q[h] = iso_map_g2(x, y);
+  }
+  G2J r = jac_from_aff(g2_to_aff(jac_add(q[0], q[1])));
+  (void)r;
   take(out);
 }
 // g2_decompress (+ subgroup check when `subgroup`: multi-key batches; the beacon path batches it on the
