@@ -95,14 +95,15 @@ def gpu_signed_rounds(lib_tbls, first, n, x):
 
 def roofline_of(kt, kernel_units, peak, extra=None):
     """Roofline object of the dominant kernel of a timing table {name: (avg us, launches)}: the kernel with
-    the largest total time among those profiles/opcounts.json prices; kernel_units[name] = units per launch."""
+    the largest total time among those profiles/opcounts.json prices; kernel_units[name] = the units all its
+    timed launches processed together (per launch: that / launches)."""
     oc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["per_unit"]
     cands = [(us * n, name, us) for name, (us, n) in kt.items() if name in oc and name in kernel_units]
     if not cands:
         return None
     _, name, us = max(cands)
     macs = oc[name]["macs"]
-    units = kernel_units[name]
+    units = kernel_units[name] / kt[name][1]
     achieved = macs * units / (us * 1e-6) / 1e12
     out = {"bound": "valu-int", "achieved": achieved, "peak": peak["tmac_s"], "unit": "TMAC/s",
            "frac": achieved / peak["tmac_s"], "traffic": traffic_of(name), "kernel": name, "kernel_avg_us": us,
@@ -253,9 +254,8 @@ def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps
     tbls.recover_batch(pub, msgs, parts, t, n, seed=9)
     kt = L.timings()
     L.check(L.lib().dg_set_timing(0))
-    units = {"k_decode_items": R * n, "k_recover_terms": R * t, "k_h2c_uncleared": R,
-             "k_kmsm_chunks": None}
-    units = {k: v for k, v in units.items() if v}
+    units = {"k_decode_items": R * n, "k_recover_terms": R * t, "k_h2c_uncleared": R, "k_exp_pm3d4": 4 * R + 2 * R * n,
+             "k_dec_p1": R * n, "k_dec_p2": R * n, "k_dec_p3": R * n}
     roof = roofline_of(kt, units, peak, {"timing": "HIP events on the launch stream, one dg_recover call"})
     out = {"metric": "Recover/s at n=%d t=%d (all %d shares VerifyPartial'd, first t valid interpolated)" % (n, t, n),
            "value": R_total / (dt + gdt), "unit": "recovers/s", "n_gpus": world, "rounds": R_total,
@@ -591,12 +591,18 @@ def main():
     if rank == 0 and kt_iso:
         oc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["per_unit"]
         per = bounds[0][1] - bounds[0][0]
-        roof = roofline_of(kt_iso, {"k_h2c_uncleared": per, "k_decode_items": per}, peak,
+        # units over the two blocking batches: rounds for the fused kernels, exponentiations (4 per round of
+        # hash-to-G2, 2 per signature) for k_exp_pm3d4, map items / items for the phases
+        nb2 = 2 * per
+        units = {"k_h2c_uncleared": nb2, "k_decode_items": nb2, "k_exp_pm3d4": 6 * nb2, "k_h2c_p1": nb2,
+                 "k_h2c_p2": 2 * nb2, "k_h2c_p3": 2 * nb2, "k_h2c_p4": nb2, "k_dec_p1": nb2, "k_dec_p2": nb2,
+                 "k_dec_p3": nb2}
+        roof = roofline_of(kt_iso, units, peak,
                            {"timing": "HIP events on the launch stream, blocking batches right after the timed "
                                       "region (the kernel alone on the chip)"})
         if roof and roof["kernel"] in kt:
             o_us = kt[roof["kernel"]][0]
-            a_o = roof["macs_per_unit"] * per / (o_us * 1e-6) / 1e12
+            a_o = roof["macs_per_unit"] * roof["units_per_launch"] / (o_us * 1e-6) / 1e12
             roof["overlapped"] = {"kernel_avg_us": o_us, "achieved": a_o, "frac": a_o / peak["tmac_s"],
                                   "note": "instrumented replay of the timed region: the launch shares the chip "
                                           "with the other batches in flight"}
@@ -606,6 +612,11 @@ def main():
             # Z = 1) over the step time; per-batch fixed work not counted
             per_round = (sum(oc[k]["macs"] for k in ("k_h2c_uncleared", "k_decode_items")) +
                          26 * oc["k_msm_chunks[mixed add]"]["macs"])
+            if "k_h2c_p1" in kt_iso:  # the phase kernels (same algorithm, one inversion fewer per round)
+                per_round = (6 * oc["k_exp_pm3d4"]["macs"] + oc["k_h2c_p1"]["macs"] + 2 * oc["k_h2c_p2"]["macs"] +
+                             2 * oc["k_h2c_p3"]["macs"] + oc["k_h2c_p4"]["macs"] +
+                             sum(oc[k]["macs"] for k in ("k_dec_p1", "k_dec_p2", "k_dec_p3")) +
+                             26 * oc["k_msm_chunks[mixed add]"]["macs"])
             chip = per_round * G * args.steps / world / dt / 1e12
             roof["chip"] = {"macs_per_round": per_round, "achieved": chip, "frac": chip / peak["tmac_s"],
                             "note": "per GPU"}

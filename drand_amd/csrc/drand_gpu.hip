@@ -80,6 +80,9 @@ struct Ctx {
   uint8_t* d_dst = nullptr;
   XmdTail* d_xmd = nullptr;
   bool dst_dev_valid = false;
+  // hash-to-G2 and sigma decode as the phase kernels of phases.h (default) or the fused one-lane kernels
+  // (DG_FUSED=1: A/B only)
+  bool phased = getenv("DG_FUSED") == nullptr;
 };
 
 std::mutex g_mu;
@@ -103,7 +106,7 @@ enum Slot {
   S_COMMITS, S_COMMITST, S_SLOTIDX, S_ITEMSLOT, S_SEL, S_SELIDX, S_RST, S_SST, S_TERMS, S_IN0, S_IN1, S_IN2, S_IN3,
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
-  S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_COUNT
+  S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -416,8 +419,24 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
   // one item per (round, key): the G2 subgroup checks of the signatures are batched on the MSM's window
   // sums (msm.h) instead of a psi check per item (several items of one key in a round share their digits)
   const uint32_t batched_sub = (b.nslots > 1 || b.k == 1) ? 1u : 0u;
-  RET(launch("k_decode_items", k_decode_items, N, 128, st, N, b.k, b.nslots, b.sigs, b.stride, b.offset, b.item_slot,
-             b.key_status, b.S, b.status, cell, iso, 1u - batched_sub));
+  if (g_ctx.phased) {
+    // phases.h: flags / x, the two roots through k_exp_pm3d4, then y, sign and the cell claim
+    DecState* ds;
+    Fp *ein, *eout;
+    RET(wsT(S_DECST, N, &ds));
+    RET(wsT(S_DEIN, N, &ein));
+    RET(wsT(S_DEOUT, N, &eout));
+    RET(launch("k_dec_p1", k_dec_p1, N, 128, st, N, b.sigs, b.stride, b.offset, b.item_slot, b.key_status, ds, ein,
+               b.status));
+    RET(launch("k_exp_pm3d4", k_exp_pm3d4, N, 128, st, N, (const Fp*)ein, eout));
+    RET(launch("k_dec_p2", k_dec_p2, N, 128, st, N, ds, ein, (const Fp*)eout, b.status));
+    RET(launch("k_exp_pm3d4", k_exp_pm3d4, N, 128, st, N, (const Fp*)ein, eout));
+    RET(launch("k_dec_p3", k_dec_p3, N, 128, st, N, b.k, b.nslots, b.item_slot, (const DecState*)ds, (const Fp*)ein,
+               (const Fp*)eout, b.S, b.status, cell, iso, 1u - batched_sub));
+  } else {
+    RET(launch("k_decode_items", k_decode_items, N, 128, st, N, b.k, b.nslots, b.sigs, b.stride, b.offset,
+               b.item_slot, b.key_status, b.S, b.status, cell, iso, 1u - batched_sub));
+  }
   if (b.nslots == 1)
     RET(launch("k_scale_items", k_scale_items, N, 128, st, N, b.nslots, seed, b.item_slot, (const G2AStore*)b.S,
                (const uint8_t*)b.status, (const uint8_t*)iso, U));
@@ -547,8 +566,25 @@ int hash_rounds(uint32_t R, const uint8_t* d_msgs, uint32_t msg_len, hipStream_t
   RET(ensure_dst());
   d_dst = g_ctx.d_dst;
   RET(wsT(S_Q, R, Q));
-  return launch("k_h2c_uncleared", k_h2c_uncleared, R, 128, st, R, d_msgs, msg_len, (const uint8_t*)d_dst,
-                (uint32_t)g_ctx.dst.size(), (const XmdTail*)g_ctx.d_xmd, *Q);
+  if (!g_ctx.phased)
+    return launch("k_h2c_uncleared", k_h2c_uncleared, R, 128, st, R, d_msgs, msg_len, (const uint8_t*)d_dst,
+                  (uint32_t)g_ctx.dst.size(), (const XmdTail*)g_ctx.d_xmd, *Q);
+  // phases.h: two maps per round, every exponentiation through k_exp_pm3d4
+  const uint32_t M = 2 * R;
+  H2cMap* hs;
+  Fp *ein, *eout;
+  G2JStore* iso;
+  RET(wsT(S_H2CST, M, &hs));
+  RET(wsT(S_EIN, M, &ein));
+  RET(wsT(S_EOUT, M, &eout));
+  RET(wsT(S_ISOPT, M, &iso));
+  RET(launch("k_h2c_p1", k_h2c_p1, R, 128, st, R, d_msgs, msg_len, (const uint8_t*)d_dst, (uint32_t)g_ctx.dst.size(),
+             (const XmdTail*)g_ctx.d_xmd, hs, ein));
+  RET(launch("k_exp_pm3d4", k_exp_pm3d4, M, 128, st, M, (const Fp*)ein, eout));
+  RET(launch("k_h2c_p2", k_h2c_p2, M, 128, st, M, hs, ein, (const Fp*)eout));
+  RET(launch("k_exp_pm3d4", k_exp_pm3d4, M, 128, st, M, (const Fp*)ein, eout));
+  RET(launch("k_h2c_p3", k_h2c_p3, M, 128, st, M, (const H2cMap*)hs, (const Fp*)ein, (const Fp*)eout, iso));
+  return launch("k_h2c_p4", k_h2c_p4, R, 128, st, R, (const G2JStore*)iso, *Q);
 }
 
 // bls.Verify batch against one key, everything device-resident

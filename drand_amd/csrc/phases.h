@@ -1,0 +1,324 @@
+// Phase kernels of hash-to-G2 (A9) and sigma decompression (A10).
+//
+// Both are dominated by Fp exponentiations x^((p-3)/4): four per round in hash-to-G2 (two per simplified
+// SWU map: the norm root and the root of (g0 + s)/2), two per item in the decompression.  Fused into one
+// lane-per-item kernel, the exponentiation chain shares the register file with everything else the item
+// keeps live (the SWU / isogeny state, the SHA-256 expansion, the Fp2 tower temporaries), the kernel sits
+// at 256 VGPRs with ~2 KB of scratch per lane, and at 100k rounds 1563 waves leave half the SIMDs with one
+// wave.  Here each item runs as a pipeline of short kernels whose state lives in HBM between them (a few
+// hundred bytes per item, microseconds of traffic against milliseconds of arithmetic), and every
+// exponentiation of the batch -- both maps of every round, both roots of every signature -- goes through
+// one register-lean kernel, k_exp_pm3d4 (SOS products in the radix-2^28 digit form, no calls, no scratch).
+//
+//   hash-to-G2 (per batch of R rounds, M = 2R map items):
+//     k_h2c_p1  (R)  expand_message_xmd, both u_h; x1 = -B/A (1 + 1/den) with ONE inversion for both
+//                    maps (Montgomery's trick); gx1; exponent input norm(gx1)
+//     k_exp     (M)  t = norm(gx1)^((p-3)/4)
+//     k_h2c_p2  (M)  s1 = t n1, square test, x / g / s of the chosen branch; input c of the second root
+//     k_exp     (M)  t2 = c^((p-3)/4)
+//     k_h2c_p3  (M)  y = sqrt(g) from c, t2 (checked; the full root as a fallback), sgn0 fix, 3-isogeny
+//     k_h2c_p4  (R)  q0 + q1, normalised to Z = 1 (one safegcd inversion)
+//   sigma decompression (per batch of N items):
+//     k_dec_p1  (N)  flags, canonical x, rhs = x^3 + 4(1+u); exponent input norm(rhs)
+//     k_exp     (N)
+//     k_dec_p2  (N)  norm root (not a square: not on the curve), input c of the second root
+//     k_exp     (N)
+//     k_dec_p3  (N)  y, sign flag, optional subgroup check, (round, key) cell claim
+// Every value is the one the fused code (h2c.h sswu_g2 / iso_map_g2, curve.h g2_decompress) computes: the
+// square roots are unique up to sign and the sign is fixed by sgn0 / the flag bit.
+#pragma once
+
+namespace dg {
+
+struct H2cMap {
+  Fp2 u, x, g;  // field element, x-coordinate and g(x) on E2' of one simplified-SWU map
+};
+struct DecState {
+  Fp2 x, g;        // x and rhs = x^3 + b'
+  uint32_t flags;  // DEC_* below
+  uint32_t pad[3];
+};
+constexpr uint32_t DEC_PENDING = 1, DEC_SIGN = 2, DEC_INF = 4;
+
+// ------------------------------------------------------------------------------ exponentiation
+// x^((p-3)/4) by the width-3 sliding-window schedule of field.h, SOS products in the digit form
+DGI Fp fp_pow_pm3d4_sos(const Fp& x) {
+  uint32_t t0[14], t1[14], t2[14], t3[14], x2[14], acc[14], nxt[14], m[14];
+  fp28_unpack(x.l, t0);
+  fp28_sos_sqr_d(t0, x2);
+  fp28_sos_mul_d(t0, x2, t1);
+  fp28_sos_mul_d(t1, x2, t2);
+  fp28_sos_mul_d(t2, x2, t3);
+  DG_COUNT_SQR();
+  DG_COUNT_MUL();
+  DG_COUNT_MUL();
+  DG_COUNT_MUL();
+  const int first = EXP_PM3D4_FIRST;
+#pragma unroll
+  for (int d = 0; d < 14; ++d) acc[d] = first == 0 ? t0[d] : first == 1 ? t1[d] : first == 2 ? t2[d] : t3[d];
+  for (int s = 0; s < EXP_PM3D4_NSTEPS; ++s) {
+    const int k = EXP_PM3D4_STEPS[s][0];
+    const int idx = EXP_PM3D4_STEPS[s][1];
+    for (int j = 0; j < k; ++j) {
+      DG_COUNT_SQR();
+      fp28_sos_sqr_d(acc, nxt);
+#pragma unroll
+      for (int d = 0; d < 14; ++d) acc[d] = nxt[d];
+    }
+    if (idx >= 0) {
+#pragma unroll
+      for (int d = 0; d < 14; ++d) m[d] = idx == 0 ? t0[d] : idx == 1 ? t1[d] : idx == 2 ? t2[d] : t3[d];
+      DG_COUNT_MUL();
+      fp28_sos_mul_d(acc, m, nxt);
+#pragma unroll
+      for (int d = 0; d < 14; ++d) acc[d] = nxt[d];
+    }
+  }
+  Fp r;
+  fp28_pack(acc, r.l);
+  return fp_reduce_once(r);
+}
+
+// ------------------------------------------------------------------------------ shared square-root tail
+// The second half of the Fp2 square root of fp2_sqrt_with_norm_root (field.h): c = (a0 + s)/2 (or a0 when
+// a1 = 0, which makes the same formula return sqrt(a0) or sqrt(-a0) u), t = c^((p-3)/4).  Returns whether
+// r^2 == a.
+DGI Fp sqrt_c_input(const Fp2& a, const Fp& s) {
+  return fp_is_zero(a.c1) ? a.c0 : fp_mul(fp_add(a.c0, s), fp_const(FP_TWO_INV));
+}
+DGI bool sqrt_finish(Fp2& r, const Fp2& a, const Fp& c, const Fp& t) {
+  Fp ct = fp_mul(c, t);
+  Fp at2 = fp_mul(fp_mul(a.c1, t), fp_const(FP_TWO_INV));
+  bool c_square = fp_eq(fp_mul(ct, t), fp_one());
+  r = Fp2{fp_sel(c_square, at2, ct), fp_sel(c_square, fp_neg(ct), at2)};
+  return fp2_eq(fp2_sqr(r), a);
+}
+
+// rare paths kept out of line so their exponentiations do not inflate the phase kernels' registers
+DGN bool fp2_sqrt_slow(Fp2& r, const Fp2& a) { return fp2_sqrt(r, a); }
+DGN bool g2_in_subgroup_slow(const Fp2& x, const Fp2& y) { return g2_in_subgroup_aff(x, y); }
+
+// ------------------------------------------------------------------------------ hash-to-G2 phases
+// P1 of round r: both maps' x1, gx1 and the first exponent inputs norm(gx1)
+DGI void h2c_p1(const Fp2 (&u)[2], H2cMap (&st)[2], Fp (&ein)[2]) {
+  const Fp2 A = fp2_const(SSWU_A), B = fp2_const(SSWU_B), Z = fp2_const(SSWU_Z);
+  Fp2 den[2], d[2];
+  bool zero[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    Fp2 zu2 = fp2_mul(Z, fp2_sqr(u[h]));
+    den[h] = fp2_add(fp2_sqr(zu2), zu2);
+    zero[h] = fp2_is_zero(den[h]);
+    d[h] = zero[h] ? fp2_one() : den[h];
+  }
+  // 1/den_0 and 1/den_1 from one inversion of the product
+  Fp2 inv = fp2_inv(fp2_mul(d[0], d[1]));
+  Fp2 inv_h[2] = {fp2_mul(inv, d[1]), fp2_mul(inv, d[0])};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    Fp2 x1 = zero[h] ? fp2_const(SSWU_B_OVER_ZA) : fp2_mul(fp2_const(SSWU_MINUS_B_OVER_A), fp2_add(fp2_one(), inv_h[h]));
+    Fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), A), x1), B);
+    st[h] = H2cMap{u[h], x1, gx1};
+    ein[h] = fp2_norm(gx1);
+  }
+}
+// P2 of one map: t = n1^((p-3)/4); the branch of sswu_g2 (h2c.h) and the input c of the second root
+DGI void h2c_p2(H2cMap& st, const Fp& n1, const Fp& t, Fp& c) {
+  const Fp2 A = fp2_const(SSWU_A), B = fp2_const(SSWU_B), Z = fp2_const(SSWU_Z);
+  Fp s1 = fp_mul(t, n1);  // n1^((p+1)/4)
+  bool sq1 = fp_eq(fp_sqr(s1), n1);
+  Fp s = s1;
+  if (!sq1) {
+    Fp2 zu2 = fp2_mul(Z, fp2_sqr(st.u));
+    st.x = fp2_mul(zu2, st.x);
+    st.g = fp2_add(fp2_mul(fp2_add(fp2_sqr(st.x), A), st.x), B);
+    // s1^2 = -n1 ; norm(gx2) = 5^3 norm(u)^6 n1 ; sqrt = norm(u)^3 * 5 * sqrt(-5) * s1
+    Fp nu = fp2_norm(st.u);
+    Fp nu3 = fp_mul(fp_sqr(nu), nu);
+    s = fp_mul(fp_mul(nu3, fp_small(5)), fp_mul(fp_const(FP_SQRT_MINUS5), s1));
+  }
+  c = sqrt_c_input(st.g, s);
+}
+// P3 of one map: y = sqrt(g), its sign by sgn0(u), then the 3-isogeny (Jacobian, no inversion)
+DGI G2J h2c_p3(const H2cMap& st, const Fp& c, const Fp& t) {
+  Fp2 y;
+  if (!sqrt_finish(y, st.g, c, t)) fp2_sqrt_slow(y, st.g);  // never taken for a square g
+  if (fp2_sgn0(st.u) != fp2_sgn0(y)) y = fp2_neg(y);
+  return iso_map_g2(st.x, y);
+}
+
+// ------------------------------------------------------------------------------ decompression phases
+// P1: flags and x of a 96 B encoding; returns the status; exponent input norm(x^3 + b')
+DGI uint8_t dec_p1(const uint8_t* in, DecState& ds, Fp& ein) {
+  ds.flags = 0;
+  ein = fp_zero();
+  const uint8_t f = in[0];
+  if (!(f & 0x80)) return 2;
+  if (f & 0x40) {
+    if (f != 0xc0) return 2;
+    uint32_t o = 0;
+    for (int i = 1; i < 96; ++i) o |= in[i];
+    if (o) return 2;
+    ds.flags = DEC_INF;
+    return 0;
+  }
+  uint8_t b[48];
+  for (int i = 0; i < 48; ++i) b[i] = in[i];
+  b[0] &= 0x1f;
+  Fp x1, x0;
+  if (!fp_from_be48_plain(x1, b)) return 2;
+  if (!fp_from_be48_plain(x0, in + 48)) return 2;
+  ds.x = Fp2{fp_to_mont(x0), fp_to_mont(x1)};
+  ds.g = fp2_add(fp2_mul(fp2_sqr(ds.x), ds.x), fp2_const(FP2_B_G2));
+  ds.flags = DEC_PENDING | ((f & 0x20) ? DEC_SIGN : 0u);
+  ein = fp2_norm(ds.g);
+  return 0;
+}
+// P2: the norm root; false when rhs is not a square (x is not on the curve); the second exponent input
+DGI bool dec_p2(const DecState& ds, const Fp& n, const Fp& t, Fp& c) {
+  Fp s = fp_mul(t, n);
+  if (!fp_eq(fp_sqr(s), n)) return false;
+  c = sqrt_c_input(ds.g, s);
+  return true;
+}
+// P3: y and its sign; false if no root (never for a square rhs) or outside G2 when `subgroup`
+DGI bool dec_p3(const DecState& ds, const Fp& c, const Fp& t, bool subgroup, G2A& out) {
+  Fp2 y;
+  if (!sqrt_finish(y, ds.g, c, t) && !fp2_sqrt_slow(y, ds.g)) return false;
+  if (((ds.flags & DEC_SIGN) != 0) != fp2_lex_largest(y)) y = fp2_neg(y);
+  out = G2A{ds.x, y, false};
+  if (subgroup && !g2_in_subgroup_slow(ds.x, y)) return false;
+  return true;
+}
+
+#if defined(__HIP__)
+#ifndef DG_EXP_WAVES
+#define DG_EXP_WAVES 2
+#endif
+#if DG_TU_HOT
+DG_KERNEL void __launch_bounds__(128, DG_EXP_WAVES) k_exp_pm3d4(uint32_t n, const Fp* in, Fp* out) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = fp_pow_pm3d4_sos(in[i]);
+}
+
+DG_KERNEL void __launch_bounds__(128) k_h2c_p1(uint32_t R, const uint8_t* msgs, uint32_t msg_len, const uint8_t* dst,
+                                               uint32_t dst_len, const XmdTail* xmd, H2cMap* st, Fp* ein) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  Fp2 u[2];
+  if (msg_len == 32 && xmd)
+    hash_to_field_xmd32(u, msgs + 32ull * r, xmd);
+  else
+    hash_to_field_fp2x2(u, msgs + (size_t)msg_len * r, msg_len, dst, dst_len);
+  H2cMap s[2];
+  Fp e[2];
+  h2c_p1(u, s, e);
+  st[2 * r] = s[0];
+  st[2 * r + 1] = s[1];
+  ein[2 * r] = e[0];
+  ein[2 * r + 1] = e[1];
+}
+DG_KERNEL void __launch_bounds__(128) k_h2c_p2(uint32_t M, H2cMap* st, Fp* ein, const Fp* eout) {
+  uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  H2cMap s = st[m];
+  Fp c;
+  h2c_p2(s, ein[m], eout[m], c);
+  st[m].x = s.x;
+  st[m].g = s.g;
+  ein[m] = c;
+}
+DG_KERNEL void __launch_bounds__(128) k_h2c_p3(uint32_t M, const H2cMap* st, const Fp* ein, const Fp* eout,
+                                               G2JStore* iso) {
+  uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  store_g2j(iso[m], h2c_p3(st[m], ein[m], eout[m]));
+}
+// normalised to Z = 1 (one safegcd inversion): the MSM and the scalar multiplications downstream then use
+// mixed additions
+DG_KERNEL void __launch_bounds__(128) k_h2c_p4(uint32_t R, const G2JStore* iso, G2JStore* outQ) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  store_g2j(outQ[r], jac_from_aff(g2_to_aff(jac_add(load_g2j(iso[2 * r]), load_g2j(iso[2 * r + 1])))));
+}
+
+// decode of every item (96 B at sigs + stride*i + offset); items whose key did not decode are PK_DECODE
+DG_KERNEL void __launch_bounds__(128) k_dec_p1(uint32_t n, const uint8_t* sigs, uint32_t stride, uint32_t offset,
+                                               const uint32_t* item_slot, const uint8_t* key_status, DecState* ds,
+                                               Fp* ein, uint8_t* status) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t slot = item_slot ? item_slot[i] : 0u;
+  DecState d;
+  Fp e;
+  uint8_t st;
+  if (key_status[slot] != DG_ST_OK_) {
+    d.flags = 0;
+    e = fp_zero();
+    st = DG_ST_PK_DECODE_;
+  } else {
+    st = dec_p1(sigs + (size_t)stride * i + offset, d, e) ? DG_ST_SIG_DECODE_ : DG_ST_OK_;
+  }
+  ds[i] = d;
+  ein[i] = e;
+  status[i] = st;
+}
+DG_KERNEL void __launch_bounds__(128) k_dec_p2(uint32_t n, DecState* ds, Fp* ein, const Fp* eout, uint8_t* status) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (!(ds[i].flags & DEC_PENDING)) return;
+  Fp c = fp_zero();
+  if (!dec_p2(ds[i], ein[i], eout[i], c)) {
+    ds[i].flags = 0;
+    status[i] = DG_ST_SIG_DECODE_;
+  }
+  ein[i] = c;
+}
+// the sigma of item i into S, with the G2 subgroup check unless the batch checks subgroup membership on the
+// MSM window sums (`subgroup` == 0, msm.h); claim the item's (round, slot) cell -- a taken cell, or a key
+// outside the batch equation, sends the item to the individual check (`isolate`)
+DG_KERNEL void __launch_bounds__(128) k_dec_p3(uint32_t n, uint32_t k, uint32_t nslots, const uint32_t* item_slot,
+                                               const DecState* ds, const Fp* ein, const Fp* eout, G2AStore* S,
+                                               uint8_t* status, uint32_t* cell, uint8_t* isolate,
+                                               uint32_t subgroup) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  isolate[i] = 0;
+  const uint32_t flags = ds[i].flags;
+  G2A a{fp2_zero(), fp2_zero(), true};
+  bool ok = status[i] == DG_ST_OK_;
+  if (ok && (flags & DEC_PENDING)) {
+    ok = dec_p3(ds[i], ein[i], eout[i], subgroup != 0, a);
+    if (!ok) {
+      a = G2A{fp2_zero(), fp2_zero(), true};
+      status[i] = DG_ST_SIG_DECODE_;
+    }
+  }
+  store_g2a(S[i], a);
+  if (ok) {
+    const uint32_t slot = item_slot ? item_slot[i] : 0u;
+    uint32_t old = slot < nslots ? atomicExch(&cell[(size_t)(i / k) * nslots + slot], 1u) : 1u;
+    isolate[i] = old ? 1 : 0;
+  }
+}
+#else
+DG_KERNEL void __launch_bounds__(128, DG_EXP_WAVES) k_exp_pm3d4(uint32_t n, const Fp* in, Fp* out);
+DG_KERNEL void __launch_bounds__(128) k_h2c_p1(uint32_t R, const uint8_t* msgs, uint32_t msg_len, const uint8_t* dst,
+                                               uint32_t dst_len, const XmdTail* xmd, H2cMap* st, Fp* ein);
+DG_KERNEL void __launch_bounds__(128) k_h2c_p2(uint32_t M, H2cMap* st, Fp* ein, const Fp* eout);
+DG_KERNEL void __launch_bounds__(128) k_h2c_p3(uint32_t M, const H2cMap* st, const Fp* ein, const Fp* eout,
+                                               G2JStore* iso);
+DG_KERNEL void __launch_bounds__(128) k_h2c_p4(uint32_t R, const G2JStore* iso, G2JStore* outQ);
+DG_KERNEL void __launch_bounds__(128) k_dec_p1(uint32_t n, const uint8_t* sigs, uint32_t stride, uint32_t offset,
+                                               const uint32_t* item_slot, const uint8_t* key_status, DecState* ds,
+                                               Fp* ein, uint8_t* status);
+DG_KERNEL void __launch_bounds__(128) k_dec_p2(uint32_t n, DecState* ds, Fp* ein, const Fp* eout, uint8_t* status);
+DG_KERNEL void __launch_bounds__(128) k_dec_p3(uint32_t n, uint32_t k, uint32_t nslots, const uint32_t* item_slot,
+                                               const DecState* ds, const Fp* ein, const Fp* eout, G2AStore* S,
+                                               uint8_t* status, uint32_t* cell, uint8_t* isolate,
+                                               uint32_t subgroup);
+#endif
+#endif
+
+}  // namespace dg

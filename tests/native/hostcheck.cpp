@@ -3,6 +3,7 @@
 #include <string.h>
 #include "../../drand_amd/csrc/pairing.h"
 #include "../../drand_amd/csrc/h2c.h"
+#include "../../drand_amd/csrc/phases.h"
 using namespace dg;
 extern "C" {
 void hc_fp_mul(const uint8_t* a48, const uint8_t* b48, uint8_t* out48) {
@@ -121,4 +122,44 @@ extern "C" int hc_h2f_xmd32_check(const uint8_t* msg32, const uint8_t* dst, uint
   hash_to_field_xmd32(a, msg32, &T);
   hash_to_field_fp2x2(b, msg32, 32, dst, dl);
   return fp2_eq(a[0], b[0]) && fp2_eq(a[1], b[1]) ? 1 : 0;
+}
+
+// the phase pipeline of phases.h (k_h2c_p1 .. p4 with fp_pow_pm3d4_sos between) against the fused
+// hash_to_g2_uncleared: 1 if the normalised points agree
+extern "C" int hc_h2c_phases_check(const uint8_t* msg, uint32_t len, const uint8_t* dst, uint32_t dl) {
+  static XmdTail T;
+  xmd_tail_build(T, dst, dl);
+  Fp2 u[2];
+  if (len == 32)
+    hash_to_field_xmd32(u, msg, &T);
+  else
+    hash_to_field_fp2x2(u, msg, len, dst, dl);
+  H2cMap st[2];
+  Fp e[2];
+  h2c_p1(u, st, e);
+  G2J q[2];
+  for (int h = 0; h < 2; ++h) {
+    Fp c;
+    h2c_p2(st[h], e[h], fp_pow_pm3d4_sos(e[h]), c);
+    q[h] = h2c_p3(st[h], c, fp_pow_pm3d4_sos(c));
+  }
+  G2A a = g2_to_aff(jac_add(q[0], q[1]));
+  G2A b = g2_to_aff(hash_to_g2_uncleared(msg, len, dst, dl));
+  return a.inf == b.inf && fp2_eq(a.x, b.x) && fp2_eq(a.y, b.y) ? 1 : 0;
+}
+// the decompression phases (k_dec_p1 .. p3) against g2_decompress: 1 if status and point agree
+extern "C" int hc_dec_phases_check(const uint8_t* in96, int subgroup) {
+  DecState ds;
+  Fp e, c = fp_zero();
+  G2A a{fp2_zero(), fp2_zero(), true};
+  bool ok = dec_p1(in96, ds, e) == 0;
+  if (ok && (ds.flags & DEC_PENDING)) {
+    ok = dec_p2(ds, e, fp_pow_pm3d4_sos(e), c);
+    if (ok) ok = dec_p3(ds, c, fp_pow_pm3d4_sos(c), subgroup != 0, a);
+  }
+  G2A b;
+  bool okb = g2_decompress(b, in96, subgroup != 0);
+  if (ok != okb) return 0;
+  if (!ok) return 1;
+  return a.inf == b.inf && (a.inf || (fp2_eq(a.x, b.x) && fp2_eq(a.y, b.y))) ? 1 : 0;
 }

@@ -61,3 +61,26 @@ def test_no_device_means_no_compute():
         from drand_amd import tbls
 
         tbls.hash_to_g2([bytes(32)])
+
+
+NATIVE = os.path.join(ROOT, "tests", "native")
+
+
+def test_cpp_caller_compiles_against_the_header_and_runs_sanitized():
+    """tests/native/abi_caller.cpp binds every entry point to a function pointer of the exact C type (so a
+    header / library signature drift breaks the build, as it would break cgo), then calls each once without a
+    device under ASan + UBSan: compute calls return DG_E_NODEV, host-only state (timing, DST) works."""
+    src = open(os.path.join(NATIVE, "abi_caller.cpp")).read()
+    missing = [n for n in declared() if "EXPECT_TYPE(%s," % n not in src]
+    assert missing == [], missing
+    subprocess.run(["make", "-s", "-C", NATIVE, "abi_caller"], check=True)
+    r = subprocess.run([os.path.join(NATIVE, "abi_caller")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "abi_caller: ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_host_arithmetic_under_asan_ubsan():
+    """The kernels' device arithmetic built for the host with AddressSanitizer and UBSan (no recovery): the
+    word-wise expansion, both phase pipelines, decode round trips and the safegcd inversion run clean."""
+    subprocess.run(["make", "-s", "-C", NATIVE, "hostcheck_san"], check=True)
+    r = subprocess.run([os.path.join(NATIVE, "hostcheck_san")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "hostcheck_san: ok" in r.stdout, r.stdout + r.stderr

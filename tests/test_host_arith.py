@@ -87,3 +87,44 @@ def test_wordwise_xmd_matches_bytewise(hc):
         for j in range(3):
             msg = hashlib.sha256(b"xmd/%d/%d" % (dl, j)).digest()
             assert hc.hc_h2f_xmd32_check(msg, dst, dl) == 1, (dl, j)
+
+
+def test_h2c_phases_match_fused(hc):
+    """The phase pipeline of hash-to-G2 (drand_amd/csrc/phases.h: p1, exponentiation, p2, exponentiation,
+    p3, then the addition of the two maps) lands on the fused hash_to_g2_uncleared's point, for 32-byte
+    messages (word-wise expansion) and other lengths (byte-wise)."""
+    import hashlib
+
+    dst = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"
+    for j in range(40):
+        msg = hashlib.sha256(b"ph/%d" % j).digest()
+        assert hc.hc_h2c_phases_check(msg, 32, dst, len(dst)) == 1, j
+    for ln in (0, 1, 55, 100):
+        msg = (hashlib.sha256(b"pl/%d" % ln).digest() * 4)[:ln]
+        assert hc.hc_h2c_phases_check(msg, ln, dst, len(dst)) == 1, ln
+
+
+def test_decode_phases_match_g2_decompress(hc):
+    """The decompression phases (k_dec_p1..p3) give g2_decompress's status and point on the golden edge
+    cases, the torsion fixtures (with and without the subgroup check) and valid / corrupted signatures."""
+    import hashlib
+
+    encs = [hx(c["enc"]) for c in load("g2_decode_edges.json")["cases"]]
+    encs += [hx(c["sig"]) for c in load("g2_torsion.json")["cases"]]
+    ch = load("chain_t3n5.json")
+    for r in ch["rounds"][:16]:
+        s = bytearray(hx(r["sig"]))
+        encs.append(bytes(s))
+        s2 = bytearray(s)
+        s2[40] ^= 4
+        encs.append(bytes(s2))
+        s3 = bytearray(s)
+        s3[0] ^= 0x20
+        encs.append(bytes(s3))
+    for j in range(16):
+        b = bytearray(hashlib.sha256(b"rnd/%d" % j).digest() * 3)
+        b[0] = (b[0] & 0x3f) | 0x80
+        encs.append(bytes(b))
+    for e in encs:
+        for sub in (0, 1):
+            assert hc.hc_dec_phases_check(e, sub) == 1, (e.hex(), sub)

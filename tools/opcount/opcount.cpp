@@ -41,6 +41,63 @@ void oc_h2c_uncleared(const uint8_t* msg, uint32_t len, const uint8_t* dst, uint
   (void)r;
   take(out);
 }
+// the phase kernels of phases.h for one round (k_h2c_p1 / p4 per round, p2 / p3 per map item, k_exp_pm3d4
+// per exponentiation): out[6 * phase + 0..2] = (mul, sqr, inv) of phase p1, exp, p2, p3, p4 (exp: one of the
+// four), summed over the round's map items
+void oc_h2c_phases(const uint8_t* msg, const uint8_t* dst, uint32_t dl, uint64_t* out) {
+  static XmdTail T;
+  xmd_tail_build(T, dst, dl);
+  Fp2 u[2];
+  H2cMap st[2];
+  Fp e[2];
+  reset();
+  hash_to_field_xmd32(u, msg, &T);
+  h2c_p1(u, st, e);
+  take(out);
+  G2J q[2];
+  uint64_t tmp[3];
+  for (int k = 3; k < 15; ++k) out[k] = 0;
+  for (int h = 0; h < 2; ++h) {
+    reset();
+    Fp t = fp_pow_pm3d4_sos(e[h]);
+    take(tmp);
+    for (int k = 0; k < 3; ++k) out[3 + k] = tmp[k];
+    Fp c;
+    reset();
+    h2c_p2(st[h], e[h], t, c);
+    take(tmp);
+    for (int k = 0; k < 3; ++k) out[6 + k] += tmp[k];
+    Fp t2 = fp_pow_pm3d4_sos(c);
+    reset();
+    q[h] = h2c_p3(st[h], c, t2);
+    take(tmp);
+    for (int k = 0; k < 3; ++k) out[9 + k] += tmp[k];
+  }
+  reset();
+  G2J r = jac_from_aff(g2_to_aff(jac_add(q[0], q[1])));
+  (void)r;
+  take(out + 12);
+}
+// the decompression phases for one item: out = p1, exp, p2, p3 (mul, sqr, inv) each
+int oc_dec_phases(const uint8_t* sig96, uint64_t* out) {
+  DecState ds;
+  Fp e, c = fp_zero();
+  G2A a;
+  reset();
+  bool ok = dec_p1(sig96, ds, e) == 0;
+  take(out);
+  reset();
+  Fp t = fp_pow_pm3d4_sos(e);
+  take(out + 3);
+  reset();
+  ok = ok && dec_p2(ds, e, t, c);
+  take(out + 6);
+  Fp t2 = fp_pow_pm3d4_sos(c);
+  reset();
+  ok = ok && dec_p3(ds, c, t2, false, a);
+  take(out + 9);
+  return ok;
+}
 // g2_decompress (+ subgroup check when `subgroup`: multi-key batches; the beacon path batches it on the
 // MSM window sums) -- k_decode_items per item; returns decode ok
 int oc_decode_g2(const uint8_t* sig96, int subgroup, uint64_t* out) {

@@ -42,6 +42,17 @@ def main():
         alpha = int.from_bytes(hashlib.sha256(b"a%d" % i).digest()[:8], "big") | 1
         L.oc_h2c_uncleared(msg, 32, DST, len(DST), o)
         add("k_h2c_uncleared")
+        ph = (ctypes.c_uint64 * 15)()
+        L.oc_h2c_phases(msg, DST, len(DST), ph)
+        for q, name, n in ((0, "k_h2c_p1", 1), (1, "k_exp_pm3d4", 1), (2, "k_h2c_p2", 2), (3, "k_h2c_p3", 2),
+                           (4, "k_h2c_p4", 1)):
+            o[0], o[1], o[2] = ph[3 * q], ph[3 * q + 1], ph[3 * q + 2]
+            add(name, n)  # per round (p1, p4), per map item (p2, p3), per exponentiation
+        dp = (ctypes.c_uint64 * 12)()
+        assert L.oc_dec_phases(sig, dp) == 1
+        for q, name in ((0, "k_dec_p1"), (2, "k_dec_p2"), (3, "k_dec_p3")):
+            o[0], o[1], o[2] = dp[3 * q], dp[3 * q + 1], dp[3 * q + 2]
+            add(name)
         assert L.oc_decode_g2(sig, 0, o) == 1
         add("k_decode_items")  # one key, one item per round: subgroup check batched (msm.h)
         assert L.oc_decode_g2(sig, 1, o) == 1
