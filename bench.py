@@ -594,9 +594,8 @@ def main():
         # units over the two blocking batches: rounds for the fused kernels, exponentiations (4 per round of
         # hash-to-G2, 2 per signature) for k_exp_pm3d4, map items / items for the phases
         nb2 = 2 * per
-        units = {"k_h2c_uncleared": nb2, "k_decode_items": nb2, "k_exp_pm3d4": 6 * nb2, "k_h2c_p1": nb2,
-                 "k_h2c_p2": 2 * nb2, "k_h2c_p3": 2 * nb2, "k_h2c_p4": nb2, "k_dec_p1": nb2, "k_dec_p2": nb2,
-                 "k_dec_p3": nb2}
+        units = {"k_h2c_uncleared": nb2, "k_decode_items": nb2, "k_exp_pm3d4": 6 * nb2, "k_h2c_p2": 2 * nb2,
+                 "k_h2c_p3": 2 * nb2, "k_dec_p1": nb2, "k_dec_p2": nb2, "k_dec_p3": nb2}
         roof = roofline_of(kt_iso, units, peak,
                            {"timing": "HIP events on the launch stream, blocking batches right after the timed "
                                       "region (the kernel alone on the chip)"})
@@ -612,9 +611,9 @@ def main():
             # Z = 1) over the step time; per-batch fixed work not counted
             per_round = (sum(oc[k]["macs"] for k in ("k_h2c_uncleared", "k_decode_items")) +
                          26 * oc["k_msm_chunks[mixed add]"]["macs"])
-            if "k_h2c_p1" in kt_iso:  # the phase kernels (same algorithm, one inversion fewer per round)
-                per_round = (6 * oc["k_exp_pm3d4"]["macs"] + oc["k_h2c_p1"]["macs"] + 2 * oc["k_h2c_p2"]["macs"] +
-                             2 * oc["k_h2c_p3"]["macs"] + oc["k_h2c_p4"]["macs"] +
+            if "k_h2c_p1a" in kt_iso:  # the phase kernels (same algorithm, batch inversions)
+                per_round = (6 * oc["k_exp_pm3d4"]["macs"] + oc["k_h2c_p1a+p1b"]["macs"] + 2 * oc["k_h2c_p2"]["macs"] +
+                             2 * oc["k_h2c_p3"]["macs"] + oc["k_h2c_p4a+p4b"]["macs"] +
                              sum(oc[k]["macs"] for k in ("k_dec_p1", "k_dec_p2", "k_dec_p3")) +
                              26 * oc["k_msm_chunks[mixed add]"]["macs"])
             chip = per_round * G * args.steps / world / dt / 1e12

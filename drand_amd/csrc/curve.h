@@ -131,6 +131,27 @@ DGH Jac<F> jac_add_aff(const Jac<F>& p, const F& qx, const F& qy) {
   return Jac<F>{X3, Y3, Z3};
 }
 
+// The same mixed addition for G2 ordered for a small live set (Z3 first, then Z1, Z1Z1 and H, HH die; at most
+// about seven Fp2 values live at once) with the exceptional cases (P = +-Q) out of line: the per-point loop of
+// the MSM chunk sums keeps its register file free of the doubling formula.  Identical results to jac_add_aff.
+DGN G2J g2_add_aff_rare(const G2J& p, const Fp2& qx, const Fp2& qy) { return jac_add_aff(p, qx, qy); }
+DGN G2J g2_add_rare(const G2J& p, const G2J& q) { return jac_add(p, q); }
+DGI G2J g2_madd_lean(const G2J& p, const Fp2& qx, const Fp2& qy) {
+  if (jac_is_inf(p)) return G2J{qx, qy, fp2_one()};
+  const Fp2 Z1Z1 = fp2_sqr(p.z);
+  const Fp2 H = fp2_sub(fp2_mul(qx, Z1Z1), p.x);
+  const Fp2 r = fp2_dbl(fp2_sub(fp2_mul(fp2_mul(qy, p.z), Z1Z1), p.y));
+  if (fp2_is_zero(H)) return g2_add_aff_rare(p, qx, qy);
+  const Fp2 HH = fp2_sqr(H);
+  const Fp2 Z3 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(p.z, H)), Z1Z1), HH);
+  const Fp2 I = fp2_dbl(fp2_dbl(HH));
+  const Fp2 J = fp2_mul(H, I);
+  const Fp2 V = fp2_mul(p.x, I);
+  const Fp2 X3 = fp2_sub(fp2_sub(fp2_sqr(r), J), fp2_dbl(V));
+  const Fp2 Y3 = fp2_sub(fp2_mul(r, fp2_sub(V, X3)), fp2_dbl(fp2_mul(p.y, J)));
+  return G2J{X3, Y3, Z3};
+}
+
 template <class F>
 DGH bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
   bool pi = jac_is_inf(p), qi = jac_is_inf(q);
@@ -250,6 +271,54 @@ DGH G2J g2_mul_u256_psi(const G2A& p, const uint32_t* k) {
     for (int i = 0; i < 4; ++i) {
       if ((pos[i] >> b) & 1) acc = jac_add_aff(acc, px[i], py[i]);
       if ((neg[i] >> b) & 1) acc = jac_add_aff(acc, px[i], fp2_neg(py[i]));
+    }
+  }
+  return acc;
+}
+// The same product with no branch on the scalar: every bit does the doubling and one mixed addition per
+// digit, kept or dropped by a select.  Where the lanes of a wave hold different scalars (Recover rounds with
+// different share sets: the C5 adversarial batches), the branching form above executes the union of every
+// lane's additions (~8 per bit); this one executes 4.  Same result as g2_mul_u256_psi.
+DGH G2J g2_mul_u256_psi_sel(const G2A& p, const uint32_t* k) {
+  if (p.inf) return jac_infinity<Fp2>();
+  uint32_t q[8];
+  for (int w = 0; w < 8; ++w) q[w] = k[w];
+  uint64_t d[4];
+  d[0] = u256_divmod_u64(q, Z_ABS);
+  d[1] = u256_divmod_u64(q, Z_ABS);
+  d[2] = u256_divmod_u64(q, Z_ABS);
+  d[3] = (uint64_t)q[1] << 32 | q[0];
+  Fp2 px[4], py[4];
+  px[0] = p.x;
+  py[0] = p.y;
+  for (int i = 1; i < 4; ++i) {
+    px[i] = px[i - 1];
+    py[i] = py[i - 1];
+    g2_psi_aff(px[i], py[i]);
+  }
+  py[1] = fp2_neg(py[1]);
+  py[3] = fp2_neg(py[3]);
+  uint64_t pos[4], neg[4];
+  uint32_t pos64 = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t hl = d[i] + (d[i] << 1), hh = (d[i] >> 63) + (hl < d[i] ? 1u : 0u);
+    pos[i] = ((hl & ~d[i]) >> 1) | (hh << 63);
+    neg[i] = (~hl & d[i]) >> 1;
+    pos64 |= (uint32_t)(hh >> 1) << i;
+  }
+  G2J acc = jac_infinity<Fp2>();
+  for (int i = 0; i < 4; ++i) {
+    G2J t = g2_madd_lean(acc, px[i], py[i]);
+    const bool on = (pos64 >> i) & 1;
+    acc = G2J{fp2_sel(on, acc.x, t.x), fp2_sel(on, acc.y, t.y), fp2_sel(on, acc.z, t.z)};
+  }
+  for (int b = 63; b >= 0; --b) {
+    acc = jac_dbl(acc);
+    for (int i = 0; i < 4; ++i) {
+      const bool pb = (pos[i] >> b) & 1, nb = (neg[i] >> b) & 1;
+      G2J t = g2_madd_lean(acc, px[i], fp2_sel(nb, py[i], fp2_neg(py[i])));
+      const bool on = pb || nb;
+      acc = G2J{fp2_sel(on, acc.x, t.x), fp2_sel(on, acc.y, t.y), fp2_sel(on, acc.z, t.z)};
     }
   }
   return acc;

@@ -106,7 +106,7 @@ enum Slot {
   S_COMMITS, S_COMMITST, S_SLOTIDX, S_ITEMSLOT, S_SEL, S_SELIDX, S_RST, S_SST, S_TERMS, S_IN0, S_IN1, S_IN2, S_IN3,
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
-  S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_COUNT
+  S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_BINV, S_NV, S_NVINV, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -542,6 +542,38 @@ int decode_key(const uint8_t* pk48_host, hipStream_t st, G1AStore** keys, uint8_
   return 0;
 }
 
+// out[i] = 1 / vals[i] (0 for 0) for n Fp values on the device: Montgomery's trick over chunks of BINV_C, a tree of
+// chunk products, one safegcd inversion at the root (phases.h k_binv_*)
+int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st) {
+  std::vector<uint32_t> sizes{n};
+  while (sizes.back() > BINV_C) sizes.push_back((sizes.back() + BINV_C - 1) / BINV_C);
+  const size_t L = sizes.size();
+  size_t total = 0;
+  for (size_t l = 0; l < L; ++l) total += 3 * (size_t)sizes[l];
+  Fp* buf;
+  RET(wsT(S_BINV, total, &buf));
+  // level l: in[l] (the values), pre[l], inv[l] (their inverses); in[0] = vals, inv[0] = out
+  std::vector<const Fp*> in(L);
+  std::vector<Fp*> pre(L), inv(L);
+  Fp* q = buf;
+  for (size_t l = 0; l < L; ++l) {
+    pre[l] = q;
+    q += sizes[l];
+    inv[l] = l == 0 ? out : q;
+    q += sizes[l];
+    in[l] = l == 0 ? vals : q;
+    q += sizes[l];
+  }
+  for (size_t l = 0; l + 1 < L; ++l)
+    RET(launch("k_binv_up", k_binv_up, (sizes[l] + BINV_C - 1) / BINV_C, 128, st, sizes[l], in[l], pre[l],
+               (Fp*)in[l + 1]));
+  RET(launch("k_binv_root", k_binv_root, 1, 64, st, sizes[L - 1], in[L - 1], inv[L - 1]));
+  for (size_t l = L - 1; l-- > 0;)
+    RET(launch("k_binv_down", k_binv_down, (sizes[l] + BINV_C - 1) / BINV_C, 128, st, sizes[l], in[l],
+               (const Fp*)pre[l], (const Fp*)inv[l + 1], inv[l]));
+  return 0;
+}
+
 // The current DST and its expand_message_xmd tail on the device (blocking upload after a DST change: batches
 // in flight keep reading the old bytes until they finish, so they are waited for first).
 int ensure_dst() {
@@ -578,13 +610,20 @@ int hash_rounds(uint32_t R, const uint8_t* d_msgs, uint32_t msg_len, hipStream_t
   RET(wsT(S_EIN, M, &ein));
   RET(wsT(S_EOUT, M, &eout));
   RET(wsT(S_ISOPT, M, &iso));
-  RET(launch("k_h2c_p1", k_h2c_p1, R, 128, st, R, d_msgs, msg_len, (const uint8_t*)d_dst, (uint32_t)g_ctx.dst.size(),
-             (const XmdTail*)g_ctx.d_xmd, hs, ein));
+  Fp *nv, *nvinv;
+  RET(wsT(S_NV, R, &nv));
+  RET(wsT(S_NVINV, R, &nvinv));
+  RET(launch("k_h2c_p1a", k_h2c_p1a, R, 128, st, R, d_msgs, msg_len, (const uint8_t*)d_dst, (uint32_t)g_ctx.dst.size(),
+             (const XmdTail*)g_ctx.d_xmd, hs, nv));
+  RET(batch_inv(R, nv, nvinv, st));
+  RET(launch("k_h2c_p1b", k_h2c_p1b, R, 128, st, R, hs, (const Fp*)nvinv, ein));
   RET(launch("k_exp_pm3d4", k_exp_pm3d4, M, 128, st, M, (const Fp*)ein, eout));
   RET(launch("k_h2c_p2", k_h2c_p2, M, 128, st, M, hs, ein, (const Fp*)eout));
   RET(launch("k_exp_pm3d4", k_exp_pm3d4, M, 128, st, M, (const Fp*)ein, eout));
   RET(launch("k_h2c_p3", k_h2c_p3, M, 128, st, M, (const H2cMap*)hs, (const Fp*)ein, (const Fp*)eout, iso));
-  return launch("k_h2c_p4", k_h2c_p4, R, 128, st, R, (const G2JStore*)iso, *Q);
+  RET(launch("k_h2c_p4a", k_h2c_p4a, R, 128, st, R, (const G2JStore*)iso, *Q, nv));
+  RET(batch_inv(R, nv, nvinv, st));
+  return launch("k_h2c_p4b", k_h2c_p4b, R, 128, st, R, *Q, (const Fp*)nvinv);
 }
 
 // bls.Verify batch against one key, everything device-resident

@@ -730,7 +730,13 @@ DG_KERNEL void __launch_bounds__(64, DG_HOT_WAVES) k_recover_terms(uint32_t R, u
     return;
   }
   Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, m);
-  store_g2j(terms[o], g2_mul_u256_psi(load_g2a(S[(size_t)r * k + sel[o]]), lam.l));
+  // one scalar for the whole wave (its rounds selected the same index set): the branching Straus is uniform;
+  // otherwise the select form (no divergence on the digits)
+  bool same = true;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) same = same && lam.l[w] == __builtin_amdgcn_readfirstlane(lam.l[w]);
+  const G2A s = load_g2a(S[(size_t)r * k + sel[o]]);
+  store_g2j(terms[o], __all(same) ? g2_mul_u256_psi(s, lam.l) : g2_mul_u256_psi_sel(s, lam.l));
 }
 #else
 DG_KERNEL void __launch_bounds__(64, DG_HOT_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,

@@ -148,11 +148,12 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_ch
   const Fp2 one = fp2_one();
   for (uint32_t i = first + 1; i < last; ++i) {
     const G2JStore& q = P[list[i]];
-    // decoded signatures enter with Z = 1: mixed addition (7M + 4S instead of 11M + 5S in Fp2)
+    // signatures and hashes enter normalised (Z = 1) or as the identity (Z = 0): mixed additions (7M + 4S
+    // instead of 11M + 5S in Fp2); any other Z takes the full addition, out of line
     if (fp2_eq(q.z, one))
-      acc = jac_add_aff(acc, q.x, q.y);
-    else
-      acc = jac_add(acc, load_g2j(q));
+      acc = g2_madd_lean(acc, q.x, q.y);
+    else if (!fp2_is_zero(q.z))
+      acc = g2_add_rare(acc, load_g2j(q));
   }
   store_g2j(out[side * max_chunks + c], acc);
 }
@@ -386,7 +387,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_kmsm_chunks(uint32_t max_c
   G2J acc = jac_from_aff(load_g2a(S[list[first]]));
   for (uint32_t i = first + 1; i < last; ++i) {
     const G2AStore& q = S[list[i]];
-    if (!q.inf) acc = jac_add_aff(acc, q.x, q.y);  // the identity encoding decodes (status OK)
+    if (!q.inf) acc = g2_madd_lean(acc, q.x, q.y);  // the identity encoding decodes (status OK)
   }
   store_g2j(out[c], acc);
 }

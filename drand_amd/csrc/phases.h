@@ -11,13 +11,16 @@
 // one register-lean kernel, k_exp_pm3d4 (SOS products in the radix-2^28 digit form, no calls, no scratch).
 //
 //   hash-to-G2 (per batch of R rounds, M = 2R map items):
-//     k_h2c_p1  (R)  expand_message_xmd, both u_h; x1 = -B/A (1 + 1/den) with ONE inversion for both
-//                    maps (Montgomery's trick); gx1; exponent input norm(gx1)
+//     k_h2c_p1a (R)  expand_message_xmd, both u_h, den_h, norm(den_0 den_1)
+//     k_binv_*       1 / norm(den_0 den_1) for every round: Montgomery's trick across the batch
+//     k_h2c_p1b (R)  x1 = -B/A (1 + 1/den) for both maps, gx1; exponent input norm(gx1)
 //     k_exp     (M)  t = norm(gx1)^((p-3)/4)
 //     k_h2c_p2  (M)  s1 = t n1, square test, x / g / s of the chosen branch; input c of the second root
 //     k_exp     (M)  t2 = c^((p-3)/4)
 //     k_h2c_p3  (M)  y = sqrt(g) from c, t2 (checked; the full root as a fallback), sgn0 fix, 3-isogeny
-//     k_h2c_p4  (R)  q0 + q1, normalised to Z = 1 (one safegcd inversion)
+//     k_h2c_p4a (R)  q0 + q1 (Jacobian), norm(Z)
+//     k_binv_*       1 / norm(Z) for every round
+//     k_h2c_p4b (R)  normalised to Z = 1
 //   sigma decompression (per batch of N items):
 //     k_dec_p1  (N)  flags, canonical x, rhs = x^3 + 4(1+u); exponent input norm(rhs)
 //     k_exp     (N)
@@ -39,26 +42,28 @@ struct DecState {
   uint32_t pad[3];
 };
 constexpr uint32_t DEC_PENDING = 1, DEC_SIGN = 2, DEC_INF = 4;
+constexpr uint32_t BINV_C = 32;  // chunk of the batch inversion (k_binv_*)
 
 // ------------------------------------------------------------------------------ exponentiation
-// x^((p-3)/4) by the width-3 sliding-window schedule of field.h, SOS products in the digit form
+// x^((p-3)/4) by a width-4 sliding-window schedule (the 8 odd powers x, x^3, .., x^15; 376 squarings and 85
+// multiplications instead of 378 and 108 at width 3; tools/microbench/expchain.hip: -7%), SOS products in the
+// digit form.  The schedule is wave-uniform (scalar loads), the table entry is picked by a v_cndmask chain.
 DGI Fp fp_pow_pm3d4_sos(const Fp& x) {
-  uint32_t t0[14], t1[14], t2[14], t3[14], x2[14], acc[14], nxt[14], m[14];
-  fp28_unpack(x.l, t0);
-  fp28_sos_sqr_d(t0, x2);
-  fp28_sos_mul_d(t0, x2, t1);
-  fp28_sos_mul_d(t1, x2, t2);
-  fp28_sos_mul_d(t2, x2, t3);
+  uint32_t tab[8][14], x2[14], acc[14], nxt[14], m[14];
+  fp28_unpack(x.l, tab[0]);
   DG_COUNT_SQR();
-  DG_COUNT_MUL();
-  DG_COUNT_MUL();
-  DG_COUNT_MUL();
-  const int first = EXP_PM3D4_FIRST;
+  fp28_sos_sqr_d(tab[0], x2);
 #pragma unroll
-  for (int d = 0; d < 14; ++d) acc[d] = first == 0 ? t0[d] : first == 1 ? t1[d] : first == 2 ? t2[d] : t3[d];
-  for (int s = 0; s < EXP_PM3D4_NSTEPS; ++s) {
-    const int k = EXP_PM3D4_STEPS[s][0];
-    const int idx = EXP_PM3D4_STEPS[s][1];
+  for (int k = 1; k < 8; ++k) {
+    DG_COUNT_MUL();
+    fp28_sos_mul_d(tab[k - 1], x2, tab[k]);
+  }
+  const int first = EXP_PM3D4_W4_FIRST;
+#pragma unroll
+  for (int d = 0; d < 14; ++d) acc[d] = tab[first][d];
+  for (int s = 0; s < EXP_PM3D4_W4_NSTEPS; ++s) {
+    const int k = EXP_PM3D4_W4_STEPS[s][0];
+    const int idx = EXP_PM3D4_W4_STEPS[s][1];
     for (int j = 0; j < k; ++j) {
       DG_COUNT_SQR();
       fp28_sos_sqr_d(acc, nxt);
@@ -67,7 +72,12 @@ DGI Fp fp_pow_pm3d4_sos(const Fp& x) {
     }
     if (idx >= 0) {
 #pragma unroll
-      for (int d = 0; d < 14; ++d) m[d] = idx == 0 ? t0[d] : idx == 1 ? t1[d] : idx == 2 ? t2[d] : t3[d];
+      for (int d = 0; d < 14; ++d) {
+        uint32_t v = tab[0][d];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) v = idx == q ? tab[q][d] : v;
+        m[d] = v;
+      }
       DG_COUNT_MUL();
       fp28_sos_mul_d(acc, m, nxt);
 #pragma unroll
@@ -99,28 +109,50 @@ DGN bool fp2_sqrt_slow(Fp2& r, const Fp2& a) { return fp2_sqrt(r, a); }
 DGN bool g2_in_subgroup_slow(const Fp2& x, const Fp2& y) { return g2_in_subgroup_aff(x, y); }
 
 // ------------------------------------------------------------------------------ hash-to-G2 phases
-// P1 of round r: both maps' x1, gx1 and the first exponent inputs norm(gx1)
-DGI void h2c_p1(const Fp2 (&u)[2], H2cMap (&st)[2], Fp (&ein)[2]) {
-  const Fp2 A = fp2_const(SSWU_A), B = fp2_const(SSWU_B), Z = fp2_const(SSWU_Z);
-  Fp2 den[2], d[2];
-  bool zero[2];
+// P1 of round r, split around a batch inversion (Montgomery's trick across the batch, k_binv_*: one
+// safegcd per ~10^5 rounds instead of one per round).  p1a: den_h of both maps (kept in st[h].x) and the
+// norm of D = d_0 d_1 (d_h = den_h, or 1 when den_h = 0), the value to invert.
+DGI void h2c_p1a(const Fp2 (&u)[2], H2cMap (&st)[2], Fp& nD) {
+  const Fp2 Z = fp2_const(SSWU_Z);
+  Fp2 d[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     Fp2 zu2 = fp2_mul(Z, fp2_sqr(u[h]));
-    den[h] = fp2_add(fp2_sqr(zu2), zu2);
-    zero[h] = fp2_is_zero(den[h]);
-    d[h] = zero[h] ? fp2_one() : den[h];
+    Fp2 den = fp2_add(fp2_sqr(zu2), zu2);
+    st[h].u = u[h];
+    st[h].x = den;
+    d[h] = fp2_is_zero(den) ? fp2_one() : den;
   }
-  // 1/den_0 and 1/den_1 from one inversion of the product
-  Fp2 inv = fp2_inv(fp2_mul(d[0], d[1]));
+  nD = fp2_norm(fp2_mul(d[0], d[1]));
+}
+// p1b: with inv_nD = 1 / norm(D): 1/den_h, x1 = -B/A (1 + 1/den) (B/(ZA) when den = 0), gx1 and the first
+// exponent inputs norm(gx1)
+DGI void h2c_p1b(H2cMap (&st)[2], const Fp& inv_nD, Fp (&ein)[2]) {
+  const Fp2 A = fp2_const(SSWU_A), B = fp2_const(SSWU_B);
+  bool zero[2];
+  Fp2 d[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    zero[h] = fp2_is_zero(st[h].x);
+    d[h] = zero[h] ? fp2_one() : st[h].x;
+  }
+  Fp2 D = fp2_mul(d[0], d[1]);
+  Fp2 inv = Fp2{fp_mul(D.c0, inv_nD), fp_neg(fp_mul(D.c1, inv_nD))};  // fp2_inv(D)
   Fp2 inv_h[2] = {fp2_mul(inv, d[1]), fp2_mul(inv, d[0])};
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     Fp2 x1 = zero[h] ? fp2_const(SSWU_B_OVER_ZA) : fp2_mul(fp2_const(SSWU_MINUS_B_OVER_A), fp2_add(fp2_one(), inv_h[h]));
     Fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), A), x1), B);
-    st[h] = H2cMap{u[h], x1, gx1};
+    st[h].x = x1;
+    st[h].g = gx1;
     ein[h] = fp2_norm(gx1);
   }
+}
+// the fused form (host checks, opcounts): both halves around one inversion
+DGI void h2c_p1(const Fp2 (&u)[2], H2cMap (&st)[2], Fp (&ein)[2]) {
+  Fp nD;
+  h2c_p1a(u, st, nD);
+  h2c_p1b(st, fp_inv(nD), ein);
 }
 // P2 of one map: t = n1^((p-3)/4); the branch of sswu_g2 (h2c.h) and the input c of the second root
 DGI void h2c_p2(H2cMap& st, const Fp& n1, const Fp& t, Fp& c) {
@@ -202,8 +234,8 @@ DG_KERNEL void __launch_bounds__(128, DG_EXP_WAVES) k_exp_pm3d4(uint32_t n, cons
   out[i] = fp_pow_pm3d4_sos(in[i]);
 }
 
-DG_KERNEL void __launch_bounds__(128) k_h2c_p1(uint32_t R, const uint8_t* msgs, uint32_t msg_len, const uint8_t* dst,
-                                               uint32_t dst_len, const XmdTail* xmd, H2cMap* st, Fp* ein) {
+DG_KERNEL void __launch_bounds__(128) k_h2c_p1a(uint32_t R, const uint8_t* msgs, uint32_t msg_len, const uint8_t* dst,
+                                                uint32_t dst_len, const XmdTail* xmd, H2cMap* st, Fp* nD) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   Fp2 u[2];
@@ -212,8 +244,18 @@ DG_KERNEL void __launch_bounds__(128) k_h2c_p1(uint32_t R, const uint8_t* msgs, 
   else
     hash_to_field_fp2x2(u, msgs + (size_t)msg_len * r, msg_len, dst, dst_len);
   H2cMap s[2];
+  h2c_p1a(u, s, nD[r]);
+  st[2 * r].u = s[0].u;
+  st[2 * r].x = s[0].x;
+  st[2 * r + 1].u = s[1].u;
+  st[2 * r + 1].x = s[1].x;
+}
+DG_KERNEL void __launch_bounds__(128) k_h2c_p1b(uint32_t R, H2cMap* st, const Fp* inv_nD, Fp* ein) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  H2cMap s[2] = {st[2 * r], st[2 * r + 1]};
   Fp e[2];
-  h2c_p1(u, s, e);
+  h2c_p1b(s, inv_nD[r], e);
   st[2 * r] = s[0];
   st[2 * r + 1] = s[1];
   ein[2 * r] = e[0];
@@ -235,12 +277,75 @@ DG_KERNEL void __launch_bounds__(128) k_h2c_p3(uint32_t M, const H2cMap* st, con
   if (m >= M) return;
   store_g2j(iso[m], h2c_p3(st[m], ein[m], eout[m]));
 }
-// normalised to Z = 1 (one safegcd inversion): the MSM and the scalar multiplications downstream then use
-// mixed additions
-DG_KERNEL void __launch_bounds__(128) k_h2c_p4(uint32_t R, const G2JStore* iso, G2JStore* outQ) {
+// P4: q0 + q1 and the norm of its Z (the value the batch inversion inverts), then the normalisation to
+// Z = 1 with that inverse: the MSM and the scalar multiplications downstream use mixed additions
+DG_KERNEL void __launch_bounds__(128) k_h2c_p4a(uint32_t R, const G2JStore* iso, G2JStore* outQ, Fp* nZ) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
-  store_g2j(outQ[r], jac_from_aff(g2_to_aff(jac_add(load_g2j(iso[2 * r]), load_g2j(iso[2 * r + 1])))));
+  G2J q = jac_add(load_g2j(iso[2 * r]), load_g2j(iso[2 * r + 1]));
+  store_g2j(outQ[r], q);
+  nZ[r] = fp2_norm(q.z);  // zero for the identity
+}
+DG_KERNEL void __launch_bounds__(128) k_h2c_p4b(uint32_t R, G2JStore* Q, const Fp* inv_nZ) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  G2J q = load_g2j(Q[r]);
+  if (jac_is_inf(q)) return;  // stays the identity (Z = 0)
+  Fp2 zinv{fp_mul(q.z.c0, inv_nZ[r]), fp_neg(fp_mul(q.z.c1, inv_nZ[r]))};  // fp2_inv(Z)
+  store_g2j(Q[r], jac_from_aff(jac_to_aff_with_inv(q, zinv)));
+}
+
+// ---- batch inversion of n Fp values (Montgomery's trick over chunks of BINV_C consecutive values, a tree of
+// chunk products, one safegcd at the root).  Zero inputs give zero.  Level arrays: vals (the inputs of the
+// level), pre (their running products inside each chunk), up (one product per chunk = the next level's
+// inputs); the inverses come back down: k_binv_down turns the inverse of each chunk product into the
+// inverses of the chunk's values.
+DG_KERNEL void __launch_bounds__(128) k_binv_up(uint32_t n, const Fp* vals, Fp* pre, Fp* up) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t a = j * BINV_C;
+  if (a >= n) return;
+  uint32_t b = a + BINV_C < n ? a + BINV_C : n;
+  Fp acc = fp_one();
+  for (uint32_t i = a; i < b; ++i) {
+    Fp v = vals[i];
+    acc = fp_mul(acc, fp_is_zero(v) ? fp_one() : v);
+    pre[i] = acc;
+  }
+  up[j] = acc;
+}
+// inv: the inverses of the chunk products (the level above); out: the inverses of vals
+DG_KERNEL void __launch_bounds__(128) k_binv_down(uint32_t n, const Fp* vals, const Fp* pre, const Fp* inv, Fp* out) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t a = j * BINV_C;
+  if (a >= n) return;
+  uint32_t b = a + BINV_C < n ? a + BINV_C : n;
+  Fp I = inv[j];
+  for (uint32_t i = b - 1; i > a; --i) {
+    Fp v = vals[i];
+    bool z = fp_is_zero(v);
+    out[i] = z ? fp_zero() : fp_mul(I, pre[i - 1]);
+    I = z ? I : fp_mul(I, v);
+  }
+  out[a] = fp_is_zero(vals[a]) ? fp_zero() : I;
+}
+// the top level (n <= BINV_C values), one lane: inverses of vals by one safegcd
+DG_KERNEL void __launch_bounds__(64) k_binv_root(uint32_t n, const Fp* vals, Fp* out) {
+  if (blockIdx.x * blockDim.x + threadIdx.x != 0) return;
+  Fp pre[BINV_C];
+  Fp acc = fp_one();
+  for (uint32_t i = 0; i < n; ++i) {
+    Fp v = vals[i];
+    acc = fp_mul(acc, fp_is_zero(v) ? fp_one() : v);
+    pre[i] = acc;
+  }
+  Fp I = fp_inv(acc);
+  for (uint32_t i = n - 1; i > 0; --i) {
+    Fp v = vals[i];
+    bool z = fp_is_zero(v);
+    out[i] = z ? fp_zero() : fp_mul(I, pre[i - 1]);
+    I = z ? I : fp_mul(I, v);
+  }
+  out[0] = fp_is_zero(vals[0]) ? fp_zero() : I;
 }
 
 // decode of every item (96 B at sigs + stride*i + offset); items whose key did not decode are PK_DECODE
@@ -304,12 +409,17 @@ DG_KERNEL void __launch_bounds__(128) k_dec_p3(uint32_t n, uint32_t k, uint32_t 
 }
 #else
 DG_KERNEL void __launch_bounds__(128, DG_EXP_WAVES) k_exp_pm3d4(uint32_t n, const Fp* in, Fp* out);
-DG_KERNEL void __launch_bounds__(128) k_h2c_p1(uint32_t R, const uint8_t* msgs, uint32_t msg_len, const uint8_t* dst,
-                                               uint32_t dst_len, const XmdTail* xmd, H2cMap* st, Fp* ein);
+DG_KERNEL void __launch_bounds__(128) k_h2c_p1a(uint32_t R, const uint8_t* msgs, uint32_t msg_len, const uint8_t* dst,
+                                                uint32_t dst_len, const XmdTail* xmd, H2cMap* st, Fp* nD);
+DG_KERNEL void __launch_bounds__(128) k_h2c_p1b(uint32_t R, H2cMap* st, const Fp* inv_nD, Fp* ein);
+DG_KERNEL void __launch_bounds__(128) k_binv_up(uint32_t n, const Fp* vals, Fp* pre, Fp* up);
+DG_KERNEL void __launch_bounds__(128) k_binv_down(uint32_t n, const Fp* vals, const Fp* pre, const Fp* inv, Fp* out);
+DG_KERNEL void __launch_bounds__(64) k_binv_root(uint32_t n, const Fp* vals, Fp* out);
 DG_KERNEL void __launch_bounds__(128) k_h2c_p2(uint32_t M, H2cMap* st, Fp* ein, const Fp* eout);
 DG_KERNEL void __launch_bounds__(128) k_h2c_p3(uint32_t M, const H2cMap* st, const Fp* ein, const Fp* eout,
                                                G2JStore* iso);
-DG_KERNEL void __launch_bounds__(128) k_h2c_p4(uint32_t R, const G2JStore* iso, G2JStore* outQ);
+DG_KERNEL void __launch_bounds__(128) k_h2c_p4a(uint32_t R, const G2JStore* iso, G2JStore* outQ, Fp* nZ);
+DG_KERNEL void __launch_bounds__(128) k_h2c_p4b(uint32_t R, G2JStore* Q, const Fp* inv_nZ);
 DG_KERNEL void __launch_bounds__(128) k_dec_p1(uint32_t n, const uint8_t* sigs, uint32_t stride, uint32_t offset,
                                                const uint32_t* item_slot, const uint8_t* key_status, DecState* ds,
                                                Fp* ein, uint8_t* status);

@@ -75,6 +75,7 @@ def test_g2_mul_psi_decomposition_host_build(hc):
     for k in ks:
         k8 = (ctypes.c_uint32 * 8)(*[(k >> (32 * w)) & 0xFFFFFFFF for w in range(8)])
         assert hc.hc_g2_mul_psi_check(sig, k8) == 1, hex(k)
+        assert hc.hc_g2_mul_sel_check(sig, k8) == 1, hex(k)  # the select form of divergent Recover waves
 
 
 def test_wordwise_xmd_matches_bytewise(hc):

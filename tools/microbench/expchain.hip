@@ -105,6 +105,70 @@ DGI void pow_d(uint32_t (&acc)[14], const uint32_t (&x)[14], int first, const in
   }
 }
 
+// V2: SOS products, width-4 window (8 odd powers), the table indexed by the wave-uniform schedule entry
+DGI void pow_w4(uint32_t (&acc)[14], const uint32_t (&x)[14]) {
+  uint32_t tab[8][14], x2[14], nxt[14];
+#pragma unroll
+  for (int d = 0; d < 14; ++d) tab[0][d] = x[d];
+  sqr_d<1>(x, x2);
+#pragma unroll
+  for (int k = 1; k < 8; ++k) mul_d<1>(tab[k - 1], x2, tab[k]);
+  const int first = EXP_PM3D4_W4_FIRST;
+#pragma unroll
+  for (int d = 0; d < 14; ++d) acc[d] = tab[first][d];
+  for (int s = 0; s < EXP_PM3D4_W4_NSTEPS; ++s) {
+    const int k = EXP_PM3D4_W4_STEPS[s][0];
+    const int idx = EXP_PM3D4_W4_STEPS[s][1];
+    for (int j = 0; j < k; ++j) {
+      sqr_d<1>(acc, nxt);
+#pragma unroll
+      for (int d = 0; d < 14; ++d) acc[d] = nxt[d];
+    }
+    if (idx >= 0) {
+      uint32_t m[14];
+#pragma unroll
+      for (int d = 0; d < 14; ++d) m[d] = tab[idx][d];
+      mul_d<1>(acc, m, nxt);
+#pragma unroll
+      for (int d = 0; d < 14; ++d) acc[d] = nxt[d];
+    }
+  }
+}
+// V3: as V2, the table selected by a v_cndmask chain
+DGI void pow_w4s(uint32_t (&acc)[14], const uint32_t (&x)[14]) {
+  uint32_t tab[8][14], x2[14], nxt[14];
+#pragma unroll
+  for (int d = 0; d < 14; ++d) tab[0][d] = x[d];
+  sqr_d<1>(x, x2);
+#pragma unroll
+  for (int k = 1; k < 8; ++k) mul_d<1>(tab[k - 1], x2, tab[k]);
+  const int first = EXP_PM3D4_W4_FIRST;
+#pragma unroll
+  for (int d = 0; d < 14; ++d) acc[d] = tab[first][d];
+  for (int s = 0; s < EXP_PM3D4_W4_NSTEPS; ++s) {
+    const int k = EXP_PM3D4_W4_STEPS[s][0];
+    const int idx = EXP_PM3D4_W4_STEPS[s][1];
+    for (int j = 0; j < k; ++j) {
+      sqr_d<1>(acc, nxt);
+#pragma unroll
+      for (int d = 0; d < 14; ++d) acc[d] = nxt[d];
+    }
+    if (idx >= 0) {
+      uint32_t m[14];
+#pragma unroll
+      for (int d = 0; d < 14; ++d) {
+        uint32_t v = tab[0][d];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) v = idx == q ? tab[q][d] : v;
+        m[d] = v;
+      }
+      mul_d<1>(acc, m, nxt);
+#pragma unroll
+      for (int d = 0; d < 14; ++d) acc[d] = nxt[d];
+    }
+  }
+}
+
 template <int V, int W>
 __global__ void __launch_bounds__(128, W) k_pow(const uint32_t* in, uint32_t* out, int n, int reps) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -113,7 +177,12 @@ __global__ void __launch_bounds__(128, W) k_pow(const uint32_t* in, uint32_t* ou
 #pragma unroll
   for (int d = 0; d < 14; ++d) x[d] = in[(size_t)d * n + i];
   for (int r = 0; r < reps; ++r) {
-    pow_d<V>(a, x, EXP_PM3D4_FIRST, EXP_PM3D4_STEPS);
+    if (V == 2)
+      pow_w4(a, x);
+    else if (V == 3)
+      pow_w4s(a, x);
+    else
+      pow_d<V>(a, x, EXP_PM3D4_FIRST, EXP_PM3D4_STEPS);
 #pragma unroll
     for (int d = 0; d < 14; ++d) x[d] = a[d];
   }
@@ -158,7 +227,8 @@ int main(int argc, char** argv) {
     const char* name;
     void (*f)(const uint32_t*, uint32_t*, int, int);
   } ks[] = {{"V0 W1", k_pow<0, 1>}, {"V0 W2", k_pow<0, 2>}, {"V0 W3", k_pow<0, 3>}, {"V0 W4", k_pow<0, 4>},
-            {"V1 W1", k_pow<1, 1>}, {"V1 W2", k_pow<1, 2>}, {"V1 W3", k_pow<1, 3>}, {"V1 W4", k_pow<1, 4>}};
+            {"V1 W1", k_pow<1, 1>}, {"V1 W2", k_pow<1, 2>}, {"V1 W3", k_pow<1, 3>}, {"V1 W4", k_pow<1, 4>},
+            {"V2 W1", k_pow<2, 1>}, {"V2 W2", k_pow<2, 2>}, {"V3 W1", k_pow<3, 1>}, {"V3 W2", k_pow<3, 2>}};
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0));
   CHK(hipEventCreate(&e1));

@@ -52,8 +52,15 @@ void oc_h2c_phases(const uint8_t* msg, const uint8_t* dst, uint32_t dl, uint64_t
   Fp e[2];
   reset();
   hash_to_field_xmd32(u, msg, &T);
-  h2c_p1(u, st, e);
+  Fp nD;
+  h2c_p1a(u, st, nD);
+  uint64_t part[3];
+  take(part);
+  Fp inv_nD = fp_inv(nD);  // the batch inversion's share (3 products per value) is not counted here
+  reset();
+  h2c_p1b(st, inv_nD, e);
   take(out);
+  for (int k = 0; k < 3; ++k) out[k] += part[k];
   G2J q[2];
   uint64_t tmp[3];
   for (int k = 3; k < 15; ++k) out[k] = 0;
@@ -74,9 +81,16 @@ void oc_h2c_phases(const uint8_t* msg, const uint8_t* dst, uint32_t dl, uint64_t
     for (int k = 0; k < 3; ++k) out[9 + k] += tmp[k];
   }
   reset();
-  G2J r = jac_from_aff(g2_to_aff(jac_add(q[0], q[1])));
-  (void)r;
+  G2J r = jac_add(q[0], q[1]);
+  Fp nZ = fp2_norm(r.z);
+  take(part);
+  Fp inv_nZ = fp_inv(nZ);  // from the batch inversion, not counted
+  reset();
+  Fp2 zinv{fp_mul(r.z.c0, inv_nZ), fp_neg(fp_mul(r.z.c1, inv_nZ))};  // as k_h2c_p4b
+  G2J a = jac_from_aff(jac_to_aff_with_inv(r, zinv));
+  (void)a;
   take(out + 12);
+  for (int k = 0; k < 3; ++k) out[12 + k] += part[k];
 }
 // the decompression phases for one item: out = p1, exp, p2, p3 (mul, sqr, inv) each
 int oc_dec_phases(const uint8_t* sig96, uint64_t* out) {

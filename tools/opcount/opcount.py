@@ -44,8 +44,8 @@ def main():
         add("k_h2c_uncleared")
         ph = (ctypes.c_uint64 * 15)()
         L.oc_h2c_phases(msg, DST, len(DST), ph)
-        for q, name, n in ((0, "k_h2c_p1", 1), (1, "k_exp_pm3d4", 1), (2, "k_h2c_p2", 2), (3, "k_h2c_p3", 2),
-                           (4, "k_h2c_p4", 1)):
+        for q, name, n in ((0, "k_h2c_p1a+p1b", 1), (1, "k_exp_pm3d4", 1), (2, "k_h2c_p2", 2), (3, "k_h2c_p3", 2),
+                           (4, "k_h2c_p4a+p4b", 1)):
             o[0], o[1], o[2] = ph[3 * q], ph[3 * q + 1], ph[3 * q + 2]
             add(name, n)  # per round (p1, p4), per map item (p2, p3), per exponentiation
         dp = (ctypes.c_uint64 * 12)()
