@@ -657,6 +657,30 @@ DGN Fp12 fp12_inv(const Fp12& a) {
   t = fp6_inv(t);
   return Fp12{fp6_mul(a.c0, t), fp6_neg(fp6_mul(a.c1, t))};
 }
+// Squaring in the cyclotomic subgroup (elements after the easy part of the final exponentiation), Granger-Scott:
+// Fp12 seen as three Fp4 = Fp2[s]/(s^2 - xi) pieces (c0.c0, c1.c1), (c1.c0, c0.c2), (c0.c1, c1.c2); 9 Fp2
+// squarings (18 Fp products) instead of the 36 of fp12_sqr.
+DGI void fp4_sqr(const Fp2& a, const Fp2& b, Fp2& c0, Fp2& c1) {
+  Fp2 t0 = fp2_sqr(a), t1 = fp2_sqr(b);
+  c0 = fp2_add(fp2_mul_xi(t1), t0);
+  c1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(a, b)), t0), t1);
+}
+DGN Fp12 fp12_cyc_sqr(const Fp12& f) {
+  Fp2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+  Fp2 t0, t1, t2, t3;
+  fp4_sqr(z0, z1, t0, t1);
+  z0 = fp2_add(fp2_dbl(fp2_sub(t0, z0)), t0);  // 3 t0 - 2 z0
+  z1 = fp2_add(fp2_dbl(fp2_add(t1, z1)), t1);  // 3 t1 + 2 z1
+  fp4_sqr(z2, z3, t0, t1);
+  fp4_sqr(z4, z5, t2, t3);
+  z4 = fp2_add(fp2_dbl(fp2_sub(t0, z4)), t0);
+  z5 = fp2_add(fp2_dbl(fp2_add(t1, z5)), t1);
+  t0 = fp2_mul_xi(t3);
+  z2 = fp2_add(fp2_dbl(fp2_add(t0, z2)), t0);
+  z3 = fp2_add(fp2_dbl(fp2_sub(t2, z3)), t2);
+  return Fp12{Fp6{z0, z4, z3}, Fp6{z2, z1, z5}};
+}
+
 // multiply by the sparse line l = c0 + c1 v + c4 v w (M-type twist; slots 0, 1, 4)
 DGN Fp12 fp12_mul_014(const Fp12& f, const Fp2& c0, const Fp2& c1, const Fp2& c4) {
   Fp6 aa = fp6_mul_01(f.c0, c0, c1);

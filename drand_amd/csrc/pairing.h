@@ -75,11 +75,11 @@ DGI Fp12 miller_loop(const G1A* P, const G2A* Q, int np) {
   return fp12_conj(f);  // z < 0
 }
 
-// a^z for a in the cyclotomic subgroup (z < 0: conjugate of a^|z|)
+// a^z for a in the cyclotomic subgroup (z < 0: conjugate of a^|z|), cyclotomic squarings
 DGN Fp12 cyc_exp_z(const Fp12& a) {
   Fp12 acc = a;
   for (int b = 62; b >= 0; --b) {
-    acc = fp12_sqr(acc);
+    acc = fp12_cyc_sqr(acc);
     if ((Z_ABS >> b) & 1) acc = fp12_mul(acc, a);
   }
   return fp12_conj(acc);

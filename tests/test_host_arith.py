@@ -129,3 +129,21 @@ def test_decode_phases_match_g2_decompress(hc):
     for e in encs:
         for sub in (0, 1):
             assert hc.hc_dec_phases_check(e, sub) == 1, (e.hex(), sub)
+
+
+def test_pairing_host_build_matches_twin(hc):
+    """The kernels' Miller loop and final exponentiation (pairing.h, with the cyclotomic squarings of the hard
+    part) give the CPU twin's e(P, Q)^3 on fixture points, and bls.Verify's verdicts on the golden chain."""
+    from oracle import twin
+
+    ch = load("chain_t3n5.json")
+    pk = hx(ch["pk"])
+    for r in ch["rounds"][:3]:
+        sig = hx(r["sig"])
+        out = ctypes.create_string_buffer(576)
+        assert hc.hc_pairing_cubed(pk, sig, out, 0) == 0
+        st, want = twin.pairing_cubed(pk, sig)
+        assert st == 0 and out.raw == want
+    for i, r in enumerate(ch["rounds"][:4]):
+        msg, sig = hx(r["msg"]), hx(ch["rounds"][(i + (i % 2)) % 64]["sig"])
+        assert hc.hc_verify(pk, msg, len(msg), sig) == (0 if i % 2 == 0 else 1)
