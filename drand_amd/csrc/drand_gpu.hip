@@ -31,10 +31,18 @@ struct Timing {
 // A workspace set: its own stream, grow-only device buffers and completion event.  Batches enqueued
 // through the asynchronous entry point rotate over kSets sets, so the latency-bound tail of one batch
 // (Miller loops, final exponentiation: a few workgroups) overlaps the throughput-bound head of the next.
-#ifndef DG_SETS
-#define DG_SETS 4
+#ifndef DG_MAX_SETS
+#define DG_MAX_SETS 8
 #endif
-constexpr int kSets = DG_SETS;
+constexpr int kSets = DG_MAX_SETS;  // capacity; DG_SETS (environment, default 4) sets are used
+int active_sets() {
+  static const int n = [] {
+    const char* e = getenv("DG_SETS");
+    int v = e ? atoi(e) : 4;
+    return v < 1 ? 1 : (v > kSets ? kSets : v);
+  }();
+  return n;
+}
 struct Set {
   hipStream_t stream = nullptr;
   std::vector<void*> pool;  // indexed by Slot
@@ -133,7 +141,7 @@ int ws(Slot s, size_t bytes, void** out) {
 int acquire_set(hipStream_t* st) {
   Ctx& c = g_ctx;
   int i = c.next;
-  c.next = (c.next + 1) % kSets;
+  c.next = (c.next + 1) % active_sets();
   Set& s = c.sets[i];
   if (s.busy) {
     HIPCHK(hipEventSynchronize(s.done));

@@ -29,6 +29,17 @@
 #else
 #define DGH DGN
 #endif
+// Fp12 / pairing level: out of line, except in the translation unit of the per-item pairing check
+// (kernels_verify.hip, DG_INLINE12=1), where Fp12 values passing through call frames in scratch memory
+// would dominate the kernel's traffic.
+#ifndef DG_INLINE12
+#define DG_INLINE12 0
+#endif
+#if DG_INLINE12
+#define DG12 DGI
+#else
+#define DG12 DGN
+#endif
 
 #include "bls_constants.h"
 #include "fp28.h"
@@ -610,7 +621,7 @@ DGH Fp6 fp6_sqr(const Fp6& a) {
   Fp2 c2 = fp2_sub(fp2_sub(fp2_add(fp2_add(s1, s2), s3), s0), s4);
   return Fp6{c0, c1, c2};
 }
-DGN Fp6 fp6_inv(const Fp6& a) {
+DG12 Fp6 fp6_inv(const Fp6& a) {
   Fp2 c0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
   Fp2 c1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
   Fp2 c2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
@@ -639,20 +650,20 @@ DGI bool fp12_is_one(const Fp12& a) {
          fp2_is_zero(a.c1.c1) && fp2_is_zero(a.c1.c2);
 }
 DGI Fp12 fp12_conj(const Fp12& a) { return Fp12{a.c0, fp6_neg(a.c1)}; }
-DGN Fp12 fp12_mul(const Fp12& a, const Fp12& b) {
+DG12 Fp12 fp12_mul(const Fp12& a, const Fp12& b) {
   Fp6 t0 = fp6_mul(a.c0, b.c0);
   Fp6 t1 = fp6_mul(a.c1, b.c1);
   Fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
   return Fp12{fp6_add(t0, fp6_mul_v(t1)), c1};
 }
-DGN Fp12 fp12_sqr(const Fp12& a) {
+DG12 Fp12 fp12_sqr(const Fp12& a) {
   // complex squaring: (a0 + a1 w)^2 = (a0^2 + v a1^2) + 2 a0 a1 w
   Fp6 ab = fp6_mul(a.c0, a.c1);
   Fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
   Fp6 c0 = fp6_sub(fp6_sub(s, ab), fp6_mul_v(ab));
   return Fp12{c0, fp6_add(ab, ab)};
 }
-DGN Fp12 fp12_inv(const Fp12& a) {
+DG12 Fp12 fp12_inv(const Fp12& a) {
   Fp6 t = fp6_sub(fp6_mul(a.c0, a.c0), fp6_mul_v(fp6_mul(a.c1, a.c1)));
   t = fp6_inv(t);
   return Fp12{fp6_mul(a.c0, t), fp6_neg(fp6_mul(a.c1, t))};
@@ -665,7 +676,7 @@ DGI void fp4_sqr(const Fp2& a, const Fp2& b, Fp2& c0, Fp2& c1) {
   c0 = fp2_add(fp2_mul_xi(t1), t0);
   c1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(a, b)), t0), t1);
 }
-DGN Fp12 fp12_cyc_sqr(const Fp12& f) {
+DG12 Fp12 fp12_cyc_sqr(const Fp12& f) {
   Fp2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
   Fp2 t0, t1, t2, t3;
   fp4_sqr(z0, z1, t0, t1);
@@ -682,7 +693,7 @@ DGN Fp12 fp12_cyc_sqr(const Fp12& f) {
 }
 
 // multiply by the sparse line l = c0 + c1 v + c4 v w (M-type twist; slots 0, 1, 4)
-DGN Fp12 fp12_mul_014(const Fp12& f, const Fp2& c0, const Fp2& c1, const Fp2& c4) {
+DG12 Fp12 fp12_mul_014(const Fp12& f, const Fp2& c0, const Fp2& c1, const Fp2& c4) {
   Fp6 aa = fp6_mul_01(f.c0, c0, c1);
   Fp6 bb = fp6_mul_1(f.c1, c4);
   Fp6 s = fp6_mul_01(fp6_add(f.c0, f.c1), c0, fp2_add(c1, c4));
@@ -690,7 +701,7 @@ DGN Fp12 fp12_mul_014(const Fp12& f, const Fp2& c0, const Fp2& c1, const Fp2& c4
   Fp6 n0 = fp6_add(fp6_mul_v(bb), aa);
   return Fp12{n0, n1};
 }
-DGN Fp12 fp12_frob(const Fp12& a) {
+DG12 Fp12 fp12_frob(const Fp12& a) {
   Fp2 g1 = fp2_const(FROB_G1), g2 = fp2_const(FROB_G2), d = fp2_const(FROB_D);
   Fp6 b0{fp2_conj(a.c0.c0), fp2_mul(fp2_conj(a.c0.c1), g1), fp2_mul(fp2_conj(a.c0.c2), g2)};
   Fp2 dg1 = fp2_mul(d, g1), dg2 = fp2_mul(d, g2);

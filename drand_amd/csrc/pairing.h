@@ -12,7 +12,7 @@ struct G2Proj {
   Fp2 x, y, z;
 };
 
-DGN void line_dbl(G2Proj& T, Fp2& c0, Fp2& c1, Fp2& c4, const Fp& px, const Fp& py) {
+DG12 void line_dbl(G2Proj& T, Fp2& c0, Fp2& c1, Fp2& c4, const Fp& px, const Fp& py) {
   Fp2 a = fp2_mul_fp(fp2_mul(T.x, T.y), fp_const(FP_TWO_INV));
   Fp2 b = fp2_sqr(T.y);
   Fp2 c = fp2_sqr(T.z);
@@ -30,7 +30,7 @@ DGN void line_dbl(G2Proj& T, Fp2& c0, Fp2& c1, Fp2& c4, const Fp& px, const Fp& 
   T.z = fp2_mul(b, h);
 }
 
-DGN void line_add(G2Proj& T, const Fp2& qx, const Fp2& qy, Fp2& c0, Fp2& c1, Fp2& c4, const Fp& px, const Fp& py) {
+DG12 void line_add(G2Proj& T, const Fp2& qx, const Fp2& qy, Fp2& c0, Fp2& c1, Fp2& c4, const Fp& px, const Fp& py) {
   Fp2 theta = fp2_sub(T.y, fp2_mul(qy, T.z));
   Fp2 lambda = fp2_sub(T.x, fp2_mul(qx, T.z));
   Fp2 c = fp2_sqr(theta);
@@ -76,7 +76,7 @@ DGI Fp12 miller_loop(const G1A* P, const G2A* Q, int np) {
 }
 
 // a^z for a in the cyclotomic subgroup (z < 0: conjugate of a^|z|), cyclotomic squarings
-DGN Fp12 cyc_exp_z(const Fp12& a) {
+DG12 Fp12 cyc_exp_z(const Fp12& a) {
   Fp12 acc = a;
   for (int b = 62; b >= 0; --b) {
     acc = fp12_cyc_sqr(acc);
@@ -85,7 +85,7 @@ DGN Fp12 cyc_exp_z(const Fp12& a) {
   return fp12_conj(acc);
 }
 
-DGN Fp12 final_exp_cubed(const Fp12& f) {
+DG12 Fp12 final_exp_cubed(const Fp12& f) {
   Fp12 f1 = fp12_mul(fp12_conj(f), fp12_inv(f));      // f^(p^6 - 1)
   Fp12 f2 = fp12_mul(fp12_frob(fp12_frob(f1)), f1);   // ^(p^2 + 1)
   Fp12 t0 = fp12_mul(cyc_exp_z(f2), fp12_conj(f2));   // f2^(z-1)
