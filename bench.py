@@ -53,14 +53,15 @@ def cpu_threads():
     return max(1, n)
 
 
-def traffic_of(kernel):
+def traffic_of(kernel, config="head"):
     """HBM-side bytes per launch of `kernel` from the committed PMC passes (profiles/traffic.json, made by
-    tools/traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench): 2 x
-    FETCH_SIZE + WRITE_SIZE (the gfx950 correction of FETCH_SIZE), or None without a profile."""
+    tools/traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench; config "head",
+    "c3" or "c5"): 2 x FETCH_SIZE + WRITE_SIZE (the gfx950 correction of FETCH_SIZE), or None without a
+    profile."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(p):
         return None
-    t = json.load(open(p)).get("kernels", {}).get(kernel)
+    t = json.load(open(p)).get("configs", {}).get(config, {}).get(kernel)
     return t["bytes_per_launch"] if t else None
 
 
@@ -93,20 +94,27 @@ def gpu_signed_rounds(lib_tbls, first, n, x):
     return prev, sigs
 
 
-def roofline_of(kt, kernel_units, peak, extra=None):
+def roofline_of(kt, kernel_units, peak, extra=None, config="head"):
     """Roofline object of the dominant kernel of a timing table {name: (avg us, launches)}: the kernel with
     the largest total time among those profiles/opcounts.json prices; kernel_units[name] = the units all its
     timed launches processed together (per launch: that / launches)."""
     oc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["per_unit"]
-    cands = [(us * n, name, us) for name, (us, n) in kt.items() if name in oc and name in kernel_units]
+    cands = [(us * n, name, us) for name, (us, n) in kt.items()
+             if name in kernel_units and (name in oc or isinstance(kernel_units[name], dict))]
     if not cands:
         return None
     _, name, us = max(cands)
-    macs = oc[name]["macs"]
-    units = kernel_units[name] / kt[name][1]
+    u = kernel_units[name]
+    if isinstance(u, dict):  # a mix of unit kinds {opcounts key: units}: MACs per unit averaged over the mix
+        total = sum(u.values())
+        macs = sum(c * oc[k]["macs"] for k, c in u.items()) / max(total, 1)
+        units = total / kt[name][1]
+    else:
+        macs = oc[name]["macs"]
+        units = u / kt[name][1]
     achieved = macs * units / (us * 1e-6) / 1e12
     out = {"bound": "valu-int", "achieved": achieved, "peak": peak["tmac_s"], "unit": "TMAC/s",
-           "frac": achieved / peak["tmac_s"], "traffic": traffic_of(name), "kernel": name, "kernel_avg_us": us,
+           "frac": achieved / peak["tmac_s"], "traffic": traffic_of(name, config), "kernel": name, "kernel_avg_us": us,
            "units_per_launch": units, "macs_per_unit": macs, "peak_source": peak["source"]}
     if extra:
         out.update(extra)
@@ -256,7 +264,7 @@ def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps
     L.check(L.lib().dg_set_timing(0))
     units = {"k_decode_items": R * n, "k_recover_terms": R * t, "k_h2c_uncleared": R, "k_exp_pm3d4": 4 * R + 2 * R * n,
              "k_dec_p1": R * n, "k_dec_p2": R * n, "k_dec_p3": R * n}
-    roof = roofline_of(kt, units, peak, {"timing": "HIP events on the launch stream, one dg_recover call"})
+    roof = roofline_of(kt, units, peak, {"timing": "HIP events on the launch stream, one dg_recover call"}, "c3")
     out = {"metric": "Recover/s at n=%d t=%d (all %d shares VerifyPartial'd, first t valid interpolated)" % (n, t, n),
            "value": R_total / (dt + gdt), "unit": "recovers/s", "n_gpus": world, "rounds": R_total,
            "rounds_per_gpu": R, "partials_per_round": n, "s_per_step": dt, "allgather_s": gdt,
@@ -268,7 +276,7 @@ def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps
     return out, (commits, msgs, parts)
 
 
-def adversarial_bench(L, tbls, shard, chain, R_total, world, rank, t=129, n=256, frac=0.10, n_short=3):
+def adversarial_bench(L, tbls, shard, chain, R_total, world, rank, peak, t=129, n=256, frac=0.10, n_short=3):
     """BASELINE configs[4]: n = 256, t = 129, ~10% of the (round, share) cells corrupted with the six
     cycling modes of tools/corrupt.py, plus `n_short` rounds with more than n - t corrupted shares (-> "not
     enough shares"); each rank its contiguous range of R_total rounds through dg_recover (the batch equation
@@ -318,9 +326,15 @@ def adversarial_bench(L, tbls, shard, chain, R_total, world, rank, t=129, n=256,
     (gs, grs, gss), gdt = timed_ranks(lambda: gather_recover(sigs, rs, ss, world, R_total), world)
     assert gs.shape == (R_total, 96) and gss.shape == (R_total, n)
     L.check(L.lib().dg_set_timing(1))
+    g0 = L.group_counts()
     tbls.recover_batch(pub, msgs, parts, t, n, seed=13)
     kt = L.timings()
+    g1 = L.group_counts()
     L.check(L.lib().dg_set_timing(0))
+    checks = {"k_verify_groups[%d]" % (m + 1): g1[m] - g0[m] for m in range(4)}
+    roof = roofline_of(kt, {"k_verify_groups": checks, "k_recover_terms": R * t}, peak,
+                       {"timing": "HIP events on the launch stream, one dg_recover call",
+                        "checks_by_members": checks}, "c5")
     ncorrupt = np.array([len(items)], np.int64)
     if world > 1:
         import torch
@@ -333,7 +347,7 @@ def adversarial_bench(L, tbls, shard, chain, R_total, world, rank, t=129, n=256,
             "value": R_total / (dt + gdt), "unit": "recovers/s", "n_gpus": world, "rounds": R_total,
             "rounds_per_gpu": R, "partials_per_round": n, "corrupted_shares": int(ncorrupt[0]),
             "short_rounds": n_short, "s_per_step": dt, "allgather_s": gdt,
-            "statuses_per_s": int((gss != 255).sum()) / (dt + gdt), "setup_s": gen_s,
+            "statuses_per_s": int((gss != 255).sum()) / (dt + gdt), "setup_s": gen_s, "roofline": roof,
             "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
             "note": "host-buffer C-ABI (dg_recover), PCIe transfer of %d MB of partials per GPU inside the timed "
                     "region; the batch equation fails, so the examined prefix of every round takes the per-item "
@@ -630,7 +644,7 @@ def main():
     if args.recover_rounds and rec_chain is not None:
         rec, rec_in = recover_bench(L, tbls, shard, rec_chain, args.recover_rounds, 33, 64, world, rank, peak)
     if args.c5_rounds and rec_chain is not None:
-        adv, adv_in = adversarial_bench(L, tbls, shard, rec_chain, args.c5_rounds, world, rank)
+        adv, adv_in = adversarial_bench(L, tbls, shard, rec_chain, args.c5_rounds, world, rank, peak)
     if rank == 0:
         if args.sync_rounds and rec_chain is not None:
             syn = sync_bench(rec_chain, args.sync_rounds)

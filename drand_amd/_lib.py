@@ -51,6 +51,7 @@ SIGNATURES = {
     "dg_wait_all": ([], _I),
     "dg_last_batch_flags": ([_P], _I),
     "dg_fallback_count": ([_P], _I),
+    "dg_group_counts": ([_P], _I),
     "dg_set_timing": ([_I], _I),
     "dg_last_timings": ([_P, _P, _P, _I], _I),
 }
@@ -142,6 +143,13 @@ def fallback_count():
     out = np.zeros(1, dtype=np.uint64)
     check(lib().dg_fallback_count(ptr(out)))
     return int(out[0])
+
+
+def group_counts():
+    """Recover's per-item pass since dg_init: [checks of 1, 2, 3, 4 shares of a round at once]."""
+    out = np.zeros(4, dtype=np.uint64)
+    check(lib().dg_group_counts(ptr(out)))
+    return [int(v) for v in out]
 
 
 def timings():

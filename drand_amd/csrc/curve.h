@@ -323,6 +323,118 @@ DGH G2J g2_mul_u256_psi_sel(const G2A& p, const uint32_t* k) {
   }
   return acc;
 }
+// The same product, regular: the four psi digits in the sign-aligned column form of Faz-Hernandez, Longa and
+// Sanchez ("Efficient and secure algorithms for GLV-based scalar multiplication", GLV-SAC).  With d0 made odd
+// (d0 + 1, corrected by one final subtraction of P), d0 = 2^64 + sum_{j<64} s_j 2^j with s_j = +-1, and every
+// other digit d_i = sum_{j<=64} s_j u_ij 2^j with u_ij in {0, 1}: each column is s_j T[u_1j + 2 u_2j + 4 u_3j],
+// T[u] = P_0 + u_1 P_1 + u_2 P_2 + u_3 P_3 (8 affine points, one batch inversion).  65 doublings and 65 mixed
+// additions whatever the lanes' scalars, against 64 + 256 for the select form: the Recover terms of rounds with
+// different share sets (divergent waves).  The table is indexed per lane, so it lives in scratch.  P_i are
+// multiples [|z|^i]P with 1 + |z| + |z|^2 + |z|^3 < r, so no table entry is the identity or +- another.
+DGH G2J g2_mul_u256_psi_sac(const G2A& p, const uint32_t* k) {
+  if (p.inf) return jac_infinity<Fp2>();
+  uint32_t q[8];
+  for (int w = 0; w < 8; ++w) q[w] = k[w];
+  uint64_t d[4];
+  d[0] = u256_divmod_u64(q, Z_ABS);
+  d[1] = u256_divmod_u64(q, Z_ABS);
+  d[2] = u256_divmod_u64(q, Z_ABS);
+  d[3] = (uint64_t)q[1] << 32 | q[0];
+  const bool even = (d[0] & 1) == 0;
+  const uint64_t k0 = d[0] + (even ? 1u : 0u);  // < Z_ABS + 1: no overflow
+  const uint64_t sgn = k0 >> 1;                  // bit j set: s_j = +1 (j < 64); s_64 = +1
+  uint64_t um[3];
+  uint32_t top = 0;  // u_{i,64}
+  for (int i = 0; i < 3; ++i) {
+    uint64_t a = d[i + 1], m = 0;
+    for (int j = 0; j < 64; ++j) {
+      const uint64_t bit = a & 1u;
+      m |= bit << j;
+      a = (a >> 1) + (bit & ~(sgn >> j) & 1u);  // b_j = -1: a = (a + 1) / 2
+    }
+    um[i] = m;
+    top |= (uint32_t)a << i;  // a is 0 or 1 here
+  }
+  // T[u], u = u1 + 2 u2 + 4 u3 (Jacobian, then one inversion of the product of the Z's)
+  Fp2 px[4], py[4];
+  px[0] = p.x;
+  py[0] = p.y;
+  for (int i = 1; i < 4; ++i) {
+    px[i] = px[i - 1];
+    py[i] = py[i - 1];
+    g2_psi_aff(px[i], py[i]);
+  }
+  py[1] = fp2_neg(py[1]);
+  py[3] = fp2_neg(py[3]);
+  G2J tj[8];
+  tj[0] = G2J{px[0], py[0], fp2_one()};
+  for (int u = 1; u < 8; ++u) {
+    const int hi = u & 4 ? 3 : (u & 2 ? 2 : 1);  // highest set bit of u -> P_hi
+    tj[u] = g2_madd_lean(tj[u & ~(1 << (hi - 1))], px[hi], py[hi]);
+  }
+  Fp2 pref[8];
+  pref[0] = fp2_one();
+  for (int u = 1; u < 8; ++u) pref[u] = fp2_mul(pref[u - 1], tj[u].z);
+  Fp2 inv = fp2_inv(pref[7]);
+  G2A tab[8];
+  tab[0] = G2A{px[0], py[0], false};
+  for (int u = 7; u >= 1; --u) {
+    const Fp2 zi = fp2_mul(inv, pref[u - 1]);
+    inv = fp2_mul(inv, tj[u].z);
+    const Fp2 zi2 = fp2_sqr(zi);
+    tab[u] = G2A{fp2_mul(tj[u].x, zi2), fp2_mul(tj[u].y, fp2_mul(zi2, zi)), false};
+  }
+  G2J acc{tab[top].x, tab[top].y, fp2_one()};
+  for (int j = 63; j >= 0; --j) {
+    acc = jac_dbl(acc);
+    const uint32_t u = (uint32_t)((um[0] >> j) & 1u) | (uint32_t)((um[1] >> j) & 1u) << 1 |
+                       (uint32_t)((um[2] >> j) & 1u) << 2;
+    const G2A t = tab[u];
+    const bool pos = (sgn >> j) & 1u;
+    acc = g2_madd_lean(acc, t.x, fp2_sel(pos, fp2_neg(t.y), t.y));  // fp2_sel(c, a, b) = c ? b : a
+  }
+  const G2J fix = g2_madd_lean(acc, px[0], fp2_neg(py[0]));
+  return G2J{fp2_sel(even, acc.x, fix.x), fp2_sel(even, acc.y, fix.y), fp2_sel(even, acc.z, fix.z)};
+}
+// sum_i [d_i] P_i over four points (any of them may be the identity) and 64-bit digits, by the same
+// sign-aligned column form with a Jacobian table (full additions, no inversion, every exceptional case
+// handled by jac_add): 65 doublings + 65 additions + 7 for the table, whatever the digits.  The random
+// linear combinations of the per-round group tests (kernels.h verify_group), in G1 and in G2.
+template <class F>
+DGH Jac<F> jac_msm4_sac(const Jac<F>* p, const uint64_t* d) {
+  const bool even = (d[0] & 1) == 0;
+  const uint64_t k0 = d[0] + (even ? 1u : 0u);  // even d0 <= 2^64 - 2: no overflow
+  const uint64_t sgn = k0 >> 1;
+  uint64_t um[3];
+  uint32_t top = 0;
+  for (int i = 0; i < 3; ++i) {
+    uint64_t a = d[i + 1], m = 0;
+    for (int j = 0; j < 64; ++j) {
+      const uint64_t bit = a & 1u;
+      m |= bit << j;
+      a = (a >> 1) + (bit & ~(sgn >> j) & 1u);
+    }
+    um[i] = m;
+    top |= (uint32_t)a << i;
+  }
+  Jac<F> tab[8];
+  tab[0] = p[0];
+  for (int u = 1; u < 8; ++u) {
+    const int hi = u & 4 ? 3 : (u & 2 ? 2 : 1);
+    tab[u] = jac_add(tab[u & ~(1 << (hi - 1))], p[hi]);
+  }
+  Jac<F> acc = tab[top];
+  for (int j = 63; j >= 0; --j) {
+    acc = jac_dbl(acc);
+    const uint32_t u = (uint32_t)((um[0] >> j) & 1u) | (uint32_t)((um[1] >> j) & 1u) << 1 |
+                       (uint32_t)((um[2] >> j) & 1u) << 2;
+    const Jac<F> t = tab[u];
+    const bool pos = (sgn >> j) & 1u;
+    acc = jac_add(acc, Jac<F>{t.x, f_sel(pos, f_neg(t.y), t.y), t.z});
+  }
+  const Jac<F> fix = jac_add(acc, jac_neg(p[0]));
+  return Jac<F>{f_sel(even, acc.x, fix.x), f_sel(even, acc.y, fix.y), f_sel(even, acc.z, fix.z)};
+}
 // P in G2  <=>  psi(P) == [z]P   (Scott, "A note on group membership tests for G1, G2 and GT")
 DGH bool g2_in_subgroup(const G2J& p) { return jac_eq(g2_psi(p), g2_mul_z(p)); }
 // the same test for an affine point (decoded signatures): [|z|]P by double-and-add from the top bit with

@@ -43,6 +43,15 @@ int active_sets() {
   }();
   return n;
 }
+// items per group test in Recover's per-item pass (kernels.h verify_group); DG_GROUP=1: every item alone
+uint32_t group_size() {
+  static const uint32_t n = [] {
+    const char* e = getenv("DG_GROUP");
+    int v = e ? atoi(e) : (int)GRP;
+    return (uint32_t)(v < 1 ? 1 : (v > (int)GRP ? (int)GRP : v));
+  }();
+  return n;
+}
 struct Set {
   hipStream_t stream = nullptr;
   std::vector<void*> pool;  // indexed by Slot
@@ -69,6 +78,7 @@ struct Ctx {
   uint8_t pk_bytes[48];
   bool pk_valid = false;
   unsigned long long* fallbacks = nullptr;  // device counter (k_count_fallback)
+  unsigned long long* gcount = nullptr;     // device counters: group checks by member count (k_verify_groups)
   // share keys X_i = PubPoly.Eval(i) of the multi-key paths for the last (commits, distinct indices):
   // a drand group verifies every round against the same polynomial (the reference's build caches X_i
   // per group too), and decode + Horner are latency-bound single-lane jobs of ~15 ms
@@ -501,19 +511,26 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
     // Recover: per-item checks over the examined prefix only, in passes that grow it by each round's deficit;
     // the last pass takes every unverified item before the t-th valid one, so the statuses Recover reads
     // are exact.  A passed batch marks nothing (only isolated items can be pending).
+    // Up to GRP fresh items of a round are checked together (kernels.h verify_group); the members of a failed
+    // group, and everything in the last pass, are checked alone.  DG_GROUP=1 checks every item alone.
     uint8_t* fin;
-    uint32_t* list;
+    uint32_t* glist;
     RET(wsT(S_FIN, N, &fin));
-    RET(wsT(S_LIST, (size_t)N + 1, &list));
+    RET(wsT(S_LIST, 4 * ((size_t)N + 1), &glist));
     RET(launch("k_prefix_init", k_prefix_init, N, 256, st, N, (const uint32_t*)flag, (const uint8_t*)iso,
                (const uint8_t*)b.status, fin));
-    constexpr int kPasses = 4;
+    // An empty pass costs two launches of returning lanes; the speculative margins (k_prefix_groups) keep
+    // the non-empty ones to ~3 at 10% corruption (a pass model over the C5 pattern: 1.75 s of per-item
+    // checks alone -> ~1.05 s).
+    const uint32_t grp = group_size();
+    constexpr int kPasses = 8;
     for (int pass = 0; pass <= kPasses; ++pass) {
-      HIPCHK(hipMemsetAsync(list, 0, 4, st));
-      RET(launch("k_prefix_mark", k_prefix_mark, b.R, 128, st, b.R, b.k, b.prefix_t, pass == kPasses ? 1u : 0u,
-                 (const uint8_t*)b.status, (const uint8_t*)fin, list));
-      RET(launch("k_verify_list", k_verify_list, N, 64, st, b.k, (const uint32_t*)list, b.keys, b.item_slot,
-                 (const G2AStore*)H, (const G2AStore*)b.S, b.status, fin, batched_sub));
+      HIPCHK(hipMemsetAsync(glist, 0, 4, st));
+      const uint32_t margin = grp < 2 ? 0u : (pass == 0 ? 6u : 2u);
+      RET(launch("k_prefix_groups", k_prefix_groups, b.R, 128, st, b.R, b.k, b.prefix_t, pass == kPasses ? 1u : 0u,
+                 grp, margin, (const uint8_t*)b.status, (const uint8_t*)fin, glist));
+      RET(launch("k_verify_groups", k_verify_groups, N, 64, st, b.k, (const uint32_t*)glist, seed, b.keys,
+                 b.item_slot, (const G2AStore*)H, (const G2AStore*)b.S, b.status, fin, batched_sub, g_ctx.gcount));
     }
   }
   RET(launch("k_count_fallback", k_count_fallback, 1, 64, st, (const uint32_t*)flag, g_ctx.fallbacks));
@@ -799,18 +816,25 @@ int dg_init(int device) {
     HIPCHK(hipMalloc(&g_ctx.fallbacks, sizeof(unsigned long long)));
     HIPCHK(hipMemset(g_ctx.fallbacks, 0, sizeof(unsigned long long)));
   }
+  if (!g_ctx.gcount) {
+    HIPCHK(hipMalloc(&g_ctx.gcount, GRP * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(g_ctx.gcount, 0, GRP * sizeof(unsigned long long)));
+  }
   // A hardware queue's scratch (private segment) grows on the first dispatch that needs more.  On MI355X
   // that growth, when it first happened inside an overlapped batch (the per-item kernels: ~14 KB per
   // lane), stalled every queue for ~0.5 s (rocprofv3 trace).  Dispatch the largest-scratch kernels once per
-  // workspace stream here, with zero items (every lane returns at once), so the growth happens now.
+  // workspace stream here, with zero items (every lane returns at once), so the growth happens now -- the
+  // largest first: a dispatch that needs a larger private segment than the queue's current one, right
+  // behind it, failed with HSA_STATUS_ERROR_OUT_OF_RESOURCES on the box.
   for (Set& x : g_ctx.sets) {
+    // glist[0] = 0 (the zeroed fallback counter): no groups
+    hipLaunchKernelGGL(k_verify_groups, dim3(1), dim3(64), 0, x.stream, 1u, (const uint32_t*)g_ctx.fallbacks,
+                       (const uint64_t*)nullptr, (const G1AStore*)nullptr, (const uint32_t*)nullptr,
+                       (const G2AStore*)nullptr, (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr, 0u,
+                       g_ctx.gcount);
     hipLaunchKernelGGL(k_verify_items, dim3(1), dim3(64), 0, x.stream, 0u, 1u, (const uint32_t*)nullptr,
                        (const G1AStore*)nullptr, (const uint32_t*)nullptr, (const G2AStore*)nullptr,
                        (const G2AStore*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, 0u);
-    // list[0] = 0 (the zeroed fallback counter): no items
-    hipLaunchKernelGGL(k_verify_list, dim3(1), dim3(64), 0, x.stream, 1u, (const uint32_t*)g_ctx.fallbacks,
-                       (const G1AStore*)nullptr, (const uint32_t*)nullptr, (const G2AStore*)nullptr,
-                       (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr, 0u);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipDeviceSynchronize());
@@ -839,12 +863,14 @@ void dg_shutdown(void) {
   if (g_ctx.pk_raw) (void)hipFree(g_ctx.pk_raw);
   if (g_ctx.pk_ready) (void)hipEventDestroy(g_ctx.pk_ready);
   if (g_ctx.fallbacks) (void)hipFree(g_ctx.fallbacks);
+  if (g_ctx.gcount) (void)hipFree(g_ctx.gcount);
   if (g_ctx.d_dst) (void)hipFree(g_ctx.d_dst);
   if (g_ctx.d_xmd) (void)hipFree(g_ctx.d_xmd);
   g_ctx.d_dst = nullptr;
   g_ctx.d_xmd = nullptr;
   g_ctx.dst_dev_valid = false;
   g_ctx.fallbacks = nullptr;
+  g_ctx.gcount = nullptr;
   if (g_ctx.poly_keys) (void)hipFree(g_ctx.poly_keys);
   if (g_ctx.poly_kst) (void)hipFree(g_ctx.poly_kst);
   if (g_ctx.poly_ready) (void)hipEventDestroy(g_ctx.poly_ready);
@@ -1089,6 +1115,17 @@ int dg_fallback_count(uint64_t* out) {
   unsigned long long v = 0;
   HIPCHK(hipMemcpy(&v, g_ctx.fallbacks, sizeof(v), hipMemcpyDeviceToHost));
   *out = v;
+  return 0;
+}
+
+int dg_group_counts(uint64_t* out4) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  if (!out4) return fail(DG_E_ARG, "bad arguments");
+  RET(wait_all());
+  unsigned long long v[GRP];
+  HIPCHK(hipMemcpy(v, g_ctx.gcount, sizeof(v), hipMemcpyDeviceToHost));
+  for (uint32_t m = 0; m < GRP; ++m) out4[m] = v[m];
   return 0;
 }
 

@@ -18,6 +18,12 @@
 #define DGI static inline
 #define DGN static
 #endif
+// pins a value in a register at this point (an optimisation barrier for the table selects of phases.h)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DG_PIN(x) asm volatile("" : "+v"(x))
+#else
+#define DG_PIN(x) asm volatile("" : "+r"(x))
+#endif
 // Code-size policy (DESIGN.md §code generation).  DGH marks the mid-level routines (Fp2/Fp6 products,
 // exponentiations, curve formulas): out of line by default (DG_FLAT=0), inlined into their kernels with
 // DG_FLAT=1.  DGN routines (Fp12 / pairing level) are always out of line.
@@ -29,9 +35,8 @@
 #else
 #define DGH DGN
 #endif
-// Fp12 / pairing level: out of line, except in the translation unit of the per-item pairing check
-// (kernels_verify.hip, DG_INLINE12=1), where Fp12 values passing through call frames in scratch memory
-// would dominate the kernel's traffic.
+// Fp12 / pairing level: out of line.  DG_INLINE12=1 inlines them into their callers, an A/B knob only:
+// built that way the per-item pairing kernel took a 24-minute compile and spilled ~19k VGPRs.
 #ifndef DG_INLINE12
 #define DG_INLINE12 0
 #endif

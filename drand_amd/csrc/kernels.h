@@ -473,20 +473,16 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_clear_rounds(uint32_t R, 
 // the per-item G2 subgroup check (batched on the MSM windows), so it is done here: a sigma outside G2
 // is a decode error, as in g2_decompress
 #if !DG_TU_HOT
-DGN void verify_item(size_t i, uint32_t k, const G1AStore* keys, const uint32_t* item_slot, const G2AStore* H,
-                     const G2AStore* S, uint8_t* status, uint32_t subgroup) {
-  G1A key = load_g1a(keys[item_slot ? item_slot[i] : 0u]);
-  G2A h = load_g2a(H[i / k]);
-  G2A s = load_g2a(S[i]);
-  if (subgroup && !s.inf && !g2_in_subgroup_aff(s.x, s.y)) {
-    status[i] = DG_ST_SIG_DECODE_;
-    return;
-  }
+// the Miller loop out of line, so its state and the final exponentiation's do not share one stack frame
+// (the per-item kernels' private segment must stay under the queue's scratch limit: ~14 KB per lane)
+DGN Fp12 miller_loop2(const G1A* P, const G2A* Q, int np) { return miller_loop<2>(P, Q, np); }
+// e(x, h) * e(-g1, s) == 1 (the identity's pairings dropped): kyber's bls.Verify equation
+DGN bool pair_check(const G1A& x, const G2A& h, const G2A& s) {
   G1A P[2];
   G2A Qa[2];
   int np = 0;
-  if (!key.inf && !h.inf) {
-    P[np] = key;
+  if (!x.inf && !h.inf) {
+    P[np] = x;
     Qa[np] = h;
     ++np;
   }
@@ -495,7 +491,16 @@ DGN void verify_item(size_t i, uint32_t k, const G1AStore* keys, const uint32_t*
     Qa[np] = s;
     ++np;
   }
-  bool good = np == 0 ? true : fp12_is_one(final_exp_cubed(miller_loop<2>(P, Qa, np)));
+  return np == 0 ? true : fp12_is_one(final_exp_cubed(miller_loop2(P, Qa, np)));
+}
+DGN void verify_item(size_t i, uint32_t k, const G1AStore* keys, const uint32_t* item_slot, const G2AStore* H,
+                     const G2AStore* S, uint8_t* status, uint32_t subgroup) {
+  const G2A s = load_g2a(S[i]);
+  if (subgroup && !s.inf && !g2_in_subgroup_aff(s.x, s.y)) {
+    status[i] = DG_ST_SIG_DECODE_;
+    return;
+  }
+  const bool good = pair_check(load_g1a(keys[item_slot ? item_slot[i] : 0u]), load_g2a(H[i / k]), s);
   status[i] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
 }
 
@@ -520,34 +525,131 @@ DG_KERNEL void __launch_bounds__(256) k_prefix_init(uint32_t n, const uint32_t* 
   if (i >= n) return;
   fin[i] = (status[i] != DG_ST_OK_ || (flag[0] && !isolate[i])) ? 1 : 0;
 }
-// per round: scanning in input order, the unverified items that could be among the first t valid ones if
-// every unverified item were valid (`all`: every unverified item before the t-th verified valid one) are
-// appended to list[1 + ...] (list[0] = count)
-DG_KERNEL void __launch_bounds__(128) k_prefix_mark(uint32_t R, uint32_t k, uint32_t t, uint32_t all,
-                                                   const uint8_t* status, const uint8_t* fin, uint32_t* list) {
-  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
-  uint32_t valid = 0, pending = 0;
-  for (uint32_t j = 0; j < k; ++j) {
-    size_t i = (size_t)r * k + j;
-    if (valid >= t || (!all && valid + pending >= t)) break;
-    if (fin[i]) {
-      if (status[i] == DG_ST_OK_) ++valid;
-    } else {
-      ++pending;
-      list[1 + atomicAdd(&list[0], 1u)] = (uint32_t)i;
+// ---- Group tests over the examined prefix.  With a corrupted fraction f of the shares, one pairing check
+// per examined item is more than Recover needs: up to GRP consecutive unverified items of one round are
+// checked together, e(sum_i rho_i X_i, H_r) == e(g1, sum_i rho_i S_i) with independent 64-bit rho_i from the
+// batch's bound seed.  Every S_i is in G2 (subgroup-checked here as in verify_item) and H_r is in G2, so a
+// member with x_i H_r != S_i makes the sum vanish for at most one rho_i value mod r: a group with a bad
+// member passes with probability <= 2^-64.  A passed group gives every member kyber's nil verdict; the
+// members of a failed group are marked for their own check (fin = FIN_RECHECK) in the next pass, which
+// decides every verdict Recover reads.  At f = 10% and GRP = 4 that is ~0.6 pairing checks per item.
+constexpr uint32_t GRP = 4;
+constexpr uint8_t FIN_PENDING = 0, FIN_DONE = 1, FIN_RECHECK = 2;
+constexpr uint64_t GROUP_TAG = 0x67726f7570746573ull;  // domain of rho_i, apart from alpha_r and beta_s
+// the members' weighted sums a = sum rho_i X_i, b = sum rho_i S_i; members failing the subgroup check are
+// decided here (decode error) and left out.  Returns the live members (their item indices in live[]).
+DGN uint32_t group_combine(const uint32_t* mem, uint32_t n, uint64_t seed, const G1AStore* keys,
+                           const uint32_t* item_slot, const G2AStore* S, uint8_t* status, uint8_t* fin,
+                           uint32_t subgroup, G1A& a, G2A& b, uint32_t* live) {
+  G1J xp[GRP];
+  G2J sp[GRP];
+  uint64_t rho[GRP];
+  uint32_t nl = 0;
+  for (uint32_t m = 0; m < n; ++m) {
+    const uint32_t i = mem[m];
+    const G2A s = load_g2a(S[i]);
+    // (a recheck was subgroup-checked by its group)
+    if (subgroup && fin[i] != FIN_RECHECK && !s.inf && !g2_in_subgroup_aff(s.x, s.y)) {
+      status[i] = DG_ST_SIG_DECODE_;
+      fin[i] = FIN_DONE;
+      continue;
     }
+    if (n == 1) {  // a share's own check: its key and signature as they are
+      a = load_g1a(keys[item_slot ? item_slot[i] : 0u]);
+      b = s;
+      live[0] = i;
+      return 1;
+    }
+    xp[nl] = jac_from_aff(load_g1a(keys[item_slot ? item_slot[i] : 0u]));
+    sp[nl] = jac_from_aff(s);
+    rho[nl] = rlc_coeff(seed ^ GROUP_TAG, i);
+    live[nl++] = i;
+  }
+  for (uint32_t m = nl; m < GRP; ++m) {
+    xp[m] = jac_infinity<Fp>();
+    sp[m] = jac_infinity<Fp2>();
+    rho[m] = 0;
+  }
+  if (nl) {
+    a = g1_to_aff(jac_msm4_sac(xp, rho));
+    b = g2_to_aff(jac_msm4_sac(sp, rho));
+  }
+  return nl;
+}
+DGN void verify_group(const uint32_t* mem, uint32_t n, uint32_t k, uint64_t seed, const G1AStore* keys,
+                      const uint32_t* item_slot, const G2AStore* H, const G2AStore* S, uint8_t* status,
+                      uint8_t* fin, uint32_t subgroup) {
+  G1A a;
+  G2A b;
+  uint32_t live[GRP];
+  const uint32_t nl = group_combine(mem, n, seed, keys, item_slot, S, status, fin, subgroup, a, b, live);
+  if (nl == 0) return;
+  // one call site of the pairing check for singles and groups alike: a wave holding both runs it once
+  const bool good = pair_check(a, load_g2a(H[mem[0] / k]), b);
+  if (n == 1) {
+    status[live[0]] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
+    fin[live[0]] = FIN_DONE;
+    return;
+  }
+  for (uint32_t m = 0; m < nl; ++m) {
+    if (good) status[live[m]] = DG_ST_OK_;
+    fin[live[m]] = good ? FIN_DONE : FIN_RECHECK;
   }
 }
-// lane g < list[0]: the per-item check of item list[1 + g]
-DG_KERNEL void __launch_bounds__(64) k_verify_list(uint32_t k, const uint32_t* list, const G1AStore* keys,
-                                                   const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
-                                                   uint8_t* status, uint8_t* fin, uint32_t subgroup) {
+// per round: scanning in input order, the unverified items up to the point where the round would reach
+// t + margin valid shares if every fresh unverified item were valid and every member of a failed group (bad
+// with probability ~1/3 at 10% corruption) counted one half -- a speculative margin, so that few rounds
+// need another pass (each costs one pairing's latency, ~60 ms); checking shares beyond the t-th valid one is
+// harmless, k_recover_select reports them not examined.  `all` (the last pass): every unverified item before
+// the t-th verified valid one, which makes the statuses Recover reads exact.  Into groups: glist[0] = count,
+// group g = glist[4 + 4g .. 8 + 4g) (item indices, ~0u = empty).  Consecutive fresh items of a round share a
+// group of up to `grp`; members of a failed group, and every item in the last pass, go alone.
+DG_KERNEL void __launch_bounds__(128) k_prefix_groups(uint32_t R, uint32_t k, uint32_t t, uint32_t all, uint32_t grp,
+                                                     uint32_t margin, const uint8_t* status, const uint8_t* fin,
+                                                     uint32_t* glist) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  uint32_t valid = 0, fresh = 0, rech = 0, cur[GRP], nc = 0;
+  auto emit = [&](const uint32_t* m, uint32_t c) {
+    uint32_t* g = glist + 4 + 4 * (size_t)atomicAdd(&glist[0], 1u);
+    for (uint32_t q = 0; q < GRP; ++q) g[q] = q < c ? m[q] : ~0u;
+  };
+  for (uint32_t j = 0; j < k; ++j) {
+    size_t i = (size_t)r * k + j;
+    if (valid >= t || (!all && 2 * (valid + fresh) + rech >= 2 * (t + margin))) break;
+    if (fin[i] == FIN_DONE) {
+      if (status[i] == DG_ST_OK_) ++valid;
+      continue;
+    }
+    if (fin[i] == FIN_RECHECK)
+      ++rech;
+    else
+      ++fresh;
+    const uint32_t one = (uint32_t)i;
+    if (all || grp < 2 || fin[i] == FIN_RECHECK) {
+      emit(&one, 1);
+    } else {
+      cur[nc++] = (uint32_t)i;
+      if (nc == grp) {
+        emit(cur, nc);
+        nc = 0;
+      }
+    }
+  }
+  if (nc) emit(cur, nc);
+}
+// lane g < glist[0]: group g (one member: the item's own check)
+DG_KERNEL void __launch_bounds__(64) k_verify_groups(uint32_t k, const uint32_t* glist, const uint64_t* seedp,
+                                                    const G1AStore* keys, const uint32_t* item_slot,
+                                                    const G2AStore* H, const G2AStore* S, uint8_t* status,
+                                                    uint8_t* fin, uint32_t subgroup, unsigned long long* cnt) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= list[0]) return;
-  uint32_t i = list[1 + g];
-  verify_item(i, k, keys, item_slot, H, S, status, subgroup);
-  fin[i] = 1;
+  if (g >= glist[0]) return;
+  const uint32_t* mem = glist + 4 + 4 * (size_t)g;
+  uint32_t n = 0;
+  while (n < GRP && mem[n] != ~0u) ++n;
+  atomicAdd(&cnt[n - 1], 1ull);
+  verify_group(mem, n, k, *seedp, keys, item_slot, H, S, status, fin, subgroup);
 }
 #endif
 
@@ -731,12 +833,16 @@ DG_KERNEL void __launch_bounds__(64, DG_HOT_WAVES) k_recover_terms(uint32_t R, u
   }
   Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, m);
   // one scalar for the whole wave (its rounds selected the same index set): the branching Straus is uniform;
-  // otherwise the select form (no divergence on the digits)
+  // otherwise the sign-aligned column form (65 doublings + 65 additions whatever the digits, no divergence)
   bool same = true;
 #pragma unroll
   for (int w = 0; w < 8; ++w) same = same && lam.l[w] == __builtin_amdgcn_readfirstlane(lam.l[w]);
   const G2A s = load_g2a(S[(size_t)r * k + sel[o]]);
+  #if DG_TERMS_SEL
   store_g2j(terms[o], __all(same) ? g2_mul_u256_psi(s, lam.l) : g2_mul_u256_psi_sel(s, lam.l));
+#else
+  store_g2j(terms[o], __all(same) ? g2_mul_u256_psi(s, lam.l) : g2_mul_u256_psi_sac(s, lam.l));
+#endif
 }
 #else
 DG_KERNEL void __launch_bounds__(64, DG_HOT_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,

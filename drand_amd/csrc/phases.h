@@ -49,18 +49,43 @@ constexpr uint32_t BINV_C = 32;  // chunk of the batch inversion (k_binv_*)
 // multiplications instead of 378 and 108 at width 3; tools/microbench/expchain.hip: -7%), SOS products in the
 // digit form.  The schedule is wave-uniform (scalar loads), the table entry is picked by a v_cndmask chain.
 DGI Fp fp_pow_pm3d4_sos(const Fp& x) {
-  uint32_t tab[8][14], x2[14], acc[14], nxt[14], m[14];
-  fp28_unpack(x.l, tab[0]);
+  // eight separately named entries, built and read with constant indices only: a table array whose build
+  // loop the compiler leaves rolled is indexed at run time and lives in scratch (10x the kernel's traffic)
+  uint32_t t0[14], t1[14], t2[14], t3[14], t4[14], t5[14], t6[14], t7[14], x2[14], acc[14], nxt[14], m[14];
+  fp28_unpack(x.l, t0);
   DG_COUNT_SQR();
-  fp28_sos_sqr_d(tab[0], x2);
+  fp28_sos_sqr_d(t0, x2);
+  DG_COUNT_MUL();
+  fp28_sos_mul_d(t0, x2, t1);
+  DG_COUNT_MUL();
+  fp28_sos_mul_d(t1, x2, t2);
+  DG_COUNT_MUL();
+  fp28_sos_mul_d(t2, x2, t3);
+  DG_COUNT_MUL();
+  fp28_sos_mul_d(t3, x2, t4);
+  DG_COUNT_MUL();
+  fp28_sos_mul_d(t4, x2, t5);
+  DG_COUNT_MUL();
+  fp28_sos_mul_d(t5, x2, t6);
+  DG_COUNT_MUL();
+  fp28_sos_mul_d(t6, x2, t7);
+  // m = t[q] for a wave-uniform q (v_cndmask chain; the empty asm keeps the chain from being folded into
+  // a load through a selected pointer)
+  auto pick = [&](int q) {
 #pragma unroll
-  for (int k = 1; k < 8; ++k) {
-    DG_COUNT_MUL();
-    fp28_sos_mul_d(tab[k - 1], x2, tab[k]);
-  }
-  const int first = EXP_PM3D4_W4_FIRST;
+    for (int d = 0; d < 14; ++d) {
+      uint32_t e[8] = {t0[d], t1[d], t2[d], t3[d], t4[d], t5[d], t6[d], t7[d]};
 #pragma unroll
-  for (int d = 0; d < 14; ++d) acc[d] = tab[first][d];
+      for (int j = 0; j < 8; ++j) DG_PIN(e[j]);
+      uint32_t v = e[0];
+#pragma unroll
+      for (int j = 1; j < 8; ++j) v = q == j ? e[j] : v;
+      m[d] = v;
+    }
+  };
+  pick(EXP_PM3D4_W4_FIRST);
+#pragma unroll
+  for (int d = 0; d < 14; ++d) acc[d] = m[d];
   for (int s = 0; s < EXP_PM3D4_W4_NSTEPS; ++s) {
     const int k = EXP_PM3D4_W4_STEPS[s][0];
     const int idx = EXP_PM3D4_W4_STEPS[s][1];
@@ -71,13 +96,7 @@ DGI Fp fp_pow_pm3d4_sos(const Fp& x) {
       for (int d = 0; d < 14; ++d) acc[d] = nxt[d];
     }
     if (idx >= 0) {
-#pragma unroll
-      for (int d = 0; d < 14; ++d) {
-        uint32_t v = tab[0][d];
-#pragma unroll
-        for (int q = 1; q < 8; ++q) v = idx == q ? tab[q][d] : v;
-        m[d] = v;
-      }
+      pick(idx);
       DG_COUNT_MUL();
       fp28_sos_mul_d(acc, m, nxt);
 #pragma unroll

@@ -147,6 +147,9 @@ int dg_last_batch_flags(uint32_t* out2);
 /* Number of batches since dg_init whose batch equation failed or that isolated items, i.e. ran the
  * per-item pass (waits for batches in flight).  A stream of valid batches keeps it at 0. */
 int dg_fallback_count(uint64_t* out);
+/* Recover's per-item pass since dg_init (waits for batches in flight): out4[m - 1] = checks of m shares of
+ * one round at once (m = 1: a share's own bls.Verify; m = 2..4: a random-linear-combination group test). */
+int dg_group_counts(uint64_t* out4);
 /* Wait for every batch enqueued by the asynchronous entry points. */
 int dg_wait_all(void);
 

@@ -40,6 +40,7 @@ EXPECT_TYPE(dg_verify_beacons_dev_async, int (*)(const uint8_t*, size_t, const u
                                                  void*, void*));
 EXPECT_TYPE(dg_last_batch_flags, int (*)(uint32_t*));
 EXPECT_TYPE(dg_fallback_count, int (*)(uint64_t*));
+EXPECT_TYPE(dg_group_counts, int (*)(uint64_t*));
 EXPECT_TYPE(dg_wait_all, int (*)(void));
 EXPECT_TYPE(dg_set_timing, int (*)(int));
 EXPECT_TYPE(dg_last_timings, int (*)(const char**, double*, int*, int));
@@ -80,6 +81,8 @@ int main() {
          dg_verify_beacons_dev_async(pk, 1, pr, rr, msg, off, sig, st, 1, nullptr, nullptr), DG_E_NODEV);
   expect("dg_last_batch_flags", dg_last_batch_flags(flags), DG_E_NODEV);
   expect("dg_fallback_count", dg_fallback_count(&u64), DG_E_NODEV);
+  uint64_t u64x4[4];
+  expect("dg_group_counts", dg_group_counts(u64x4), DG_E_NODEV);
   expect("dg_wait_all", dg_wait_all(), DG_E_NODEV);
   // host-only state works without a device
   expect("dg_set_timing", dg_set_timing(0), 0);

@@ -170,3 +170,27 @@ extern "C" int hc_g2_mul_sel_check(const uint8_t* sig96, const uint32_t* k8) {
   if (!g2_decompress(a, sig96, true)) return -1;
   return jac_eq(g2_mul_u256_psi_sel(a, k8), g2_mul_u256_psi(a, k8)) ? 1 : 0;
 }
+// the same product by the sign-aligned column form (GLV-SAC): 1 if it agrees with the branching psi-Straus
+extern "C" int hc_g2_mul_sac_check(const uint8_t* sig96, const uint32_t* k8) {
+  G2A a;
+  if (!g2_decompress(a, sig96, true)) return -1;
+  return jac_eq(g2_mul_u256_psi_sac(a, k8), g2_mul_u256_psi(a, k8)) ? 1 : 0;
+}
+
+// sum_i [d_i] P_i by the four-point sign-aligned column form (curve.h jac_msm4_sac), in G2 on four signatures
+// and in G1 on four keys, against double-and-add per point; bit i of inf_mask replaces point i by the
+// identity.  1 if both agree.
+extern "C" int hc_msm4_check(const uint8_t* sigs384, const uint8_t* keys192, const uint64_t* d, uint32_t inf_mask) {
+  G2J s[4], s_ref = jac_infinity<Fp2>();
+  G1J x[4], x_ref = jac_infinity<Fp>();
+  for (int i = 0; i < 4; ++i) {
+    G2A a;
+    G1A b;
+    if (!g2_decompress(a, sigs384 + 96 * i, true) || !g1_decompress(b, keys192 + 48 * i, true)) return -1;
+    s[i] = (inf_mask >> i) & 1 ? jac_infinity<Fp2>() : jac_from_aff(a);
+    x[i] = (inf_mask >> i) & 1 ? jac_infinity<Fp>() : jac_from_aff(b);
+    s_ref = jac_add(s_ref, jac_mul_u64(s[i], d[i]));
+    x_ref = jac_add(x_ref, jac_mul_u64(x[i], d[i]));
+  }
+  return jac_eq(jac_msm4_sac(s, d), s_ref) && jac_eq(jac_msm4_sac(x, d), x_ref) ? 1 : 0;
+}

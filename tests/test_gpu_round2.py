@@ -263,3 +263,52 @@ def test_sharded_1m_chain_equals_one_batch():
     m = max(len(b) for b in bits)
     flat = shard.unpack_bits(np.concatenate([np.pad(b, (0, m - len(b))) for b in bits]), sizes)
     assert np.array_equal(flat, (one != 0).astype(np.uint8))
+
+
+def test_group_tests_reject_cancelling_errors():
+    """Recover's per-item pass checks up to four fresh shares of a round together (random 64-bit weights
+    from the bound seed, kernels.h verify_group).  Shares crafted so their errors cancel in the unweighted sum
+    (sigma'_0 = sigma_0 + E, sigma'_1 = sigma_1 - E in the same group; E, -2E, +E spread over a group of
+    three) fail the weighted group test and are rejected one by one; clean groups pass.  Statuses and
+    recovered signatures equal the twin's."""
+    t, n, R = 5, 12, 6
+    coeffs, commits, shares = group(t, n)
+    msgs = [hashlib.sha256(b"grp/%d" % r).digest() for r in range(R)]
+    parts = tbls.sign_batch([v for _ in range(R) for _, v in shares], [m for m in msgs for _ in range(n)],
+                            [i for _ in range(R) for i, _ in shares]).reshape(R, n, 98)
+    E = B.G2C.mul(B.G2_GEN, 24681357)
+
+    def shift(r, j, mult):
+        s = B.g2_decompress(bytes(parts[r, j, 2:]))
+        parts[r, j, 2:] = np.frombuffer(B.g2_compress(B.G2C.add(s, B.G2C.mul(E, mult % B.R))), np.uint8)
+
+    shift(0, 0, 1), shift(0, 1, -1)                  # one cancelling pair in the first group
+    shift(2, 4, 1), shift(2, 5, -2), shift(2, 6, 1)  # three in the second group, sum zero
+    shift(3, 1, 3), shift(3, 2, -3), shift(3, 9, 1)  # a pair plus a lone bad share further on
+    pub = tbls.PubPoly(commits)
+    sigs, rs, ss = tbls.recover_batch(pub, msgs, parts, t, n, seed=21)
+    tw = twin.recover_batch(commits, t, n, np.array([list(m) for m in msgs], np.uint8), parts, 8)
+    assert np.array_equal(rs, tw[1]) and np.array_equal(ss, tw[2]) and np.array_equal(sigs, tw[0])
+    assert ss[0, :2].tolist() == [1, 1] and ss[2, 4:7].tolist() == [1, 1, 1] and ss[3, 1:3].tolist() == [1, 1]
+    assert not rs.any() and all(bytes(sigs[r]) == twin.sign(coeffs[0], msgs[r]) for r in range(R))
+
+
+def test_clean_groups_pass_on_the_group_path():
+    """A Recover batch whose batch equation fails for one bad share in round 0: every other round's group
+    tests must pass (only round 0's failed group goes to single checks).  Counted with dg_group_counts: a
+    failed clean group would add four single checks; at most one tail share per round (t = 5 plus the
+    speculative margin) and round 0's rechecks and replacement are checked alone."""
+    t, n, R = 5, 12, 40
+    coeffs, commits, shares = group(t, n)
+    msgs = [hashlib.sha256(b"clean/%d" % r).digest() for r in range(R)]
+    parts = tbls.sign_batch([v for _ in range(R) for _, v in shares], [m for m in msgs for _ in range(n)],
+                            [i for _ in range(R) for i, _ in shares]).reshape(R, n, 98)
+    parts[0, 2, 2:] = np.frombuffer(twin.sign((shares[2][1] + 1) % S.R, msgs[0]), np.uint8)
+    pub = tbls.PubPoly(commits)
+    g0 = L.group_counts()
+    sigs, rs, ss = tbls.recover_batch(pub, msgs, parts, t, n, seed=23)
+    g1 = L.group_counts()
+    d = [b - a for a, b in zip(g0, g1)]
+    assert not rs.any() and ss[0, :6].tolist() == [0, 0, 1, 0, 0, 0]
+    if d[3]:  # group tests enabled (DG_GROUP unset)
+        assert d[3] >= R and d[0] <= R + 5, d

@@ -76,6 +76,42 @@ def test_g2_mul_psi_decomposition_host_build(hc):
         k8 = (ctypes.c_uint32 * 8)(*[(k >> (32 * w)) & 0xFFFFFFFF for w in range(8)])
         assert hc.hc_g2_mul_psi_check(sig, k8) == 1, hex(k)
         assert hc.hc_g2_mul_sel_check(sig, k8) == 1, hex(k)  # the select form of divergent Recover waves
+        assert hc.hc_g2_mul_sac_check(sig, k8) == 1, hex(k)  # the sign-aligned column form
+
+
+def test_g2_mul_sac_digit_edges_host_build(hc):
+    """The sign-aligned column recoding (curve.h g2_mul_u256_psi_sac) at digit edges: even and odd d0,
+    zero digits, digits z - 1 (the longest carry chains of the recoding), single high bits."""
+    z = 0xD201000000010000
+    sig = hx(load("chain_t3n5.json")["rounds"][5]["sig"])
+    edge = [0, 1, 2, 3, z - 1, z - 2, 1 << 63, (1 << 63) + 1, 0x5555555555555555, 0xAAAAAAAAAAAAAAAA % z]
+    rng = random.Random(12)
+    cases = [(a, b, c, d) for a in edge[:6] for b, c, d in ((0, 0, 0), (z - 1, z - 1, z - 1), (1, 0, 1))]
+    cases += [tuple(rng.choice(edge) for _ in range(4)) for _ in range(24)]
+    for d in cases:
+        k = d[0] + d[1] * z + d[2] * z * z + d[3] * z ** 3
+        if k >= B.R:
+            continue
+        k8 = (ctypes.c_uint32 * 8)(*[(k >> (32 * w)) & 0xFFFFFFFF for w in range(8)])
+        assert hc.hc_g2_mul_sac_check(sig, k8) == 1, [hex(x) for x in d]
+
+
+def test_msm4_sac_host_build(hc):
+    """The four-point sign-aligned column combination of the group tests (curve.h jac_msm4_sac) in G1 and G2
+    equals per-point double-and-add: odd / even / zero / all-ones digits, repeated points (P_0 = P_1) and
+    identities."""
+    rounds = load("chain_t3n5.json")["rounds"]
+    keys = [hx(k) for k in load("groups.json")["t3"]]
+    sigs = [hx(rounds[i]["sig"]) for i in range(4)]
+    rng = random.Random(13)
+    M = (1 << 64) - 1
+    digs = [(1, 1, 1, 1), (0, 0, 0, 0), (2, 0, 0, 0), (M, M, M, M), (M - 1, 1, M, 0), (1 << 63, 3, 5, 7)]
+    digs += [tuple(rng.getrandbits(64) for _ in range(4)) for _ in range(10)]
+    for n, d in enumerate(digs):
+        for mask, ss, kk in ((0, sigs, keys[:3] + keys[:1]), (0b0110, sigs, keys[:3] + keys[:1]),
+                             (0, [sigs[0], sigs[0]] + sigs[2:], [keys[0], keys[0]] + keys[1:3]), (0b0001, sigs, keys[:3] + keys[:1])):
+            dd = (ctypes.c_uint64 * 4)(*d)
+            assert hc.hc_msm4_check(b"".join(ss), b"".join(kk), dd, mask) == 1, (n, mask, [hex(x) for x in d])
 
 
 def test_wordwise_xmd_matches_bytewise(hc):

@@ -15,3 +15,15 @@ print("roofline", r.get("kernel"), "frac %.3f" % r.get("frac", 0), "us %.0f" % r
 print("iso", d.get("kernel_avg_us_isolated"))
 print("ovl", d.get("kernel_avg_us"))
 PY
+if [ -n "$C5" ]; then
+  timeout -k 10 300 python -u bench.py --steps 1 --warmup 1 --recover-rounds ${C3_ROUNDS:-0} --c5-rounds 10000 --sync-rounds 0 --no-c1 --no-cpu-baseline > gpurun_out/bench_c5.json 2> gpurun_out/bench_c5.err || { echo "c5 bench failed"; tail -30 gpurun_out/bench_c5.err; exit 1; }
+  python3 - <<'PY'
+import json
+d = json.loads(open("gpurun_out/bench_c5.json").read().strip().splitlines()[-1])
+for key in ("recover", "adversarial"):
+    a = d.get(key)
+    if a:
+        kt = sorted(a["kernel_avg_us"].items(), key=lambda x: -x[1])[:8]
+        print(key, "%.0f recovers/s" % a["value"], "s/step %.3f" % a["s_per_step"], kt)
+PY
+fi

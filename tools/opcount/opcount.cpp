@@ -210,3 +210,40 @@ void oc_recover_term(const uint8_t* sig96, const uint32_t* lam8, uint64_t* out) 
   take(out);
 }
 }
+
+// Recover's per-item pass (kernels.h k_verify_groups) for a check of m shares of one round (pk48s: m keys,
+// sigs: m signatures, h from msg): m subgroup checks, for m > 1 the two weighted sums (jac_msm4_sac in G1
+// and G2) and their affine forms, then one two-pair pairing check.  The cleared hash H_r is per round
+// (k_clear_rounds), not counted.
+extern "C" void oc_verify_group(const uint8_t* pk48s, const uint8_t* msg, const uint8_t* dst, uint32_t dl,
+                                const uint8_t* sigs96, uint32_t m, uint64_t* out) {
+  G2J q = hash_to_g2_uncleared(msg, 32, dst, dl);
+  G2A h = g2_to_aff(g2_clear_cofactor(q));
+  G1A pk[4];
+  G2A s[4];
+  for (uint32_t i = 0; i < m; ++i) {
+    g1_decompress(pk[i], pk48s + 48 * i, false);
+    g2_decompress(s[i], sigs96 + 96 * i, false);
+  }
+  reset();
+  for (uint32_t i = 0; i < m; ++i) (void)g2_in_subgroup_aff(s[i].x, s[i].y);
+  G1A a = pk[0];
+  G2A b = s[0];
+  if (m > 1) {
+    G1J xp[4];
+    G2J sp[4];
+    uint64_t rho[4];
+    for (uint32_t i = 0; i < 4; ++i) {
+      xp[i] = i < m ? jac_from_aff(pk[i]) : jac_infinity<Fp>();
+      sp[i] = i < m ? jac_from_aff(s[i]) : jac_infinity<Fp2>();
+      rho[i] = i < m ? rlc_coeff(0x5eed, i) : 0;
+    }
+    a = g1_to_aff(jac_msm4_sac(xp, rho));
+    b = g2_to_aff(jac_msm4_sac(sp, rho));
+  }
+  G1A P[2] = {a, G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false}};
+  G2A Q[2] = {h, b};
+  bool ok = fp12_is_one(final_exp_cubed(miller_loop<2>(P, Q, 2)));
+  (void)ok;
+  take(out);
+}

@@ -73,6 +73,10 @@ def main():
         if i < 8:
             L.oc_verify_item(pk, msg, 32, DST, len(DST), sig, o)
             add("k_verify_items")
+            nxt4 = b"".join(bytes.fromhex(rounds[(i + q) % len(rounds)]["sig"]) for q in range(4))
+            for m in range(1, 5):
+                L.oc_verify_group(pk * m, msg, DST, len(DST), nxt4[:96 * m], m, o)
+                add("k_verify_groups[%d]" % m)
             L.oc_batch_final(pk, sig, nxt, o)
             add("k_pair_miller+k_final_check")
     out = {"mac_per_mul": MAC_MUL, "mac_per_sqr": MAC_SQR, "mac_per_inv": MAC_INV, "sample": "tests/golden/chain_t3n5.json (64 rounds)",

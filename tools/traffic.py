@@ -1,8 +1,12 @@
-"""rocprofv3 --pmc CSVs (separate FETCH_SIZE / WRITE_SIZE / SQ_* passes of `bench.py --sync --steps 1`)
--> profiles/traffic.json (per-kernel HBM-side bytes per launch, read by bench.py) and a per-kernel counter
-summary CSV.  Tooling only.
+"""rocprofv3 --pmc CSVs -> profiles/traffic.json (per-kernel HBM-side bytes per launch, read by bench.py's
+roofline objects) and a per-kernel counter summary CSV.  Tooling only.
 
-    python tools/traffic.py gpurun_out/prof profiles/r1_pmc_summary.csv
+    python tools/traffic.py gpurun_out/r2prof profiles/r2_pmc_summary.csv
+
+The profile directory holds one rocprofv3 output directory per counter pass, named pmc_<config>_<counter>
+(tools/gpu/profile_r2.sh): config "head" = bench.py --sync --steps 1 (the headline batches), "c3" = the
+Recover run at BASELINE configs[2], "c5" = the adversarial Recover run at configs[4].  Values are averaged
+over every dispatch of a kernel in the run, the same launch mix as bench.py's per-launch kernel averages.
 
 FETCH_SIZE and WRITE_SIZE are in KB per dispatch.  On gfx950 FETCH_SIZE counts half the bytes of wide
 coalesced reads (MI355X_MICROARCH.md, HBM section), so bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
@@ -12,38 +16,50 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def load(prof):
-    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    """{config: {kernel: {counter: mean value per dispatch}}}"""
+    acc = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(list)))
     for f in glob.glob(os.path.join(prof, "pmc_*", "*counter_collection.csv")):
+        m = re.match(r"pmc_([a-z0-9]+)_", os.path.basename(os.path.dirname(f)))
+        cfg = m.group(1) if m else "head"
+        per = collections.defaultdict(float)
+        names = {}
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"]
-            if not name.startswith("k_"):
+            if not r["Kernel_Name"].startswith("k_"):
                 continue
-            acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+            per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+            names[r["Dispatch_Id"]] = r["Kernel_Name"]
+        for (d, c), v in per.items():
+            acc[cfg][names[d]][c].append(v)
+    return {cfg: {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in ks.items()} for cfg, ks in acc.items()}
 
 
 def main(prof, out_csv):
     m = load(prof)
-    kernels = {}
-    for k, c in sorted(m.items()):
-        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            kernels[k] = {"fetch_kb": c["FETCH_SIZE"], "write_kb": c["WRITE_SIZE"],
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate runs per counter (tools/gpu/profile_r2.sh); "
+                     "bytes = 2 * FETCH_SIZE + WRITE_SIZE (gfx950); head = bench.py --sync --steps 1, c3 = Recover "
+                     "configs[2], c5 = adversarial Recover configs[4]", "configs": {}}
+    for cfg, ks in sorted(m.items()):
+        sec = {}
+        for k, c in sorted(ks.items()):
+            if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                sec[k] = {"fetch_kb": c["FETCH_SIZE"], "write_kb": c["WRITE_SIZE"],
                           "bytes_per_launch": 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024}
-    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate runs of bench.py --sync --steps 1 "
-                         "--warmup 1 (tools/gpu/profile.sh); bytes = 2 * FETCH_SIZE + WRITE_SIZE (gfx950)",
-               "kernels": kernels}, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
-    cols = sorted({c for cs in m.values() for c in cs})
+        out["configs"][cfg] = sec
+    json.dump(out, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
+    cols = sorted({c for ks in m.values() for cs in ks.values() for c in cs})
     with open(out_csv, "w", newline="") as f:
         w = csv.writer(f)
-        w.writerow(["kernel"] + cols)
-        for k, cs in sorted(m.items()):
-            w.writerow([k] + ["%.6g" % cs[c] if c in cs else "" for c in cols])
+        w.writerow(["config", "kernel"] + cols)
+        for cfg, ks in sorted(m.items()):
+            for k, cs in sorted(ks.items()):
+                w.writerow([cfg, k] + ["%.6g" % cs[c] if c in cs else "" for c in cols])
     print(open(out_csv).read())
 
 
