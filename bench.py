@@ -204,16 +204,17 @@ def make_group_rounds(tbls, chain_sigs, first, R, t, n):
 
 
 def gather_recover(sigs, rs, ss, world, total):
-    """All-gather of the Recover outputs of every rank's contiguous range (RCCL) -> numpy (total, ...)."""
+    """All-gather of the Recover outputs of every rank's contiguous range (RCCL; device tensors from
+    dg_recover_dev go in as they are) -> numpy (total, ...)."""
     import torch
 
     from drand_amd import shard
 
-    if world == 1:
-        return sigs, rs, ss
     dev = torch.device("cuda", torch.cuda.current_device())
-    out = [shard.allgather_rows(torch.from_numpy(np.ascontiguousarray(x)).to(dev), world, total).cpu().numpy()
-           for x in (sigs, rs, ss)]
+    xs = [x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (sigs, rs, ss)]
+    if world > 1:
+        xs = [shard.allgather_rows(x, world, total) for x in xs]
+    out = [x.cpu().numpy() for x in xs]
     return out[0], out[1].reshape(-1), out[2]
 
 
@@ -246,20 +247,28 @@ def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps
     a, b = shard.round_range(R_total, world, rank)
     R = b - a
     t0 = time.perf_counter()
+    import torch
+
     pub, commits, shares, msgs, parts = make_group_rounds(tbls, chain, a + 1, R, t, n)
     gen_s = time.perf_counter() - t0
-    tbls.recover_batch(pub, msgs, parts, t, n, seed=5)  # warmup (workspace growth)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    d_msgs = torch.from_numpy(np.ascontiguousarray(msgs)).to(dev)
+    d_parts = torch.from_numpy(np.ascontiguousarray(parts)).to(dev)
+    tbls.recover_batch_dev(pub, d_msgs, d_parts, t, n, seed=5)  # warmup (workspace growth)
     dts = []
     for s in range(steps):
-        (sigs, rs, ss), dt = timed_ranks(lambda: tbls.recover_batch(pub, msgs, parts, t, n, seed=6 + s), world)
+        (sigs, rs, ss), dt = timed_ranks(lambda: tbls.recover_batch_dev(pub, d_msgs, d_parts, t, n, seed=6 + s), world)
         dts.append(dt)
     (gs, grs, gss), gdt = timed_ranks(lambda: gather_recover(sigs, rs, ss, world, R_total), world)
     assert not grs.any() and np.array_equal(gs, chain[:R_total]), "recovered signatures differ from the chain"
     assert (gss[:, :t] == 0).all() and (gss[:, t:] == 255).all(), "share statuses"
     dt = min(dts)
+    # the host-buffer entry point (dg_recover): the 98 B partials cross PCIe inside the call
+    (hs, hrs, hss), host_dt = timed_ranks(lambda: tbls.recover_batch(pub, msgs, parts, t, n, seed=7), world)
+    assert np.array_equal(hs, gs[a:b]) and np.array_equal(hss, gss[a:b]), "host and device Recover differ"
     # per-kernel timing of one more call: the dominant kernel's roofline
     L.check(L.lib().dg_set_timing(1))
-    tbls.recover_batch(pub, msgs, parts, t, n, seed=9)
+    tbls.recover_batch_dev(pub, d_msgs, d_parts, t, n, seed=9)
     kt = L.timings()
     L.check(L.lib().dg_set_timing(0))
     units = {"k_decode_items": R * n, "k_recover_terms": R * t, "k_h2c_uncleared": R, "k_exp_pm3d4": 4 * R + 2 * R * n,
@@ -269,10 +278,11 @@ def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps
            "value": R_total / (dt + gdt), "unit": "recovers/s", "n_gpus": world, "rounds": R_total,
            "rounds_per_gpu": R, "partials_per_round": n, "s_per_step": dt, "allgather_s": gdt,
            "partials_verified_per_s": R_total * n / (dt + gdt), "partials_generated_s": gen_s,
+           "host_api_s_per_step": host_dt, "host_api_value": R_total / (host_dt + gdt),
            "roofline": roof, "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
-           "note": "host-buffer C-ABI (dg_recover): PCIe transfer of %d MB of partials per GPU inside the timed "
-                   "region; outputs all-gathered (RCCL) and equal to the chain's signatures"
-                   % (R * n * 98 // 10**6)}
+           "note": "inputs resident in HBM (dg_recover_dev), outputs all-gathered (RCCL) and equal to the chain's "
+                   "signatures; host_api_value: the host-buffer dg_recover, with the PCIe transfer of %d MB of "
+                   "partials per GPU inside the call" % (R * n * 98 // 10**6)}
     return out, (commits, msgs, parts)
 
 
@@ -316,18 +326,26 @@ def adversarial_bench(L, tbls, shard, chain, R_total, world, rank, peak, t=129, 
     bad = np.zeros((R, n), dtype=bool)
     for r, j, _ in items:
         bad[r, j] = True
-    tbls.recover_batch(pub, msgs, parts, t, n, seed=11)  # warmup
-    (sigs, rs, ss), dt = timed_ranks(lambda: tbls.recover_batch(pub, msgs, parts, t, n, seed=12), world)
+    import torch
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    d_msgs = torch.from_numpy(np.ascontiguousarray(msgs)).to(dev)
+    d_parts = torch.from_numpy(np.ascontiguousarray(parts)).to(dev)
+    tbls.recover_batch_dev(pub, d_msgs, d_parts, t, n, seed=11)  # warmup
+    (d_sigs, d_rs, d_ss), dt = timed_ranks(lambda: tbls.recover_batch_dev(pub, d_msgs, d_parts, t, n, seed=12), world)
+    sigs, rs, ss = (x.cpu().numpy() for x in (d_sigs, d_rs, d_ss))
+    (hs, hrs, hss), host_dt = timed_ranks(lambda: tbls.recover_batch(pub, msgs, parts, t, n, seed=12), world)
+    assert np.array_equal(hs, sigs) and np.array_equal(hrs, rs) and np.array_equal(hss, ss), "host / device differ"
     ok_r = np.array([r not in short for r in range(R)], dtype=bool)
     assert np.array_equal(rs != 0, ~ok_r) and (rs[~ok_r] == 5).all(), "round statuses"
     assert np.array_equal(sigs[ok_r], chain[a:b][ok_r]), "recovered signatures differ from the chain"
     examined = ss != 255
     assert (ss[examined & bad] != 0).all() and (ss[examined & ~bad] == 0).all(), "share statuses"
-    (gs, grs, gss), gdt = timed_ranks(lambda: gather_recover(sigs, rs, ss, world, R_total), world)
+    (gs, grs, gss), gdt = timed_ranks(lambda: gather_recover(d_sigs, d_rs, d_ss, world, R_total), world)
     assert gs.shape == (R_total, 96) and gss.shape == (R_total, n)
     L.check(L.lib().dg_set_timing(1))
     g0 = L.group_counts()
-    tbls.recover_batch(pub, msgs, parts, t, n, seed=13)
+    tbls.recover_batch_dev(pub, d_msgs, d_parts, t, n, seed=13)
     kt = L.timings()
     g1 = L.group_counts()
     L.check(L.lib().dg_set_timing(0))
@@ -348,10 +366,12 @@ def adversarial_bench(L, tbls, shard, chain, R_total, world, rank, peak, t=129, 
             "rounds_per_gpu": R, "partials_per_round": n, "corrupted_shares": int(ncorrupt[0]),
             "short_rounds": n_short, "s_per_step": dt, "allgather_s": gdt,
             "statuses_per_s": int((gss != 255).sum()) / (dt + gdt), "setup_s": gen_s, "roofline": roof,
+            "host_api_s_per_step": host_dt, "host_api_value": R_total / (host_dt + gdt),
             "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
-            "note": "host-buffer C-ABI (dg_recover), PCIe transfer of %d MB of partials per GPU inside the timed "
-                    "region; the batch equation fails, so the examined prefix of every round takes the per-item "
-                    "pairing check; outputs all-gathered (RCCL)" % (R * n * 98 // 10**6)}, (commits, msgs, parts,
+            "note": "inputs resident in HBM (dg_recover_dev); the batch equation fails, so the examined prefix of "
+                    "every round takes the per-item pass (group tests, then single checks); outputs all-gathered "
+                    "(RCCL); host_api_value: the host-buffer dg_recover with the PCIe transfer of %d MB of partials "
+                    "per GPU inside the call" % (R * n * 98 // 10**6)}, (commits, msgs, parts,
                                                                                              ss, rs)
 
 

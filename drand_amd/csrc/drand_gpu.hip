@@ -124,7 +124,8 @@ enum Slot {
   S_COMMITS, S_COMMITST, S_SLOTIDX, S_ITEMSLOT, S_SEL, S_SELIDX, S_RST, S_SST, S_TERMS, S_IN0, S_IN1, S_IN2, S_IN3,
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
-  S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_BINV, S_NV, S_NVINV, S_COUNT
+  S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_BINV, S_NV, S_NVINV,
+  S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -714,15 +715,32 @@ int poly_keys(const uint8_t* commits48, uint32_t t, const std::vector<uint32_t>&
 // VerifyPartial over R rounds x k partials: keys X_i = PubPoly.Eval(i) for every distinct index
 int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const uint8_t* msgs, uint32_t msg_len,
                         uint32_t k, const uint8_t* partials98, uint64_t seed, hipStream_t st, uint8_t** d_status,
-                        uint8_t** d_partials, G2AStore** d_S, uint32_t prefix_t = 0) {
+                        uint8_t** d_partials, G2AStore** d_S, uint32_t prefix_t = 0, bool on_device = false) {
   const size_t N = (size_t)R * k;
-  // Key slots (host bookkeeping over the 2-byte index fields only).  An index enters the batch equation
-  // as its own key set only if it occurs in at least 1/8 of the rounds, and at most kMaxSlots of them
-  // (most frequent first): each set costs an MSM bucket array, a column of the (round, key) cell map and
-  // possibly a correction pairing, so a signer that sends a fresh index every round must not get one
-  // per index.  Items of the other indices are checked on their own (their verdicts stay exact).
-  std::vector<uint32_t> count(65536, 0);
-  for (size_t i = 0; i < N; ++i) ++count[(uint32_t)partials98[98 * i] << 8 | partials98[98 * i + 1]];
+  uint8_t *d_m, *d_p, *kst;
+  if (on_device) {  // msgs and partials98 are device pointers (dg_recover_dev)
+    d_m = const_cast<uint8_t*>(msgs);
+    d_p = const_cast<uint8_t*>(partials98);
+  } else {
+    RET(upload(S_MSGS, msgs, (size_t)R * msg_len, &d_m, st));
+    RET(upload(S_IN1, partials98, N * 98, &d_p, st));
+  }
+  // Key slots.  An index enters the batch equation as its own key set only if it occurs in at least 1/8 of
+  // the rounds, and at most kMaxSlots of them (most frequent first): each set costs an MSM bucket array, a
+  // column of the (round, key) cell map and possibly a correction pairing, so a signer that sends a fresh
+  // index every round must not get one per index.  Items of the other indices are checked on their own
+  // (their verdicts stay exact).  Counts and first positions come from the device (k_index_scan: 2 x 256 KB
+  // back to the host instead of a host pass over the partials); the slot table goes back up (256 KB).
+  uint32_t *d_cnt, *d_first;
+  RET(wsT(S_IDXCNT, 65536, &d_cnt));
+  RET(wsT(S_IDXFIRST, 65536, &d_first));
+  HIPCHK(hipMemsetAsync(d_cnt, 0, 65536 * 4, st));
+  HIPCHK(hipMemsetAsync(d_first, 0xff, 65536 * 4, st));
+  RET(launch("k_index_scan", k_index_scan, (uint32_t)N, 256, st, (uint32_t)N, (const uint8_t*)d_p, d_cnt, d_first));
+  std::vector<uint32_t> count(65536), first(65536);
+  HIPCHK(hipMemcpyAsync(count.data(), d_cnt, 65536 * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(first.data(), d_first, 65536 * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
   std::vector<uint32_t> distinct;
   for (uint32_t idx = 0; idx < 65536; ++idx)
     if (count[idx]) distinct.push_back(idx);
@@ -733,26 +751,22 @@ int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const 
     ++nslots;
   // slots in first-occurrence order within each class (batched, alone), so the usual batch keeps the
   // input's index order
+  std::vector<uint32_t> slot_idx(distinct.begin(), distinct.begin() + nslots);
+  std::vector<uint32_t> alone(distinct.begin() + nslots, distinct.end());
+  auto by_first = [&](uint32_t a, uint32_t b) { return first[a] < first[b]; };
+  std::sort(slot_idx.begin(), slot_idx.end(), by_first);
+  std::sort(alone.begin(), alone.end(), by_first);
+  slot_idx.insert(slot_idx.end(), alone.begin(), alone.end());
   std::vector<int32_t> slot_of(65536, -1);
-  std::vector<uint8_t> batched(65536, 0);
-  for (uint32_t q = 0; q < nslots; ++q) batched[distinct[q]] = 1;
-  std::vector<uint32_t> slot_idx, item_slot(N);
-  for (int pass = 0; pass < 2; ++pass)
-    for (size_t i = 0; i < N; ++i) {
-      uint32_t idx = (uint32_t)partials98[98 * i] << 8 | partials98[98 * i + 1];
-      if (slot_of[idx] < 0 && batched[idx] == (pass == 0 ? 1 : 0)) {
-        slot_of[idx] = (int32_t)slot_idx.size();
-        slot_idx.push_back(idx);
-      }
-    }
-  for (size_t i = 0; i < N; ++i) item_slot[i] = (uint32_t)slot_of[(uint32_t)partials98[98 * i] << 8 | partials98[98 * i + 1]];
-  uint8_t *d_m, *d_p, *kst;
+  for (size_t q = 0; q < slot_idx.size(); ++q) slot_of[slot_idx[q]] = (int32_t)q;
   G1AStore* keys;
   uint32_t* d_itemslot;
+  int32_t* d_slotof;
   RET(poly_keys(commits48, t, slot_idx, st, &keys, &kst));
-  RET(upload(S_ITEMSLOT, item_slot.data(), N, &d_itemslot, st));
-  RET(upload(S_MSGS, msgs, (size_t)R * msg_len, &d_m, st));
-  RET(upload(S_IN1, partials98, N * 98, &d_p, st));
+  RET(upload(S_SLOTOF, slot_of.data(), 65536, &d_slotof, st));
+  RET(wsT(S_ITEMSLOT, N, &d_itemslot));
+  RET(launch("k_item_slots", k_item_slots, (uint32_t)N, 256, st, (uint32_t)N, (const uint8_t*)d_p,
+             (const int32_t*)d_slotof, d_itemslot));
   G2JStore* Q;
   RET(hash_rounds(R, d_m, msg_len, st, &Q));
   RET(wsT(S_S, N, d_S));
@@ -765,7 +779,8 @@ int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const 
 }
 
 // Recover after the VerifyPartial statuses are known (d_st): per round the first t valid partials, xyCommit
-// dedupe, Lagrange terms lambda_j S_j, row sums, compression; results copied to the host buffers.
+// dedupe, Lagrange terms lambda_j S_j, row sums, compression; results copied to the output buffers (host or
+// device memory: hipMemcpyDefault).
 int recover_tail(uint32_t R, uint32_t k, uint32_t t, const uint8_t* d_p, const uint8_t* d_st, const G2AStore* d_S,
                  uint8_t* out_sig96, uint8_t* round_status, uint8_t* share_status, hipStream_t st) {
   uint8_t *d_rst, *d_sst, *d_out;
@@ -783,9 +798,9 @@ int recover_tail(uint32_t R, uint32_t k, uint32_t t, const uint8_t* d_p, const u
   RET(reduce_rows(terms, tmp, R, t, st));
   RET(wsT(S_OUT0, (size_t)R * 96, &d_out));
   RET(launch("k_compress_g2", k_compress_g2, R, 128, st, R, (const G2JStore*)terms, (const uint8_t*)d_rst, d_out));
-  HIPCHK(hipMemcpyAsync(out_sig96, d_out, (size_t)R * 96, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(round_status, d_rst, R, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(share_status, d_sst, (size_t)R * k, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(out_sig96, d_out, (size_t)R * 96, hipMemcpyDefault, st));
+  HIPCHK(hipMemcpyAsync(round_status, d_rst, R, hipMemcpyDefault, st));
+  HIPCHK(hipMemcpyAsync(share_status, d_sst, (size_t)R * k, hipMemcpyDefault, st));
   HIPCHK(hipStreamSynchronize(st));
   if (g_ctx.timing) collect_timings();
   return 0;
@@ -826,15 +841,25 @@ int dg_init(int device) {
   // workspace stream here, with zero items (every lane returns at once), so the growth happens now -- the
   // largest first: a dispatch that needs a larger private segment than the queue's current one, right
   // behind it, failed with HSA_STATUS_ERROR_OUT_OF_RESOURCES on the box.
+  // (largest first, by the private segment sizes of the code objects)
+  hipFuncAttributes fa_items{}, fa_groups{};
+  HIPCHK(hipFuncGetAttributes(&fa_items, reinterpret_cast<const void*>(k_verify_items)));
+  HIPCHK(hipFuncGetAttributes(&fa_groups, reinterpret_cast<const void*>(k_verify_groups)));
+  const bool items_first = fa_items.localSizeBytes > fa_groups.localSizeBytes;
   for (Set& x : g_ctx.sets) {
-    // glist[0] = 0 (the zeroed fallback counter): no groups
-    hipLaunchKernelGGL(k_verify_groups, dim3(1), dim3(64), 0, x.stream, 1u, (const uint32_t*)g_ctx.fallbacks,
-                       (const uint64_t*)nullptr, (const G1AStore*)nullptr, (const uint32_t*)nullptr,
-                       (const G2AStore*)nullptr, (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr, 0u,
-                       g_ctx.gcount);
-    hipLaunchKernelGGL(k_verify_items, dim3(1), dim3(64), 0, x.stream, 0u, 1u, (const uint32_t*)nullptr,
-                       (const G1AStore*)nullptr, (const uint32_t*)nullptr, (const G2AStore*)nullptr,
-                       (const G2AStore*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, 0u);
+    for (int pass = 0; pass < 2; ++pass) {
+      if ((pass == 0) == items_first) {
+        hipLaunchKernelGGL(k_verify_items, dim3(1), dim3(64), 0, x.stream, 0u, 1u, (const uint32_t*)nullptr,
+                           (const G1AStore*)nullptr, (const uint32_t*)nullptr, (const G2AStore*)nullptr,
+                           (const G2AStore*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, 0u);
+      } else {
+        // glist[0] = 0 (the zeroed fallback counter): no groups
+        hipLaunchKernelGGL(k_verify_groups, dim3(1), dim3(64), 0, x.stream, 1u, (const uint32_t*)g_ctx.fallbacks,
+                           (const uint64_t*)nullptr, (const G1AStore*)nullptr, (const uint32_t*)nullptr,
+                           (const G2AStore*)nullptr, (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr,
+                           0u, g_ctx.gcount);
+      }
+    }
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipDeviceSynchronize());
@@ -1264,6 +1289,27 @@ int dg_recover(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t ro
   RET(verify_partials_dev(commits48, t, R, msgs, (uint32_t)msg_len, k, partials98, fresh_seed(seed), st, &d_st, &d_p,
                           &d_S, t));
   return recover_tail(R, k, t, d_p, d_st, d_S, out_sig96, round_status, share_status, st);
+}
+
+int dg_recover_dev(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t rounds, const uint8_t* d_msgs,
+                   size_t msg_len, uint32_t k, const uint8_t* d_partials98, uint8_t* d_out_sig96,
+                   uint8_t* d_round_status, uint8_t* d_share_status, uint64_t seed) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  (void)nshares;
+  if (rounds == 0) return 0;
+  if (!commits48 || t == 0 || k == 0 || !d_msgs || !d_partials98 || !d_out_sig96 || !d_round_status ||
+      !d_share_status)
+    return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(rounds * (size_t)(k > t ? k : t)));
+  hipStream_t st;
+  RET(acquire_set(&st));
+  const uint32_t R = (uint32_t)rounds;
+  uint8_t *d_st, *d_p;
+  G2AStore* d_S;
+  RET(verify_partials_dev(commits48, t, R, d_msgs, (uint32_t)msg_len, k, d_partials98, fresh_seed(seed), st, &d_st,
+                          &d_p, &d_S, t, true));
+  return recover_tail(R, k, t, d_p, d_st, d_S, d_out_sig96, d_round_status, d_share_status, st);
 }
 
 int dg_recover_verified(uint32_t t, uint32_t nshares, size_t rounds, uint32_t k, const uint8_t* partials98,

@@ -231,10 +231,10 @@ DGI Fp fp_small(uint32_t v) {
   return fp_to_mont(a);
 }
 
-// The digit-form chain is used in the hot translation unit only (hash-to-G2 -8%, decode -13% per launch):
-// built into the library TU as well, the overlapped batches ran 3-5x slower on MI355X although every
-// kernel was as fast or faster alone (measured, cause not isolated), so the library keeps the per-step
-// form below.
+// The digit-form chain is used in the hot translation unit only (hash-to-G2 -8%, decode -13% per launch).
+// Built into the library TU as well (round 1), the overlapped batches ran 3-5x slower although every kernel
+// was as fast or faster alone; the likely cause is the queue scratch regrowth of DESIGN.md §5.2 (a library
+// kernel's private segment outgrowing the prewarmed one), which dg_init now rules out.
 #if DG_TU_HOT
 // x^e for a fixed exponent given as a width-3 sliding-window schedule (tools/gen_constants.py).
 // The schedule is wave-uniform (scalar loads); the odd-power table is selected with v_cndmask.  The chain

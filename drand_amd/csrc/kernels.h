@@ -10,6 +10,9 @@
 #ifndef DG_HOT_WAVES
 #define DG_HOT_WAVES 2  // min waves per SIMD for the hot kernels: 256 VGPRs each (measured: 2 beats 1 by 6%)
 #endif
+#ifndef DG_TERMS_WAVES
+#define DG_TERMS_WAVES DG_HOT_WAVES  // min waves per SIMD of k_recover_terms
+#endif
 #ifndef DG_BULK_WAVES
 #define DG_BULK_WAVES 1  // min waves per SIMD for the other per-lane group-arithmetic kernels
 #endif
@@ -19,6 +22,10 @@
 #ifndef DG_TU_HOT
 #define DG_TU_HOT 0  // 1 in kernels_hot.hip: only the hot kernels are defined there (DESIGN.md §code generation)
 #endif
+#ifndef DG_TU_VERIFY
+#define DG_TU_VERIFY 0  // 1 in kernels_verify.hip: only the per-item pairing kernels are defined there
+#endif
+#define DG_TU_LIB (!DG_TU_HOT && !DG_TU_VERIFY)  // the library translation unit (drand_gpu.hip)
 
 namespace dg {
 
@@ -83,7 +90,7 @@ DGI uint64_t rlc_coeff(uint64_t seed, uint64_t i) {
 #define DG_KERNEL extern "C" __global__
 
 // A1: beacon messages
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(256) k_beacon_msgs(uint32_t n, const uint64_t* prev_round, const uint64_t* round,
                                                     const uint8_t* prev_sigs, const uint32_t* off, uint8_t* out32) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -94,7 +101,7 @@ DG_KERNEL void __launch_bounds__(256) k_beacon_msgs(uint32_t n, const uint64_t* 
 #endif
 
 // A2: randomness
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(256) k_randomness(uint32_t n, const uint8_t* sigs96, uint8_t* out32) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -106,7 +113,7 @@ DG_KERNEL void __launch_bounds__(256) k_randomness(uint32_t n, const uint8_t* si
 #endif
 
 // A13: link check
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(256) k_links(uint32_t n, uint64_t cur_round, const uint8_t* cur_sig, uint32_t cur_len,
                                               const uint64_t* prev_round, const uint64_t* round,
                                               const uint8_t* prev_sigs, const uint32_t* off, const uint8_t* sigs96,
@@ -125,7 +132,7 @@ DG_KERNEL void __launch_bounds__(256) k_links(uint32_t n, uint64_t cur_round, co
 #endif
 
 // A9: full hash-to-G2, compressed
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128) k_hash_to_g2(uint32_t n, const uint8_t* msgs, uint32_t msg_len,
                                                    const uint8_t* dst, uint32_t dst_len, uint8_t* out96) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -164,7 +171,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_h2c_uncleared(uint32_t n, 
 #endif
 
 // sigma decode + subgroup check (A10)
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128) k_decode_sigs(uint32_t n, const uint8_t* sigs, uint32_t stride, uint32_t offset,
                                                     G2AStore* outS, uint8_t* status) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -178,7 +185,7 @@ DG_KERNEL void __launch_bounds__(128) k_decode_sigs(uint32_t n, const uint8_t* s
 #endif
 
 // G1 decode (keys, commits), with subgroup check
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(64) k_decode_g1(uint32_t n, const uint8_t* in48, G1AStore* out, uint8_t* status) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -217,7 +224,7 @@ DGN Jac<F> jac_mul_small(const Jac<F>& p, uint32_t k) {
 DGI uint32_t be16(const uint8_t* p) { return (uint32_t)p[0] << 8 | p[1]; }
 
 // A12: PubPoly.Eval(idx) = sum_j C_j x^j at x = idx + 1 (Horner), affine (+ compressed when out48)
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(64) k_pubpoly_eval(uint32_t n, uint32_t t, const G1AStore* commits,
                                                     const uint8_t* commit_status, const uint32_t* idx,
                                                     G1AStore* out, uint8_t* out_status, uint8_t* out48) {
@@ -274,7 +281,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_decode_items(uint32_t n, u
 #endif
 
 // U_i = beta_slot S_i for batch items, O otherwise
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_scale_items(uint32_t n, uint32_t nslots, const uint64_t* seedp,
                                                     const uint32_t* item_slot, const G2AStore* S,
                                                     const uint8_t* status, const uint8_t* isolate, G2JStore* U) {
@@ -295,7 +302,7 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_scale_items(uint32_t n, u
 // of key s is K_s = K - C_s with K = sum over the active rounds of alpha_r Q_r (one Pippenger MSM, msm.h)
 // and C_s = sum of A_r over the active rounds without an item of s (k_key_accum) -- nothing when every
 // share is present in every round
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_round_combine(uint32_t R, uint32_t k, uint32_t nslots, const uint64_t* seedp,
                                                       const G2JStore* U, const uint8_t* status,
                                                       const uint8_t* isolate, const G2JStore* Q, const uint32_t* cell,
@@ -324,7 +331,7 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_round_combine(uint32_t R,
 
 // Kp[s * nchunks + c] = -(sum of A_r over the active rounds r in chunk c without an item of key s), so the
 // row sums are -C_s (k_round_combine)
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_key_accum(uint32_t R, uint32_t nslots, uint32_t chunk, uint32_t nchunks,
                                                   const uint32_t* cell, const uint8_t* active, const G2JStore* A,
                                                   G2JStore* Kp) {
@@ -361,7 +368,7 @@ DG_KERNEL void __launch_bounds__(256) k_key_combine(uint32_t nslots, const uint6
 #endif
 
 // 2-D segmented sum: out[row * ocols + j] = sum_{c in [j*chunk, (j+1)*chunk) and < cols} in[row * cols + c]
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_sum_rows(uint32_t rows, uint32_t cols, uint32_t chunk, const G2JStore* in,
                                                  G2JStore* out) {
   uint32_t ocols = (cols + chunk - 1) / chunk;
@@ -381,7 +388,7 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_sum_rows(uint32_t rows, u
 // Pairs: (beta_s X_s, h_eff K_s) for s < nslots, (-g1, T) for s == nslots; with several keys (Kc given)
 // K_s = -C_s and one more pair (Xc, h_eff Kc), Xc = sum_s beta_s X_s: prod_s e(beta_s X_s, h(Kc - C_s)).
 // f[s] = 1 when a side is the identity (every correction pair when all shares are present).
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_pair_miller_coop(uint32_t nslots, const uint64_t* seedp, const G1AStore* keys,
                                                          const G2JStore* K, const G2JStore* T, const G1AStore* Xc,
                                                          const G2JStore* Kc, Fp12* f) {
@@ -437,7 +444,7 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_pair_miller_coop(uint32_t
 #endif
 
 // product of the npairs Miller values and one final exponentiation on one 128-lane workgroup
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_final_coop(uint32_t npairs, const Fp12* f, uint32_t* ok) {
   __shared__ CoGT gt;
   __shared__ Fp12W F, G, S[7];
@@ -461,7 +468,7 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_final_coop(uint32_t npair
 
 // H_r = h_eff(Q_r), affine (individual checks)
 // (skipped when the batch verified and nothing was isolated: flag[0] = batch ok, flag[1] = any isolated)
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_clear_rounds(uint32_t R, const uint32_t* flag, const G2JStore* Q, G2AStore* H) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R || (flag[0] && !flag[1])) return;
@@ -472,7 +479,18 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_clear_rounds(uint32_t R, 
 // individual bls.Verify of item i: e(X_slot, H_{i/k}) == e(g1, S_i); with `subgroup` the decode skipped
 // the per-item G2 subgroup check (batched on the MSM windows), so it is done here: a sigma outside G2
 // is a decode error, as in g2_decompress
-#if !DG_TU_HOT
+// ---- Group tests over the examined prefix.  With a corrupted fraction f of the shares, one pairing check
+// per examined item is more than Recover needs: up to GRP consecutive unverified items of one round are
+// checked together, e(sum_i rho_i X_i, H_r) == e(g1, sum_i rho_i S_i) with independent 64-bit rho_i from the
+// batch's bound seed.  Every S_i is in G2 (subgroup-checked here as in verify_item) and H_r is in G2, so a
+// member with x_i H_r != S_i makes the sum vanish for at most one rho_i value mod r: a group with a bad
+// member passes with probability <= 2^-64.  A passed group gives every member kyber's nil verdict; the
+// members of a failed group are marked for their own check (fin = FIN_RECHECK) in the next pass, which
+// decides every verdict Recover reads.  At f = 10% and GRP = 4 that is ~0.6 pairing checks per item.
+constexpr uint32_t GRP = 4;
+constexpr uint8_t FIN_PENDING = 0, FIN_DONE = 1, FIN_RECHECK = 2;
+constexpr uint64_t GROUP_TAG = 0x67726f7570746573ull;  // domain of rho_i, apart from alpha_r and beta_s
+#if DG_TU_VERIFY
 // the Miller loop out of line, so its state and the final exponentiation's do not share one stack frame
 // (the per-item kernels' private segment must stay under the queue's scratch limit: ~14 KB per lane)
 DGN Fp12 miller_loop2(const G1A* P, const G2A* Q, int np) { return miller_loop<2>(P, Q, np); }
@@ -504,38 +522,6 @@ DGN void verify_item(size_t i, uint32_t k, const G1AStore* keys, const uint32_t*
   status[i] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
 }
 
-// every decoded item after a failed batch (flag[0] == 0), only the isolated ones after a passed batch
-DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
-                                                    const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
-                                                    const uint8_t* isolate, uint8_t* status, uint32_t subgroup) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (status[i] != DG_ST_OK_) return;
-  if (flag[0] && !isolate[i]) return;
-  verify_item(i, k, keys, item_slot, H, S, status, subgroup);
-}
-
-// ---- Recover's per-item pass over the examined prefix only.  Recover (kyber tbls.Recover) checks the
-// partials of a round in input order and stops at the t-th valid one, so after a failed batch only the
-// items up to that point need their own pairing check: about t / (1 - corrupted fraction) of the k.
-// fin[i] = the verdict of item i is final (decode failure, or a passed batch and not isolated).
-DG_KERNEL void __launch_bounds__(256) k_prefix_init(uint32_t n, const uint32_t* flag, const uint8_t* isolate,
-                                                   const uint8_t* status, uint8_t* fin) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  fin[i] = (status[i] != DG_ST_OK_ || (flag[0] && !isolate[i])) ? 1 : 0;
-}
-// ---- Group tests over the examined prefix.  With a corrupted fraction f of the shares, one pairing check
-// per examined item is more than Recover needs: up to GRP consecutive unverified items of one round are
-// checked together, e(sum_i rho_i X_i, H_r) == e(g1, sum_i rho_i S_i) with independent 64-bit rho_i from the
-// batch's bound seed.  Every S_i is in G2 (subgroup-checked here as in verify_item) and H_r is in G2, so a
-// member with x_i H_r != S_i makes the sum vanish for at most one rho_i value mod r: a group with a bad
-// member passes with probability <= 2^-64.  A passed group gives every member kyber's nil verdict; the
-// members of a failed group are marked for their own check (fin = FIN_RECHECK) in the next pass, which
-// decides every verdict Recover reads.  At f = 10% and GRP = 4 that is ~0.6 pairing checks per item.
-constexpr uint32_t GRP = 4;
-constexpr uint8_t FIN_PENDING = 0, FIN_DONE = 1, FIN_RECHECK = 2;
-constexpr uint64_t GROUP_TAG = 0x67726f7570746573ull;  // domain of rho_i, apart from alpha_r and beta_s
 // the members' weighted sums a = sum rho_i X_i, b = sum rho_i S_i; members failing the subgroup check are
 // decided here (decode error) and left out.  Returns the live members (their item indices in live[]).
 DGN uint32_t group_combine(const uint32_t* mem, uint32_t n, uint64_t seed, const G1AStore* keys,
@@ -596,6 +582,51 @@ DGN void verify_group(const uint32_t* mem, uint32_t n, uint32_t k, uint64_t seed
     fin[live[m]] = good ? FIN_DONE : FIN_RECHECK;
   }
 }
+// every decoded item after a failed batch (flag[0] == 0), only the isolated ones after a passed batch
+DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
+                                                    const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
+                                                    const uint8_t* isolate, uint8_t* status, uint32_t subgroup) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (status[i] != DG_ST_OK_) return;
+  if (flag[0] && !isolate[i]) return;
+  verify_item(i, k, keys, item_slot, H, S, status, subgroup);
+}
+
+// lane g < glist[0]: group g (one member: the item's own check)
+DG_KERNEL void __launch_bounds__(64) k_verify_groups(uint32_t k, const uint32_t* glist, const uint64_t* seedp,
+                                                    const G1AStore* keys, const uint32_t* item_slot,
+                                                    const G2AStore* H, const G2AStore* S, uint8_t* status,
+                                                    uint8_t* fin, uint32_t subgroup, unsigned long long* cnt) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= glist[0]) return;
+  const uint32_t* mem = glist + 4 + 4 * (size_t)g;
+  uint32_t n = 0;
+  while (n < GRP && mem[n] != ~0u) ++n;
+  atomicAdd(&cnt[n - 1], 1ull);
+  verify_group(mem, n, k, *seedp, keys, item_slot, H, S, status, fin, subgroup);
+}
+#elif DG_TU_LIB
+// (defined in kernels_verify.hip)
+DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
+                                                    const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
+                                                    const uint8_t* isolate, uint8_t* status, uint32_t subgroup);
+DG_KERNEL void __launch_bounds__(64) k_verify_groups(uint32_t k, const uint32_t* glist, const uint64_t* seedp,
+                                                    const G1AStore* keys, const uint32_t* item_slot,
+                                                    const G2AStore* H, const G2AStore* S, uint8_t* status,
+                                                    uint8_t* fin, uint32_t subgroup, unsigned long long* cnt);
+#endif
+#if DG_TU_LIB
+// ---- Recover's per-item pass over the examined prefix only.  Recover (kyber tbls.Recover) checks the
+// partials of a round in input order and stops at the t-th valid one, so after a failed batch only the
+// items up to that point need their own pairing check: about t / (1 - corrupted fraction) of the k.
+// fin[i] = the verdict of item i is final (decode failure, or a passed batch and not isolated).
+DG_KERNEL void __launch_bounds__(256) k_prefix_init(uint32_t n, const uint32_t* flag, const uint8_t* isolate,
+                                                   const uint8_t* status, uint8_t* fin) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fin[i] = (status[i] != DG_ST_OK_ || (flag[0] && !isolate[i])) ? 1 : 0;
+}
 // per round: scanning in input order, the unverified items up to the point where the round would reach
 // t + margin valid shares if every fresh unverified item were valid and every member of a failed group (bad
 // with probability ~1/3 at 10% corruption) counted one half -- a speculative margin, so that few rounds
@@ -638,23 +669,29 @@ DG_KERNEL void __launch_bounds__(128) k_prefix_groups(uint32_t R, uint32_t k, ui
   }
   if (nc) emit(cur, nc);
 }
-// lane g < glist[0]: group g (one member: the item's own check)
-DG_KERNEL void __launch_bounds__(64) k_verify_groups(uint32_t k, const uint32_t* glist, const uint64_t* seedp,
-                                                    const G1AStore* keys, const uint32_t* item_slot,
-                                                    const G2AStore* H, const G2AStore* S, uint8_t* status,
-                                                    uint8_t* fin, uint32_t subgroup, unsigned long long* cnt) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= glist[0]) return;
-  const uint32_t* mem = glist + 4 + 4 * (size_t)g;
-  uint32_t n = 0;
-  while (n < GRP && mem[n] != ~0u) ++n;
-  atomicAdd(&cnt[n - 1], 1ull);
-  verify_group(mem, n, k, *seedp, keys, item_slot, H, S, status, fin, subgroup);
+#endif
+
+// Key-slot statistics of a VerifyPartial / Recover batch (drand_gpu.hip verify_partials_dev): per share
+// index its number of partials and its first position; then each item's slot from the host's slot table.
+#if DG_TU_LIB
+DG_KERNEL void __launch_bounds__(256) k_index_scan(uint32_t n, const uint8_t* partials98, uint32_t* count,
+                                                  uint32_t* first) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t idx = (uint32_t)partials98[98ull * i] << 8 | partials98[98ull * i + 1];
+  atomicAdd(&count[idx], 1u);
+  if (i < first[idx]) atomicMin(&first[idx], i);
+}
+DG_KERNEL void __launch_bounds__(256) k_item_slots(uint32_t n, const uint8_t* partials98, const int32_t* slot_of,
+                                                  uint32_t* item_slot) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  item_slot[i] = (uint32_t)slot_of[(uint32_t)partials98[98ull * i] << 8 | partials98[98ull * i + 1]];
 }
 #endif
 
 // *flag |= 1 if any byte of v[0..n) is non-zero
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(256) k_any(uint32_t n, const uint8_t* v, uint32_t* flag) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n && v[i]) atomicOr(flag, 1u);
@@ -754,7 +791,7 @@ DG_KERNEL void __launch_bounds__(64) k_digest_seed(Seed0 s0, const uint8_t* d32,
 // per round: the first t items (input order) that passed VerifyPartial, sorted by index, duplicates
 // collapsed (kyber xyCommit); round_status NOT_ENOUGH if fewer than t distinct remain.  share_status
 // = the verify status of every item examined, NOT_EXAMINED after the t-th collected one.
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128) k_recover_select(uint32_t R, uint32_t k, uint32_t t, const uint8_t* partials,
                                                        const uint8_t* status, uint32_t* sel, uint32_t* selidx,
                                                        uint8_t* round_status, uint8_t* share_status) {
@@ -798,7 +835,7 @@ DG_KERNEL void __launch_bounds__(128) k_recover_select(uint32_t R, uint32_t k, u
 // Recover with known VerifyPartial verdicts (dg_recover_verified, the live round: beacon/beacon.go:148 has
 // already verified every partial the round cache holds, :488 would re-verify them): decode the sigma of
 // the partials whose verdict is OK (already subgroup-checked by that VerifyPartial), carry the others' verdicts
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128) k_decode_verified(uint32_t n, const uint8_t* partials, const uint8_t* vst,
                                                         G2AStore* S, uint8_t* status) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -820,7 +857,7 @@ DG_KERNEL void __launch_bounds__(128) k_decode_verified(uint32_t n, const uint8_
 // multiplication's digit-dependent branches are uniform across the wave.
 // hot translation unit (kernels_hot.hip: flat, 2 waves/SIMD; measured -27% / -36%)
 #if DG_TU_HOT
-DG_KERNEL void __launch_bounds__(64, DG_HOT_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
+DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
                                                      const uint32_t* selidx, const uint8_t* round_status,
                                                      const G2AStore* S, G2JStore* terms) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -845,13 +882,13 @@ DG_KERNEL void __launch_bounds__(64, DG_HOT_WAVES) k_recover_terms(uint32_t R, u
 #endif
 }
 #else
-DG_KERNEL void __launch_bounds__(64, DG_HOT_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
+DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
                                                      const uint32_t* selidx, const uint8_t* round_status,
                                                      const G2AStore* S, G2JStore* terms);
 #endif
 
 // compress points (zeros where status != OK)
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128) k_compress_g2(uint32_t n, const G2JStore* P, const uint8_t* st, uint8_t* out96) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -864,7 +901,7 @@ DG_KERNEL void __launch_bounds__(128) k_compress_g2(uint32_t n, const G2JStore* 
 #endif
 
 // A7: bls.Sign / tbls.Sign -- x * H(m); scalars are 32 B big-endian (< r)
-#if !DG_TU_HOT
+#if DG_TU_LIB
 DG_KERNEL void __launch_bounds__(128) k_sign(uint32_t n, const uint8_t* sc32, const uint16_t* index, const uint8_t* msgs,
                                              uint32_t msg_len, const uint8_t* dst, uint32_t dst_len, uint8_t* out) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

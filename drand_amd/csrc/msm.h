@@ -40,7 +40,7 @@ constexpr uint32_t MSM_CHUNK = 8;   // points per first-level lane
 constexpr uint32_t MSM_BSPLIT = 32;  // lanes per bucket at the second level
 constexpr uint32_t MSM_SLICE_LANES = 64;  // lanes per (side, window, bit slice) in k_msm_slices
 
-#if defined(__HIP__) && !DG_TU_HOT
+#if defined(__HIP__) && DG_TU_LIB
 // digits of round r in windows 0..nwin-1: the bytes of alpha_r, then (nwin > MSM_WIN) the first
 // MSM_TWIN bytes of SHA-256(seed' || r), an independent hash
 struct MsmDigits {
@@ -165,7 +165,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_ch
                                                    G2JStore* out);
 #endif
 
-#if defined(__HIP__) && !DG_TU_HOT
+#if defined(__HIP__) && DG_TU_LIB
 // lane g: side, bucket b, lane-in-bucket q < MSM_BSPLIT: strided partial sum of the bucket's chunks,
 // BP[(side * NBK + b) * MSM_BSPLIT + q]; the MSM_BSPLIT partials are then row-summed into B[side][b]
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_buckets(uint32_t max_chunks, uint32_t nsides, uint32_t nbk,
@@ -397,7 +397,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_kmsm_chunks(uint32_t max_c
                                                                    const uint32_t* chunk_off, const uint32_t* list,
                                                                    const G2AStore* S, G2JStore* out);
 #endif
-#if defined(__HIP__) && !DG_TU_HOT
+#if defined(__HIP__) && DG_TU_LIB
 
 // lane = bucket key: sum of its chunks (identity when empty)
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_buckets(uint32_t nkeys, const uint32_t* chunk_off,

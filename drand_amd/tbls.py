@@ -140,6 +140,24 @@ def recover_batch(pub: PubPoly, msgs, partials, t, n, seed=0):
     return out, rs, ss
 
 
+def recover_batch_dev(pub: PubPoly, d_msgs, d_partials, t, n, seed=0):
+    """recover_batch with device-resident inputs and outputs (dg_recover_dev): d_msgs a (R, msg_len) and
+    d_partials a (R, k, 98) uint8 torch tensor on the current GPU.  Returns device tensors (sigs (R, 96),
+    round_status (R,), share_status (R, k))."""
+    import torch
+
+    R, k = d_partials.shape[0], d_partials.shape[1]
+    dev = d_partials.device
+    out = torch.empty((R, 96), dtype=torch.uint8, device=dev)
+    rs = torch.empty(R, dtype=torch.uint8, device=dev)
+    ss = torch.empty((R, k), dtype=torch.uint8, device=dev)
+    c = pub.commits_array()
+    torch.cuda.current_stream(dev).synchronize()  # inputs written on torch's stream are visible to the library's
+    L.check(L.lib().dg_recover_dev(L.ptr(c), c.shape[0], n, R, L.ptr(d_msgs), d_msgs.shape[1], k, L.ptr(d_partials),
+                                   L.ptr(out), L.ptr(rs), L.ptr(ss), seed))
+    return out, rs, ss
+
+
 def recover_verified_batch(pub: PubPoly, msgs, partials, verified_status, t, n):
     """The live round's Recover (beacon/beacon.go:472-494) with the VerifyPartial verdicts ProcessBeacon
     already holds (beacon/beacon.go:148): partials (R, k, 98), verified_status (R, k) DG_ST_* ->

@@ -127,6 +127,11 @@ int dg_recover_verified(uint32_t t, uint32_t nshares, size_t rounds, uint32_t k,
 int dg_verify_beacons_dev(const uint8_t* pk48_host, size_t n, const uint64_t* d_prev_round, const uint64_t* d_round,
                           const uint8_t* d_prev_sigs, const uint32_t* d_prev_sig_off, const uint8_t* d_sigs96,
                           uint8_t* d_status, uint64_t seed, void* stream);
+/* dg_recover with messages, partials and outputs in device memory (commits48 stays a host buffer): the
+ * multi-GPU Recover path, whose outputs go straight into the RCCL all-gather.  Completes before return. */
+int dg_recover_dev(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t rounds, const uint8_t* d_msgs,
+                   size_t msg_len, uint32_t k, const uint8_t* d_partials98, uint8_t* d_out_sig96,
+                   uint8_t* d_round_status, uint8_t* d_share_status, uint64_t seed);
 
 /* Asynchronous device-resident VerifyBeacon batch (the streaming form of syncFrom's catch-up,
  * beacon/beacon.go:529-607): enqueues the batch on the next of the library's rotating workspace sets and

@@ -223,6 +223,20 @@ def test_large_group_corrupted_vs_twin(t, n, R):
             assert bytes(sigs[r]) == twin.sign(x, msgs[r])
 
 
+@pytest.mark.parametrize("t,n,R,frac", [(33, 64, 64, 0.1), (129, 256, 24, 0.1), (129, 256, 8, 0.3)])
+def test_recover_corrupted_at_scale_vs_twin(t, n, R, frac):
+    """C3 / C5 shapes over many rounds (the group tests, the speculative passes and the final exact pass of
+    the per-item check): signatures, round statuses and every share status equal the CPU twin's Recover
+    (kyber's algorithm: each examined share verified in input order)."""
+    coeffs, commits, msgs, parts, items = _group_rounds(t, n, R, frac, b"rs%d/%d" % (n, R))
+    pub = tbls.PubPoly(commits)
+    sigs, rs, ss = tbls.recover_batch(pub, msgs, parts, t, n, seed=31)
+    tw_sigs, tw_rs, tw_ss = twin.recover_batch(commits, t, n, np.array([list(m) for m in msgs], np.uint8), parts, 16)
+    assert np.array_equal(rs, tw_rs) and np.array_equal(ss, tw_ss)
+    assert np.array_equal(sigs[rs == 0], tw_sigs[tw_rs == 0])
+    assert (ss == L.ST_BAD_SIG).sum() > 0
+
+
 def test_not_enough_shares_many_rounds():
     t, n, R = 3, 5, 6
     coeffs, commits, msgs, parts, _ = _group_rounds(t, n, R, 0.0, b"ne")

@@ -312,3 +312,26 @@ def test_clean_groups_pass_on_the_group_path():
     assert not rs.any() and ss[0, :6].tolist() == [0, 0, 1, 0, 0, 0]
     if d[3]:  # group tests enabled (DG_GROUP unset)
         assert d[3] >= R and d[0] <= R + 5, d
+
+
+def test_recover_dev_equals_host_and_twin():
+    """dg_recover_dev (messages, partials and outputs in HBM) gives dg_recover's and the twin's signatures,
+    round statuses and share statuses, including an index that occurs in fewer than 1/8 of the rounds (checked
+    alone) and a duplicated index."""
+    import torch
+
+    t, n, R = 5, 12, 24
+    coeffs, commits, msgs, parts = _group_rounds(t, n, R, 0.15, b"dev")
+    parts[3, 7, :2] = [0, 200]      # a rare index (key slot of its own, outside the batch equation)
+    parts[5, 1] = parts[5, 0]      # duplicate index among the first t
+    pub = tbls.PubPoly(commits)
+    a = tbls.recover_batch(pub, msgs, parts, t, n, seed=41)
+    dev = torch.device("cuda", 0)
+    d_m = torch.from_numpy(np.array([list(m) for m in msgs], np.uint8)).to(dev)
+    d_p = torch.from_numpy(np.ascontiguousarray(parts)).to(dev)
+    b = [x.cpu().numpy() for x in tbls.recover_batch_dev(pub, d_m, d_p, t, n, seed=41)]
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    tw = twin.recover_batch(commits, t, n, np.array([list(m) for m in msgs], np.uint8), parts, 8)
+    assert np.array_equal(b[1], tw[1]) and np.array_equal(b[2], tw[2])
+    assert np.array_equal(b[0][b[1] == 0], tw[0][tw[1] == 0])

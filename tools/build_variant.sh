@@ -10,6 +10,6 @@ C=$R/drand_amd/csrc
 O=$R/tools/variants
 mkdir -p $O
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -Wno-unused-result -fPIC -c -DDG_FLAT=1 "$@" -o $O/hot_$name.o $C/kernels_hot.hip
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libdrandgpu_$name.so $C/drand_gpu.o $O/hot_$name.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libdrandgpu_$name.so $C/drand_gpu.o $O/hot_$name.o $C/kernels_verify.o
 rm -f $O/hot_$name.o
 echo $O/libdrandgpu_$name.so

@@ -201,7 +201,7 @@ __global__ void __launch_bounds__(128, W) k_pow(const uint32_t* in, uint32_t* ou
 
 int main(int argc, char** argv) {
   const int only = argc > 1 ? atoi(argv[1]) : -1;  // run one variant (profiling)
-  const int n = 200000, reps = 4;
+  const int n = argc > 2 ? atoi(argv[2]) : 200000, reps = argc > 3 ? atoi(argv[3]) : 4;  // items, chains per lane
   int nsq = 1, nmul = 3;
   for (int s = 0; s < EXP_PM3D4_NSTEPS; ++s) {
     nsq += EXP_PM3D4_STEPS[s][0];
@@ -271,7 +271,7 @@ int main(int argc, char** argv) {
     }
     double per_launch_us = ms * 1e3 / reps;
     double rate = (double)n * macs / (per_launch_us * 1e-6) / 1e12;
-    printf("%-6s  %9.1f us per 200k-lane exponentiation  %6.2f TMAC/s  %s\n", k.name, per_launch_us, rate,
+    printf("%-6s n=%d reps=%d  %9.1f us per launch-exponentiation  %6.2f TMAC/s  %s\n", k.name, n, reps, per_launch_us, rate,
            same ? "match" : "MISMATCH");
   }
   return 0;
