@@ -244,16 +244,18 @@ DGH G2J g2_mul_u256_psi(const G2A& p, const uint32_t* k) {
   d[1] = u256_divmod_u64(q, Z_ABS);
   d[2] = u256_divmod_u64(q, Z_ABS);
   d[3] = (uint64_t)q[1] << 32 | q[0];  // < Z_ABS since k < Z_ABS^4
-  Fp2 px[4], py[4];
-  px[0] = p.x;
-  py[0] = p.y;
-  for (int i = 1; i < 4; ++i) {
-    px[i] = px[i - 1];
-    py[i] = py[i - 1];
-    g2_psi_aff(px[i], py[i]);
-  }
-  py[1] = fp2_neg(py[1]);
-  py[3] = fp2_neg(py[3]);
+  // Only P and psi(P) stay live (96 words instead of 192 for the four points: the spills of the scalar
+  // loop were a few hundred GB of scratch traffic per 100k-round Recover, PMC): psi^2 is (x, y) -> (w x, -y)
+  // on E2 (w = N(PSI_CX), a cube root of unity in Fp), so P_2 = psi^2 P = (w x0, -y0) and
+  // P_3 = -psi^3 P = (w x1, y1) cost one Fp2 x Fp product of the x-coordinate where they are added.
+  const Fp2 x0 = p.x, y0 = p.y;
+  Fp2 x1 = p.x, y1 = p.y;
+  g2_psi_aff(x1, y1);
+  auto add_i = [&](const G2J& acc, int i, bool neg) {
+    const Fp2 x = i == 0 ? x0 : i == 1 ? x1 : fp2_mul_fp(i == 2 ? x0 : x1, fp_const(PSI2_W));
+    const Fp2 y = i == 0 ? y0 : i == 1 ? fp2_neg(y1) : i == 2 ? fp2_neg(y0) : y1;
+    return jac_add_aff(acc, x, neg ? fp2_neg(y) : y);
+  };
   // non-adjacent forms of the digits (65 signed digits, ~1/3 non-zero): h = 3d, digit j = h_{j+1} - d_{j+1}
   uint64_t pos[4], neg[4];
   uint32_t pos64 = 0;
@@ -264,13 +266,15 @@ DGH G2J g2_mul_u256_psi(const G2A& p, const uint32_t* k) {
     pos64 |= (uint32_t)(hh >> 1) << i;
   }
   G2J acc = jac_infinity<Fp2>();
+#pragma unroll
   for (int i = 0; i < 4; ++i)
-    if ((pos64 >> i) & 1) acc = jac_add_aff(acc, px[i], py[i]);
+    if ((pos64 >> i) & 1) acc = add_i(acc, i, false);
   for (int b = 63; b >= 0; --b) {
     acc = jac_dbl(acc);
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if ((pos[i] >> b) & 1) acc = jac_add_aff(acc, px[i], py[i]);
-      if ((neg[i] >> b) & 1) acc = jac_add_aff(acc, px[i], fp2_neg(py[i]));
+      if ((pos[i] >> b) & 1) acc = add_i(acc, i, false);
+      if ((neg[i] >> b) & 1) acc = add_i(acc, i, true);
     }
   }
   return acc;

@@ -20,6 +20,7 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PLAUSIBLE_BYTES_S = 10e12  # above MI355X HBM (8 TB/s) plus on-die cache hits counted at the memory side
 
 
 def load(prof):
@@ -29,14 +30,17 @@ def load(prof):
         m = re.match(r"pmc_([a-z0-9]+)_", os.path.basename(os.path.dirname(f)))
         cfg = m.group(1) if m else "head"
         per = collections.defaultdict(float)
-        names = {}
+        names, dur = {}, {}
         for r in csv.DictReader(open(f)):
             if not r["Kernel_Name"].startswith("k_"):
                 continue
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
             names[r["Dispatch_Id"]] = r["Kernel_Name"]
+            dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
         for (d, c), v in per.items():
             acc[cfg][names[d]][c].append(v)
+            if c in ("FETCH_SIZE", "WRITE_SIZE"):
+                acc[cfg][names[d]]["_dur_" + c].append(dur[d])
     return {cfg: {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in ks.items()} for cfg, ks in acc.items()}
 
 
@@ -49,11 +53,17 @@ def main(prof, out_csv):
         sec = {}
         for k, c in sorted(ks.items()):
             if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-                sec[k] = {"fetch_kb": c["FETCH_SIZE"], "write_kb": c["WRITE_SIZE"],
-                          "bytes_per_launch": 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024}
+                b = 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
+                t = max(1e-9, min(c["_dur_FETCH_SIZE"], c["_dur_WRITE_SIZE"]))
+                sec[k] = {"fetch_kb": c["FETCH_SIZE"], "write_kb": c["WRITE_SIZE"], "bytes_per_launch": b,
+                          "implied_tb_s": b / t / 1e12}
+                if b / t > PLAUSIBLE_BYTES_S:  # beyond the memory system: the counter, not traffic
+                    sec[k]["bytes_per_launch"] = None
+                    sec[k]["note"] = ("FETCH/WRITE_SIZE imply %.0f TB/s over the launch, beyond the memory "
+                                      "system: counter not usable for this (long, scratch-heavy) kernel" % (b / t / 1e12))
         out["configs"][cfg] = sec
     json.dump(out, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
-    cols = sorted({c for ks in m.values() for cs in ks.values() for c in cs})
+    cols = sorted({c for ks in m.values() for cs in ks.values() for c in cs if not c.startswith("_")})
     with open(out_csv, "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["config", "kernel"] + cols)
