@@ -152,6 +152,84 @@ DGI G2J g2_madd_lean(const G2J& p, const Fp2& qx, const Fp2& qy) {
   return G2J{X3, Y3, Z3};
 }
 
+// The same mixed addition with the accumulator in LDS (one slot per lane): its nine Fp2 limbs leave the register
+// file, which then holds only the formula's temporaries (at most five Fp2 values and one product), so the chunk
+// sums run at 2 waves/SIMD without scratch.  Identical results to g2_madd_lean.
+#ifndef DG_MADD_FORM
+#define DG_MADD_FORM 3  // Fp2 products of g2_madd_lds: 1 one call each (fp2_mul_rc), 2 inlined (fp2_mul_in), 3 inlined and serialised
+#endif
+#if DG_MADD_FORM == 1
+#define DG_MADD_MUL fp2_mul_rc
+#define DG_MADD_SQR fp2_sqr_rc
+#elif DG_MADD_FORM == 3
+#define DG_MADD_MUL fp2_mul_seq
+#define DG_MADD_SQR fp2_sqr_seq
+#else
+#define DG_MADD_MUL fp2_mul_in
+#define DG_MADD_SQR fp2_sqr_in
+#endif
+template <class S>
+DGI void g2_madd_lds(S& a, const Fp2& qx, const Fp2& qy) {
+  if (fp2_is_zero(a.z)) {
+    a.x = qx;
+    a.y = qy;
+    a.z = fp2_one();
+    return;
+  }
+  const Fp2 Z1Z1 = DG_MADD_SQR(a.z);
+  const Fp2 H = fp2_sub(DG_MADD_MUL(qx, Z1Z1), a.x);
+  const Fp2 r = fp2_dbl(fp2_sub(DG_MADD_MUL(DG_MADD_MUL(qy, a.z), Z1Z1), a.y));
+  if (fp2_is_zero(H)) {
+    const G2J t = g2_add_aff_rare(G2J{a.x, a.y, a.z}, qx, qy);
+    a.x = t.x;
+    a.y = t.y;
+    a.z = t.z;
+    return;
+  }
+  const Fp2 HH = DG_MADD_SQR(H);
+  a.z = fp2_sub(fp2_sub(DG_MADD_SQR(fp2_add(a.z, H)), Z1Z1), HH);
+  const Fp2 I = fp2_dbl(fp2_dbl(HH));
+  const Fp2 J = DG_MADD_MUL(H, I);
+  const Fp2 V = DG_MADD_MUL(a.x, I);
+  const Fp2 YJ2 = fp2_dbl(DG_MADD_MUL(a.y, J));
+  const Fp2 X3 = fp2_sub(fp2_sub(DG_MADD_SQR(r), J), fp2_dbl(V));
+  a.x = X3;
+  a.y = fp2_sub(DG_MADD_MUL(r, fp2_sub(V, X3)), YJ2);
+}
+
+// Affine pair additions with an externally supplied inverse (the affine levels of the MSM, msm.h; Montgomery's
+// trick over the batch supplies 1 / N(d)).  kind: 0 pass-through (an identity operand), 1 chord (x1 != x2),
+// 2 tangent (P + P), 3 identity result (P + (-P)).  E' has no 2-torsion (h2 is odd), so a tangent has y != 0.
+DGI uint32_t g2_aff_kind(const G2A& p, const G2A& q) {
+  if (p.inf || q.inf) return 0;
+  if (!fp2_eq(p.x, q.x)) return 1;
+  return fp2_eq(p.y, q.y) ? 2u : 3u;
+}
+// N(d) of the pair's denominator d (chord: x2 - x1, tangent: 2 y1); 1 where no inversion is needed
+DGI Fp g2_aff_den(const G2A& p, const G2A& q, uint32_t kind) {
+  if (kind == 1) return fp2_norm(fp2_sub(q.x, p.x));
+  if (kind == 2) return fp2_norm(fp2_dbl(p.y));
+  return fp_one();
+}
+// p + q given nv = 1 / g2_aff_den(p, q, kind): 1/d = conj(d) nv, lambda = (y2 - y1)/d or 3 x1^2 / d,
+// x3 = lambda^2 - x1 - x2, y3 = lambda (x1 - x3) - y1 (products serialised, field.h fp2_mul_seq)
+DGI G2A g2_aff_sum(const G2A& p, const G2A& q, uint32_t kind, const Fp& nv) {
+  if (kind == 0) return p.inf ? q : p;
+  if (kind == 3) return G2A{fp2_zero(), fp2_zero(), true};
+  const Fp2 d = kind == 1 ? fp2_sub(q.x, p.x) : fp2_dbl(p.y);
+  const Fp2 dinv = Fp2{fp_mul_seq(d.c0, nv), fp_neg(fp_mul_seq(d.c1, nv))};
+  Fp2 num;
+  if (kind == 1) {
+    num = fp2_sub(q.y, p.y);
+  } else {
+    const Fp2 xx = fp2_sqr_seq(p.x);
+    num = fp2_add(fp2_dbl(xx), xx);
+  }
+  const Fp2 lam = fp2_mul_seq(num, dinv);
+  const Fp2 x3 = fp2_sub(fp2_sub(fp2_sqr_seq(lam), p.x), q.x);
+  return G2A{x3, fp2_sub(fp2_mul_seq(lam, fp2_sub(p.x, x3)), p.y), false};
+}
+
 template <class F>
 DGH bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
   bool pi = jac_is_inf(p), qi = jac_is_inf(q);

@@ -101,6 +101,8 @@ struct Ctx {
   // hash-to-G2 and sigma decode as the phase kernels of phases.h (default) or the fused one-lane kernels
   // (DG_FUSED=1: A/B only)
   bool phased = getenv("DG_FUSED") == nullptr;
+  // single-key MSM first levels as mixed Jacobian chunk sums (DG_MSM_JAC=1: A/B only) instead of affine levels
+  bool msm_jac = getenv("DG_MSM_JAC") != nullptr;
 };
 
 std::mutex g_mu;
@@ -125,7 +127,7 @@ enum Slot {
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
   S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_BINV, S_NV, S_NVINV,
-  S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_COUNT
+  S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -327,14 +329,48 @@ int bind_seed(const Batch& b, uint64_t seed, hipStream_t st, uint64_t** d_seed) 
 // Pippenger MSM (msm.h): out[0] = sum_r alpha_r PA_r, out[1] = sum_r alpha_r PB_r (PB may be null),
 // over the rounds with active[r] != 0.  With `test_windows` side A also gets the MSM_TWIN test windows of
 // the batched subgroup check; *win = its MSM_WT window sums (checked by k_msm_subgroup).
+int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st);
+
+// `affine`: every point of PA and PB has Z = 1 or Z = 0, so the first levels are affine additions (msm.h).
 int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JStore* PA, const G2JStore* PB, bool test_windows,
-            G2JStore** out, G2JStore** win, hipStream_t st) {
+            bool affine, G2JStore** out, G2JStore** win, hipStream_t st) {
   const uint32_t nsides = PB ? 2 : 1, nwin = test_windows ? MSM_WT : MSM_WIN, nbk = nwin * MSM_NB;
   uint32_t *cnt, *list;
   G2JStore *chunks, *BP, *tmp, *P1, *W;
-  RET(wsT(S_MSM_CNT, 4 * nbk + 1, &cnt));
+  RET(wsT(S_MSM_CNT, 4 * nbk + 1 + MSM_AFF_L * (nbk + 1), &cnt));
   uint32_t *offset = cnt + nbk, *cursor = offset + nbk, *chunk_off = cursor + nbk;
   RET(wsT(S_MSM_LIST, (size_t)nwin * R + 1, &list));
+  if (affine && !g_ctx.msm_jac) {
+    const size_t E = (size_t)nwin * R;
+    if (E * nsides > 0x7fffffffull) return fail(DG_E_ARG, "batch too large for the MSM");
+    uint32_t* gofs = chunk_off + nbk + 1;
+    G2AStore* A;
+    Fp *den, *dinv;
+    const uint32_t maxg0 = (uint32_t)(E / 2) + nbk;
+    RET(wsT(S_MSM_AFF, E * nsides, &A));
+    RET(wsT(S_MSM_DEN, (size_t)maxg0 * nsides, &den));
+    RET(wsT(S_MSM_DINV, (size_t)maxg0 * nsides, &dinv));
+    RET(wsT(S_MSM_B, (size_t)nbk * MSM_BSPLIT * nsides, &BP));
+    RET(wsT(S_MSM_G, (size_t)nbk * MSM_BSPLIT * nsides, &tmp));
+    RET(wsT(S_MSM_P1, (size_t)nwin * MSM_C * MSM_SLICE_LANES * nsides, &P1));
+    RET(wsT(S_MSM_W, (size_t)nwin * nsides, &W));
+    RET(wsT(S_MSM_OUT, 2, out));
+    HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * nbk, st));
+    RET(launch("k_msm_count", k_msm_count, R, 256, st, R, nwin, seed, active, cnt));
+    RET(launch("k_msm_scan_aff", k_msm_scan_aff, 256, 256, st, nbk, (const uint32_t*)cnt, offset, cursor, gofs));
+    RET(launch("k_msm_scatter", k_msm_scatter, R, 256, st, R, nwin, seed, active, cursor, list));
+    for (uint32_t l = 0; l < MSM_AFF_L; ++l) {
+      const uint32_t maxg = (uint32_t)(E >> (l + 1)) + nbk, n = maxg * nsides;
+      const uint32_t* gl = gofs + l * (nbk + 1);
+      RET(launch("k_msm_aff_den", k_msm_aff_den, n, 128, st, l, maxg, nsides, nbk, (const uint32_t*)cnt,
+                 (const uint32_t*)offset, gl, (const uint32_t*)list, PA, PB, (const G2AStore*)A, (uint32_t)E, den));
+      RET(batch_inv(n, den, dinv, st));
+      RET(launch("k_msm_aff_add", k_msm_aff_add, n, 128, st, l, maxg, nsides, nbk, (const uint32_t*)cnt,
+                 (const uint32_t*)offset, gl, (const uint32_t*)list, PA, PB, A, (uint32_t)E, (const Fp*)dinv));
+    }
+    RET(launch("k_msm_buckets_aff", k_msm_buckets_aff, nbk * MSM_BSPLIT * nsides, 128, st, nsides, nbk,
+               (const uint32_t*)cnt, (const uint32_t*)offset, (const G2AStore*)A, (uint32_t)E, BP));
+  } else {
   const size_t max_chunks_sz = ((size_t)nwin * R) / MSM_CHUNK + nbk;
   if (max_chunks_sz * nsides > 0xffffffffull) return fail(DG_E_ARG, "batch too large for the MSM");
   const uint32_t max_chunks = (uint32_t)max_chunks_sz;
@@ -352,6 +388,7 @@ int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JSt
              (const uint32_t*)offset, (const uint32_t*)chunk_off, (const uint32_t*)list, PA, PB, chunks));
   RET(launch("k_msm_buckets", k_msm_buckets, nbk * MSM_BSPLIT * nsides, 128, st, max_chunks, nsides, nbk,
              (const uint32_t*)chunk_off, (const G2JStore*)chunks, BP));
+  }
   RET(reduce_rows(BP, tmp, nbk * nsides, MSM_BSPLIT, st));  // B[side][b] = BP[side * nbk + b]
   RET(launch("k_msm_slices", k_msm_slices, nsides * nwin * MSM_C * MSM_SLICE_LANES, 128, st, nsides, nwin, (const G2JStore*)BP, P1));
   RET(reduce_rows(P1, tmp, nsides * nwin * MSM_C, MSM_SLICE_LANES, st));  // S[side][w][k] = P1[...]
@@ -466,7 +503,7 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
   G2JStore* win = nullptr;
   if (b.nslots == 1) {
     // T = sum alpha_r V_r and K = sum alpha_r Q_r in one MSM (shared bucket sort)
-    RET(msm_run(b.R, seed, active, V, b.Q, batched_sub != 0, &msm, &win, st));
+    RET(msm_run(b.R, seed, active, V, b.Q, batched_sub != 0, g_ctx.phased && b.k == 1, &msm, &win, st));
     T = msm;
     K = msm + 1;
   } else {
@@ -486,7 +523,7 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
     K = Kp;
     // Kc = sum over the active rounds of alpha_r Q_r (one MSM), Xc = sum_s beta_s X_s
     G2JStore* kmsm;
-    RET(msm_run(b.R, seed, active, b.Q, nullptr, false, &kmsm, nullptr, st));
+    RET(msm_run(b.R, seed, active, b.Q, nullptr, false, g_ctx.phased, &kmsm, nullptr, st));
     Kc = kmsm;
     RET(wsT(S_XC, 1, &Xc));
     RET(launch("k_key_combine", k_key_combine, 256, 256, st, b.nslots, seed, b.keys, b.key_status, Xc));

@@ -535,6 +535,68 @@ DGH Fp2 fp2_sqr(const Fp2& a) {
   Fp m = fp_mul(a.c0, a.c1);
   return Fp2{fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(m)};
 }
+// Fp2 products as one out-of-line call each, operands and result in VGPRs (48 / 24 scalar arguments, the
+// three or two Fp products inlined in the callee).  A caller of the Fp-level calls must keep its whole live set
+// in the ~108 callee-saved VGPRs across every one of them (or spill it to scratch); across one Fp2-level call
+// the Karatsuba temporaries stay inside the callee, so a curve formula's live set fits (g2_madd_lds).
+#if defined(__HIP_DEVICE_COMPILE__) && DG_FP_CALL == 1
+__device__ __noinline__ Fp2 fp2_mul_r(DG_P12(a), DG_P12(b), DG_P12(c), DG_P12(d)) {
+  const Fp x0{{DG_L12(a)}}, x1{{DG_L12(b)}}, y0{{DG_L12(c)}}, y1{{DG_L12(d)}};
+  const Fp t0 = fp28_mul(x0, y0);
+  const Fp t1 = fp28_mul(x1, y1);
+  const Fp t2 = fp28_mul(fp_add(x0, x1), fp_add(y0, y1));
+  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+__device__ __noinline__ Fp2 fp2_sqr_r(DG_P12(a), DG_P12(b)) {
+  const Fp x0{{DG_L12(a)}}, x1{{DG_L12(b)}};
+  const Fp m = fp28_mul(x0, x1);
+  return Fp2{fp28_mul(fp_add(x0, x1), fp_sub(x0, x1)), fp_dbl(m)};
+}
+DGI Fp2 fp2_mul_rc(const Fp2& a, const Fp2& b) { return fp2_mul_r(DG_A12(a.c0), DG_A12(a.c1), DG_A12(b.c0), DG_A12(b.c1)); }
+DGI Fp2 fp2_sqr_rc(const Fp2& a) { return fp2_sqr_r(DG_A12(a.c0), DG_A12(a.c1)); }
+#else
+DGI Fp2 fp2_mul_rc(const Fp2& a, const Fp2& b) { return fp2_mul(a, b); }
+DGI Fp2 fp2_sqr_rc(const Fp2& a) { return fp2_sqr(a); }
+#endif
+// Inlined and serialised: each Fp product completes before the next one's operands are formed (DG_PIN_FP: an
+// empty asm that reads and writes every limb, and volatile asms keep their order), so at most one product's
+// temporaries are live -- the scheduler otherwise interleaves the three independent Karatsuba products and a
+// curve formula around them outgrows 256 VGPRs (k_msm_aff_add: 300 VGPRs unserialised).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DG_PIN_FP(f)                                                                                                  \
+  asm volatile("" : "+v"((f).l[0]), "+v"((f).l[1]), "+v"((f).l[2]), "+v"((f).l[3]), "+v"((f).l[4]), "+v"((f).l[5]), \
+               "+v"((f).l[6]), "+v"((f).l[7]), "+v"((f).l[8]), "+v"((f).l[9]), "+v"((f).l[10]), "+v"((f).l[11]))
+#else
+#define DG_PIN_FP(f) ((void)0)
+#endif
+DGI Fp fp_mul_seq(Fp a, Fp b) {
+  DG_PIN_FP(a);
+  DG_PIN_FP(b);
+  Fp r = fp_mul_inl(a, b);
+  DG_PIN_FP(r);
+  return r;
+}
+DGI Fp2 fp2_mul_seq(const Fp2& a, const Fp2& b) {
+  const Fp t0 = fp_mul_seq(a.c0, b.c0);
+  const Fp t1 = fp_mul_seq(a.c1, b.c1);
+  const Fp t2 = fp_mul_seq(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+DGI Fp2 fp2_sqr_seq(const Fp2& a) {
+  const Fp m = fp_mul_seq(a.c0, a.c1);
+  return Fp2{fp_mul_seq(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(m)};
+}
+// and inlined (the products' code at every call site)
+DGI Fp2 fp2_mul_in(const Fp2& a, const Fp2& b) {
+  const Fp t0 = fp_mul_inl(a.c0, b.c0);
+  const Fp t1 = fp_mul_inl(a.c1, b.c1);
+  const Fp t2 = fp_mul_inl(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+DGI Fp2 fp2_sqr_in(const Fp2& a) {
+  const Fp m = fp_mul_inl(a.c0, a.c1);
+  return Fp2{fp_mul_inl(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(m)};
+}
 DGI Fp2 fp2_mul_fp(const Fp2& a, const Fp& b) { return Fp2{fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
 DGI Fp2 fp2_mul_xi(const Fp2& a) { return Fp2{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }  // (1+u) a
 DGI Fp fp2_norm(const Fp2& a) { return fp_add(fp_sqr(a.c0), fp_sqr(a.c1)); }

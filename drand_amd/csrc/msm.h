@@ -36,6 +36,12 @@ constexpr uint32_t MSM_TWIN = 10, MSM_WT = MSM_WIN + MSM_TWIN;  // test windows 
 constexpr uint32_t MSM_NBT = MSM_WT * MSM_NB;                   // 4608 bucket slots with the test windows
 // keyed MSM bucket key: (window, digit, key set), the set fastest
 DGI uint32_t kmsm_key(uint32_t w, uint32_t d, uint32_t set, uint32_t nsets) { return (w * MSM_NB + d) * nsets + set; }
+#ifndef DG_MSM_LDS
+#define DG_MSM_LDS 1  // chunk sums: 1 running sum in LDS, 2 in registers (g2_madd_lds form), 0 round-2 form
+#endif
+#ifndef DG_MSM_WAVES
+#define DG_MSM_WAVES DG_HOT_WAVES  // min waves per SIMD of the chunk sums
+#endif
 constexpr uint32_t MSM_CHUNK = 8;   // points per first-level lane
 constexpr uint32_t MSM_BSPLIT = 32;  // lanes per bucket at the second level
 constexpr uint32_t MSM_SLICE_LANES = 64;  // lanes per (side, window, bit slice) in k_msm_slices
@@ -122,7 +128,7 @@ DG_KERNEL void __launch_bounds__(256) k_msm_scatter(uint32_t R, uint32_t nwin, c
 #if defined(__HIP__) && DG_TU_HOT
 // lane g: side = g / max_chunks, chunk c = g % max_chunks; sums its chunk of points of side `side`
 // (side 0: PA, side 1: PB) into out[side * max_chunks + c]; side 1 has no test windows (buckets >= MSM_NBK)
-DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, uint32_t nbk, const uint32_t* count,
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, uint32_t nbk, const uint32_t* count,
                                                    const uint32_t* offset, const uint32_t* chunk_off,
                                                    const uint32_t* list, const G2JStore* PA, const G2JStore* PB,
                                                    G2JStore* out) {
@@ -144,8 +150,26 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_ch
   uint32_t last = offset[b] + count[b];
   if (last > first + MSM_CHUNK) last = first + MSM_CHUNK;
   const G2JStore* P = side ? PB : PA;
-  G2J acc = load_g2j(P[list[first]]);
   const Fp2 one = fp2_one();
+#if DG_MSM_LDS
+  // the running sum lives in LDS (36 KB per workgroup, 4 workgroups per CU at 2 waves/SIMD) or in registers
+#if DG_MSM_LDS == 1
+  __shared__ G2JStore s_acc[128];
+  G2JStore& acc = s_acc[threadIdx.x];
+#else
+  G2JStore acc;
+#endif
+  acc = P[list[first]];
+  for (uint32_t i = first + 1; i < last; ++i) {
+    const G2JStore& q = P[list[i]];
+    if (fp2_eq(q.z, one))
+      g2_madd_lds(acc, q.x, q.y);
+    else if (!fp2_is_zero(q.z))
+      store_g2j(acc, g2_add_rare(load_g2j(acc), load_g2j(q)));
+  }
+  out[side * max_chunks + c] = acc;
+#else
+  G2J acc = load_g2j(P[list[first]]);
   for (uint32_t i = first + 1; i < last; ++i) {
     const G2JStore& q = P[list[i]];
     // signatures and hashes enter normalised (Z = 1) or as the identity (Z = 0): mixed additions (7M + 4S
@@ -156,13 +180,182 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_ch
       acc = g2_add_rare(acc, load_g2j(q));
   }
   store_g2j(out[side * max_chunks + c], acc);
+#endif
 }
 
 #elif defined(__HIP__)
-DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, uint32_t nbk, const uint32_t* count,
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_msm_chunks(uint32_t max_chunks, uint32_t nsides, uint32_t nbk, const uint32_t* count,
                                                    const uint32_t* offset, const uint32_t* chunk_off,
                                                    const uint32_t* list, const G2JStore* PA, const G2JStore* PB,
                                                    G2JStore* out);
+#endif
+
+// ---------------------------------------------------------------------------------------------------
+// Affine first levels (single-key path, every input point with Z = 1 or Z = 0).  Instead of one lane summing
+// a chunk of 8 points with mixed Jacobian additions (7M + 4S in Fp2 each, 29 Fp products), the points of every
+// bucket are summed pairwise in MSM_AFF_L levels of affine additions, each level's denominators inverted
+// together (Montgomery's trick over the whole batch, batch_inv):
+//   lambda = (y2 - y1) / (x2 - x1), x3 = lambda^2 - x1 - x2, y3 = lambda (x1 - x3) - y1
+// 1/d = conj(d) / N(d) with N(d) = d0^2 + d1^2 in Fp, so one Fp inversion per level serves every pair: about
+// 2 (norm) + 3 (batch inversion) + 2 (conj) + 8 (lambda, x3, y3) = 15 Fp products per addition.
+// Level l pairs the entries i and i + 2^l of each group of 2^(l+1) consecutive entries of a bucket (bucket order of
+// the shared list) and writes the sum in place at i (A: one G2AStore per list position and side); after
+// MSM_AFF_L levels A[offset[b] + k 2^L] holds the k-th chunk sum of bucket b, which k_msm_buckets_aff reads.
+// Exceptional pairs are exact: P + (-P) = identity, P + P by the tangent (d = 2y; E' has no 2-torsion, h2 is
+// odd), identity operands pass the other one through; they take no inversion (denominator 1).
+constexpr uint32_t MSM_AFF_L = 3;  // affine levels: chunk sums of 2^3 = 8 entries
+DGI G2A aff_src0(const G2JStore& p) { return G2A{p.x, p.y, fp2_is_zero(p.z)}; }
+DGI G2A aff_srcA(const G2AStore& p) { return G2A{p.x, p.y, p.inf != 0}; }
+// group g of level l (groups of 2^(l+1) entries of one bucket) -> its first entry i and bucket end
+DGI bool aff_group(uint32_t nbk, const uint32_t* count, const uint32_t* offset, const uint32_t* gofs, uint32_t l,
+                   uint32_t g, uint32_t& i, uint32_t& end) {
+  uint32_t lo = 0, hi = nbk;
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) / 2;
+    if (gofs[mid] <= g)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  i = offset[lo] + ((g - gofs[lo]) << (l + 1));
+  end = offset[lo] + count[lo];
+  return i + (1u << l) < end;  // has a partner
+}
+
+#if defined(__HIP__) && DG_TU_LIB
+// offset / cursor as k_msm_scan, and gofs[l * (nbk + 1) + b] = exclusive scan of ceil(count / 2^(l+1)) for the
+// MSM_AFF_L levels (gofs[l * (nbk + 1) + nbk] = groups of level l).  One workgroup of 256 lanes.
+DG_KERNEL void __launch_bounds__(256) k_msm_scan_aff(uint32_t nbk, const uint32_t* count, uint32_t* offset,
+                                                     uint32_t* cursor, uint32_t* gofs) {
+  __shared__ uint32_t s_cnt[256], s_g[MSM_AFF_L][256];
+  const uint32_t t = threadIdx.x, per = nbk / 256;
+  uint32_t c = 0, k[MSM_AFF_L] = {};
+  for (uint32_t j = 0; j < per; ++j) {
+    uint32_t v = count[t * per + j];
+    c += v;
+    for (uint32_t l = 0; l < MSM_AFF_L; ++l) k[l] += (v + (2u << l) - 1) >> (l + 1);
+  }
+  s_cnt[t] = c;
+  for (uint32_t l = 0; l < MSM_AFF_L; ++l) s_g[l][t] = k[l];
+  __syncthreads();
+  if (t <= MSM_AFF_L) {  // lane 0: the entry scan, lane 1 + l: level l's group scan
+    uint32_t* s = t == 0 ? s_cnt : s_g[t - 1];
+    uint32_t a = 0;
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t x = s[i];
+      s[i] = a;
+      a += x;
+    }
+    if (t > 0) gofs[(t - 1) * (nbk + 1) + nbk] = a;
+  }
+  __syncthreads();
+  uint32_t a = s_cnt[t], b[MSM_AFF_L];
+  for (uint32_t l = 0; l < MSM_AFF_L; ++l) b[l] = s_g[l][t];
+  for (uint32_t j = 0; j < per; ++j) {
+    uint32_t i = t * per + j, v = count[i];
+    offset[i] = a;
+    cursor[i] = a;
+    a += v;
+    for (uint32_t l = 0; l < MSM_AFF_L; ++l) {
+      gofs[l * (nbk + 1) + i] = b[l];
+      b[l] += (v + (2u << l) - 1) >> (l + 1);
+    }
+  }
+}
+#endif
+
+#if defined(__HIP__) && DG_TU_HOT
+// level l, lane t = side * maxg + g: the norm of the denominator of group g's pair (1 where no inversion is
+// needed, and on the lanes past the level's group count, so every value batch_inv sees is a field element)
+DG_KERNEL void __launch_bounds__(128) k_msm_aff_den(uint32_t l, uint32_t maxg, uint32_t nsides, uint32_t nbk,
+                                                    const uint32_t* count, const uint32_t* offset, const uint32_t* gofs,
+                                                    const uint32_t* list, const G2JStore* PA, const G2JStore* PB,
+                                                    const G2AStore* A, uint32_t E, Fp* den) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= maxg * nsides) return;
+  const uint32_t side = t / maxg, g = t % maxg;
+  Fp n = fp_one();
+  uint32_t i, end;
+  if (g < gofs[side ? MSM_NBK : nbk] && aff_group(nbk, count, offset, gofs, l, g, i, end)) {
+    const uint32_t j = i + (1u << l);
+    G2A p, q;
+    if (l == 0) {
+      const G2JStore* P = side ? PB : PA;
+      p = aff_src0(P[list[i]]);
+      q = aff_src0(P[list[j]]);
+    } else {
+      p = aff_srcA(A[(size_t)side * E + i]);
+      q = aff_srcA(A[(size_t)side * E + j]);
+    }
+    n = g2_aff_den(p, q, g2_aff_kind(p, q));
+  }
+  den[t] = n;
+}
+
+// level l: the pair sums with the inverted norms (same lanes as k_msm_aff_den); level 0 also copies the unpaired
+// entries into A
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_aff_add(uint32_t l, uint32_t maxg, uint32_t nsides,
+                                                                 uint32_t nbk, const uint32_t* count,
+                                                                 const uint32_t* offset, const uint32_t* gofs,
+                                                                 const uint32_t* list, const G2JStore* PA,
+                                                                 const G2JStore* PB, G2AStore* A, uint32_t E,
+                                                                 const Fp* ninv) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= maxg * nsides) return;
+  const uint32_t side = t / maxg, g = t % maxg;
+  if (g >= gofs[side ? MSM_NBK : nbk]) return;
+  uint32_t i, end;
+  const bool pair = aff_group(nbk, count, offset, gofs, l, g, i, end);
+  G2AStore* Aside = A + (size_t)side * E;
+  if (!pair && l > 0) return;  // the lone entry already sits at i
+  G2A p, q;
+  if (l == 0) {
+    const G2JStore* P = side ? PB : PA;
+    p = aff_src0(P[list[i]]);
+    if (!pair) {
+      store_g2a(Aside[i], p);
+      return;
+    }
+    q = aff_src0(P[list[i + 1]]);
+  } else {
+    p = aff_srcA(Aside[i]);
+    q = aff_srcA(Aside[i + (1u << l)]);
+  }
+  const G2A r = g2_aff_sum(p, q, g2_aff_kind(p, q), ninv[t]);
+  store_g2a(Aside[i], r);
+}
+#elif defined(__HIP__)
+DG_KERNEL void __launch_bounds__(128) k_msm_aff_den(uint32_t l, uint32_t maxg, uint32_t nsides, uint32_t nbk,
+                                                    const uint32_t* count, const uint32_t* offset, const uint32_t* gofs,
+                                                    const uint32_t* list, const G2JStore* PA, const G2JStore* PB,
+                                                    const G2AStore* A, uint32_t E, Fp* den);
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_aff_add(uint32_t l, uint32_t maxg, uint32_t nsides,
+                                                                 uint32_t nbk, const uint32_t* count,
+                                                                 const uint32_t* offset, const uint32_t* gofs,
+                                                                 const uint32_t* list, const G2JStore* PA,
+                                                                 const G2JStore* PB, G2AStore* A, uint32_t E,
+                                                                 const Fp* ninv);
+#endif
+
+#if defined(__HIP__) && DG_TU_LIB
+// the bucket sums from the affine chunk sums: lane (side, b, q < MSM_BSPLIT) adds chunks q, q + MSM_BSPLIT, ...
+// of bucket b (A[offset[b] + c 2^L]) with mixed additions; the partials are then row-summed as before
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_buckets_aff(uint32_t nsides, uint32_t nbk, const uint32_t* count,
+                                                                       const uint32_t* offset, const G2AStore* A,
+                                                                       uint32_t E, G2JStore* BP) {
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nbk * MSM_BSPLIT * nsides) return;
+  uint32_t q = g % MSM_BSPLIT, sb = g / MSM_BSPLIT;
+  uint32_t side = sb / nbk, b = sb % nbk;
+  const uint32_t nch = side && b >= MSM_NBK ? 0u : (count[b] + (1u << MSM_AFF_L) - 1) >> MSM_AFF_L;
+  const G2AStore* As = A + (size_t)side * E + offset[b];
+  G2J acc = jac_infinity<Fp2>();
+  for (uint32_t c = q; c < nch; c += MSM_BSPLIT) {
+    const G2A a = load_g2a(As[c << MSM_AFF_L]);
+    if (!a.inf) acc = jac_add_aff(acc, a.x, a.y);
+  }
+  store_g2j(BP[g], acc);
+}
 #endif
 
 #if defined(__HIP__) && DG_TU_LIB
@@ -367,7 +560,7 @@ DG_KERNEL void __launch_bounds__(256) k_kmsm_scatter(uint32_t N, uint32_t k, uin
 #endif
 // hot translation unit (kernels_hot.hip: flat, 2 waves/SIMD; measured -27% / -36%)
 #if defined(__HIP__) && DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_kmsm_chunks(uint32_t max_chunks, uint32_t nkeys,
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_chunks(uint32_t max_chunks, uint32_t nkeys,
                                                                    const uint32_t* count, const uint32_t* offset,
                                                                    const uint32_t* chunk_off, const uint32_t* list,
                                                                    const G2AStore* S, G2JStore* out) {
@@ -384,15 +577,30 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_kmsm_chunks(uint32_t max_c
   uint32_t first = offset[lo] + (c - chunk_off[lo]) * MSM_CHUNK;
   uint32_t last = offset[lo] + count[lo];
   if (last > first + MSM_CHUNK) last = first + MSM_CHUNK;
+#if DG_MSM_LDS
+#if DG_MSM_LDS == 1
+  __shared__ G2JStore s_acc[128];
+  G2JStore& acc = s_acc[threadIdx.x];
+#else
+  G2JStore acc;
+#endif
+  store_g2j(acc, jac_from_aff(load_g2a(S[list[first]])));
+  for (uint32_t i = first + 1; i < last; ++i) {
+    const G2AStore& q = S[list[i]];
+    if (!q.inf) g2_madd_lds(acc, q.x, q.y);  // the identity encoding decodes (status OK)
+  }
+  out[c] = acc;
+#else
   G2J acc = jac_from_aff(load_g2a(S[list[first]]));
   for (uint32_t i = first + 1; i < last; ++i) {
     const G2AStore& q = S[list[i]];
     if (!q.inf) acc = g2_madd_lean(acc, q.x, q.y);  // the identity encoding decodes (status OK)
   }
   store_g2j(out[c], acc);
+#endif
 }
 #elif defined(__HIP__)
-DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_kmsm_chunks(uint32_t max_chunks, uint32_t nkeys,
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_chunks(uint32_t max_chunks, uint32_t nkeys,
                                                                    const uint32_t* count, const uint32_t* offset,
                                                                    const uint32_t* chunk_off, const uint32_t* list,
                                                                    const G2AStore* S, G2JStore* out);

@@ -194,3 +194,23 @@ extern "C" int hc_msm4_check(const uint8_t* sigs384, const uint8_t* keys192, con
   }
   return jac_eq(jac_msm4_sac(s, d), s_ref) && jac_eq(jac_msm4_sac(x, d), x_ref) ? 1 : 0;
 }
+
+// One affine pair addition of the MSM's affine levels (curve.h g2_aff_kind / g2_aff_den / g2_aff_sum, the inverse
+// supplied as the batch inversion would) against the Jacobian addition.  mode 0: P + Q, 1: P + P, 2: P + (-P),
+// 3: O + Q, 4: P + O, 5: O + O.  1 if both agree, -1 if a signature does not decode.
+extern "C" int hc_aff_add_check(const uint8_t* sig_a, const uint8_t* sig_b, int mode) {
+  G2A a, b;
+  if (!g2_decompress(a, sig_a, false) || !g2_decompress(b, sig_b, false)) return -1;
+  const G2A O{fp2_zero(), fp2_zero(), true};
+  G2A p = a, q = b;
+  if (mode == 1) q = a;
+  if (mode == 2) q = G2A{a.x, fp2_neg(a.y), false};
+  if (mode == 3 || mode == 5) p = O;
+  if (mode == 4 || mode == 5) q = O;
+  const uint32_t kind = g2_aff_kind(p, q);
+  const Fp den = g2_aff_den(p, q, kind);
+  const G2A r = g2_aff_sum(p, q, kind, fp_inv(den));
+  const G2J want = jac_add(jac_from_aff(p), jac_from_aff(q));
+  if (r.inf != jac_is_inf(want)) return 0;
+  return jac_eq(jac_from_aff(r), want) ? 1 : 0;
+}

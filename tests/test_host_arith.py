@@ -183,3 +183,13 @@ def test_pairing_host_build_matches_twin(hc):
     for i, r in enumerate(ch["rounds"][:4]):
         msg, sig = hx(r["msg"]), hx(ch["rounds"][(i + (i % 2)) % 64]["sig"])
         assert hc.hc_verify(pk, msg, len(msg), sig) == (0 if i % 2 == 0 else 1)
+
+
+def test_affine_pair_addition_matches_jacobian(hc):
+    """The MSM's affine levels (msm.h k_msm_aff_*): chord, tangent, P + (-P) and identity operands through
+    curve.h g2_aff_sum with the inverse supplied as the batch inversion would, against the Jacobian addition."""
+    c = load("chain_t3n5.json")
+    sigs = [hx(r["sig"]) for r in c["rounds"][:6]]
+    for i in range(len(sigs) - 1):
+        for mode in range(6):
+            assert hc.hc_aff_add_check(sigs[i], sigs[i + 1], mode) == 1, (i, mode)
