@@ -59,6 +59,21 @@ DGI Fp2 fp2_mul_b3(const Fp2& c) {
 #if defined(__HIP__)
 constexpr int CO_THREADS = 128;
 
+// The per-lane product of a phase.  Out of line by default: a cooperative kernel has dozens of phases, and with
+// the ~650-instruction product inlined at each (k_pair_miller_coop: 140k instructions) one Miller step streams
+// several hundred KB of code through the 64 KB instruction cache with only two waves to hide the fetches; one
+// shared routine stays resident.  DG_COOP_INLINE=1 inlines it (A/B).
+#ifndef DG_COOP_INLINE
+#define DG_COOP_INLINE 0
+#endif
+__device__ __forceinline__ Fp co_mul(const Fp& a, const Fp& b) {
+#if DG_COOP_INLINE
+  return fp_mul_inl(a, b);
+#else
+  return fp_mul(a, b);
+#endif
+}
+
 // product jobs: o = a * b
 struct CoM2 {
   const Fp2* a;
@@ -102,11 +117,11 @@ __device__ __forceinline__ void co_phase(const CoM2 (&j2)[N2], const CoM1 (&j1)[
   if (t < 3 * N2) {
     int q = t / 3, m = t - 3 * q;
     CoM2 j = co_pick(j2, q);
-    tmp[t] = fp_mul_inl(co_kara_operand(*j.a, m), co_kara_operand(*j.b, m));
+    tmp[t] = co_mul(co_kara_operand(*j.a, m), co_kara_operand(*j.b, m));
   } else if (t < 3 * N2 + 2 * N1) {
     int u = t - 3 * N2, q = u / 2, m = u - 2 * q;
     CoM1 j = co_pick(j1, q);
-    tmp[t] = fp_mul_inl(m ? j.a->c1 : j.a->c0, *j.b);
+    tmp[t] = co_mul(m ? j.a->c1 : j.a->c0, *j.b);
   }
   __syncthreads();
   if (t < 2 * N2) {
@@ -131,7 +146,7 @@ __device__ __forceinline__ void co_phase(const CoM2 (&j2)[N2], Fp* tmp) {
   if (t < 3 * N2) {
     int q = t / 3, m = t - 3 * q;
     CoM2 j = co_pick(j2, q);
-    tmp[t] = fp_mul_inl(co_kara_operand(*j.a, m), co_kara_operand(*j.b, m));
+    tmp[t] = co_mul(co_kara_operand(*j.a, m), co_kara_operand(*j.b, m));
   }
   __syncthreads();
   if (t < 2 * N2) {
@@ -156,13 +171,13 @@ __device__ __forceinline__ void co_phase_f(LD2 ld2, ST2 st2, LD1 ld1, ST1 st1, F
     int q = t / 3, m = t - 3 * q;
     Fp2 a, b;
     ld2(q, a, b);
-    tmp[t] = fp_mul_inl(co_kara_operand(a, m), co_kara_operand(b, m));
+    tmp[t] = co_mul(co_kara_operand(a, m), co_kara_operand(b, m));
   } else if (t < 3 * N2 + 2 * N1) {
     int u = t - 3 * N2, q = u / 2, m = u - 2 * q;
     Fp2 a;
     Fp b;
     ld1(q, a, b);
-    tmp[t] = fp_mul_inl(m ? a.c1 : a.c0, b);
+    tmp[t] = co_mul(m ? a.c1 : a.c0, b);
   }
   __syncthreads();
   if (t < 2 * N2) {
@@ -270,7 +285,7 @@ __device__ __forceinline__ void co_fp12_mul(Fp12W* dst, const Fp12W* a, const Fp
   const int t = threadIdx.x;
   if (t < 108) {
     int q = t / 3, m = t - 3 * q;
-    s->tmp[t] = fp_mul_inl(co_kara_operand(a->e[q / 6], m), co_kara_operand(b->e[q % 6], m));
+    s->tmp[t] = co_mul(co_kara_operand(a->e[q / 6], m), co_kara_operand(b->e[q % 6], m));
   }
   __syncthreads();
   if (t < 72) {
@@ -286,7 +301,7 @@ __device__ __forceinline__ void co_fp12_mul_line(Fp12W* dst, const Fp12W* a, con
   if (t < 54) {
     int q = t / 3, m = t - 3 * q;  // q = 3 i + jj, line slot {0, 2, 3}[jj]
     int i = q / 3, jj = q - 3 * i;
-    s->tmp[t] = fp_mul_inl(co_kara_operand(a->e[i], m), co_kara_operand(L->e[jj == 0 ? 0 : jj + 1], m));
+    s->tmp[t] = co_mul(co_kara_operand(a->e[i], m), co_kara_operand(L->e[jj == 0 ? 0 : jj + 1], m));
   }
   __syncthreads();
   if (t < 36) {
@@ -312,7 +327,7 @@ __device__ __forceinline__ void co_fp12_frob(Fp12W* dst, const Fp12W* a, CoGT* s
   const int t = threadIdx.x;
   if (t < 18) {
     int q = t / 3, m = t - 3 * q;
-    s->tmp[t] = fp_mul_inl(co_kara_operand(fp2_conj(a->e[q]), m), co_kara_operand(s->gamma[q], m));
+    s->tmp[t] = co_mul(co_kara_operand(fp2_conj(a->e[q]), m), co_kara_operand(s->gamma[q], m));
   }
   __syncthreads();
   if (t < 6) dst->e[t] = co_kara_combine(s->tmp + 3 * t);

@@ -103,6 +103,8 @@ struct Ctx {
   bool phased = getenv("DG_FUSED") == nullptr;
   // single-key MSM first levels as mixed Jacobian chunk sums (DG_MSM_JAC=1: A/B only) instead of affine levels
   bool msm_jac = getenv("DG_MSM_JAC") != nullptr;
+  // batch inversions by the chunked form only (DG_BINV_CHUNKED=1: A/B only) instead of the block tree
+  bool binv_chunked = getenv("DG_BINV_CHUNKED") != nullptr;
 };
 
 std::mutex g_mu;
@@ -127,7 +129,7 @@ enum Slot {
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
   S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_BINV, S_NV, S_NVINV,
-  S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_COUNT
+  S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_BINV_PRE, S_BINV_ROOTS, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -607,14 +609,29 @@ int decode_key(const uint8_t* pk48_host, hipStream_t st, G1AStore** keys, uint8_
 
 // out[i] = 1 / vals[i] (0 for 0) for n Fp values on the device: Montgomery's trick over chunks of BINV_C, a tree of
 // chunk products, one safegcd inversion at the root (phases.h k_binv_*)
+int batch_inv_chunked(uint32_t n, const Fp* vals, Fp* out, hipStream_t st, Slot slot);
 int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st) {
+  constexpr uint32_t PER = BINV_T * BINV_K;
+  if (n <= 2 * PER || g_ctx.binv_chunked) return batch_inv_chunked(n, vals, out, st, S_BINV);
+  // block tree (phases.h k_binv_blk_*): per block of PER values a root; the roots by the chunked form
+  const uint32_t nb = (n + PER - 1) / PER;
+  Fp *pre, *roots, *rinv;
+  RET(wsT(S_BINV_PRE, n, &pre));
+  RET(wsT(S_BINV_ROOTS, 2 * (size_t)nb, &roots));
+  rinv = roots + nb;
+  RET(launch("k_binv_blk_up", k_binv_blk_up, nb * BINV_T, BINV_T, st, n, vals, pre, roots));
+  RET(batch_inv_chunked(nb, roots, rinv, st, S_BINV));
+  return launch("k_binv_blk_down", k_binv_blk_down, nb * BINV_T, BINV_T, st, n, vals, (const Fp*)pre, (const Fp*)rinv,
+                out);
+}
+int batch_inv_chunked(uint32_t n, const Fp* vals, Fp* out, hipStream_t st, Slot slot) {
   std::vector<uint32_t> sizes{n};
   while (sizes.back() > BINV_C) sizes.push_back((sizes.back() + BINV_C - 1) / BINV_C);
   const size_t L = sizes.size();
   size_t total = 0;
   for (size_t l = 0; l < L; ++l) total += 3 * (size_t)sizes[l];
   Fp* buf;
-  RET(wsT(S_BINV, total, &buf));
+  RET(wsT(slot, total, &buf));
   // level l: in[l] (the values), pre[l], inv[l] (their inverses); in[0] = vals, inv[0] = out
   std::vector<const Fp*> in(L);
   std::vector<Fp*> pre(L), inv(L);

@@ -43,6 +43,7 @@ struct DecState {
 };
 constexpr uint32_t DEC_PENDING = 1, DEC_SIGN = 2, DEC_INF = 4;
 constexpr uint32_t BINV_C = 32;  // chunk of the batch inversion (k_binv_*)
+constexpr uint32_t BINV_T = 256, BINV_K = 4;  // block-tree batch inversion (k_binv_blk_*): lanes x values per lane
 
 // ------------------------------------------------------------------------------ exponentiation
 // x^((p-3)/4) by a width-4 sliding-window schedule (the 8 odd powers x, x^3, .., x^15; 376 squarings and 85
@@ -367,6 +368,64 @@ DG_KERNEL void __launch_bounds__(64) k_binv_root(uint32_t n, const Fp* vals, Fp*
   out[0] = fp_is_zero(vals[0]) ? fp_zero() : I;
 }
 
+// ---- the same batch inversion as a block tree: a workgroup of BINV_T lanes takes BINV_T * BINV_K consecutive
+// values (BINV_K per lane: running products in `pre`, the last one is the lane's leaf), multiplies the leaves up a
+// binary tree in LDS and writes the root; the roots are inverted by the chunked form above (n / 1024 values); the
+// down kernel rebuilds the tree, sends each node's inverse to its children (inv(left) = inv(node) * right) and
+// walks each lane's values back.  Per value ~3 products, every lane busy: the chunked form left n / 32 lanes
+// with 32 dependent products each (k_binv_down 113 us per 200k values, one pass per level).
+__device__ __forceinline__ void binv_tree_up(Fp* T, uint32_t l) {
+#pragma unroll 1
+  for (uint32_t s = BINV_T / 2; s >= 1; s >>= 1) {
+    __syncthreads();
+    if (l < s) T[s + l] = fp_mul(T[2 * (s + l)], T[2 * (s + l) + 1]);
+  }
+  __syncthreads();
+}
+DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_up(uint32_t n, const Fp* vals, Fp* pre, Fp* roots) {
+  __shared__ Fp T[2 * BINV_T];
+  const uint32_t l = threadIdx.x, a = (blockIdx.x * BINV_T + l) * BINV_K;
+  Fp acc = fp_one();
+  for (uint32_t c = 0; c < BINV_K && a + c < n; ++c) {
+    const Fp v = vals[a + c];
+    acc = fp_mul(acc, fp_is_zero(v) ? fp_one() : v);
+    pre[a + c] = acc;
+  }
+  T[BINV_T + l] = acc;
+  binv_tree_up(T, l);
+  if (l == 0) roots[blockIdx.x] = T[1];
+}
+// rinv: the inverses of the block roots; out: the inverses of vals (zero for zero)
+DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_down(uint32_t n, const Fp* vals, const Fp* pre, const Fp* rinv,
+                                                         Fp* out) {
+  __shared__ Fp T[2 * BINV_T];
+  const uint32_t l = threadIdx.x, a = (blockIdx.x * BINV_T + l) * BINV_K;
+  const uint32_t b = a >= n ? a : (a + BINV_K < n ? a + BINV_K : n);  // this lane's values: [a, b)
+  T[BINV_T + l] = b > a ? pre[b - 1] : fp_one();
+  binv_tree_up(T, l);
+  if (l == 0) T[1] = rinv[blockIdx.x];
+#pragma unroll 1
+  for (uint32_t s = 1; s < BINV_T; s <<= 1) {
+    __syncthreads();
+    if (l < s) {
+      const uint32_t k = s + l;
+      const Fp I = T[k], left = T[2 * k], right = T[2 * k + 1];
+      T[2 * k] = fp_mul(I, right);
+      T[2 * k + 1] = fp_mul(I, left);
+    }
+  }
+  __syncthreads();
+  if (b == a) return;
+  Fp I = T[BINV_T + l];
+  for (uint32_t i = b - 1; i > a; --i) {
+    const Fp v = vals[i];
+    const bool z = fp_is_zero(v);
+    out[i] = z ? fp_zero() : fp_mul(I, pre[i - 1]);
+    I = z ? I : fp_mul(I, v);
+  }
+  out[a] = fp_is_zero(vals[a]) ? fp_zero() : I;
+}
+
 // decode of every item (96 B at sigs + stride*i + offset); items whose key did not decode are PK_DECODE
 DG_KERNEL void __launch_bounds__(128) k_dec_p1(uint32_t n, const uint8_t* sigs, uint32_t stride, uint32_t offset,
                                                const uint32_t* item_slot, const uint8_t* key_status, DecState* ds,
@@ -434,6 +493,9 @@ DG_KERNEL void __launch_bounds__(128) k_h2c_p1b(uint32_t R, H2cMap* st, const Fp
 DG_KERNEL void __launch_bounds__(128) k_binv_up(uint32_t n, const Fp* vals, Fp* pre, Fp* up);
 DG_KERNEL void __launch_bounds__(128) k_binv_down(uint32_t n, const Fp* vals, const Fp* pre, const Fp* inv, Fp* out);
 DG_KERNEL void __launch_bounds__(64) k_binv_root(uint32_t n, const Fp* vals, Fp* out);
+DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_up(uint32_t n, const Fp* vals, Fp* pre, Fp* roots);
+DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_down(uint32_t n, const Fp* vals, const Fp* pre, const Fp* rinv,
+                                                         Fp* out);
 DG_KERNEL void __launch_bounds__(128) k_h2c_p2(uint32_t M, H2cMap* st, Fp* ein, const Fp* eout);
 DG_KERNEL void __launch_bounds__(128) k_h2c_p3(uint32_t M, const H2cMap* st, const Fp* ein, const Fp* eout,
                                                G2JStore* iso);
