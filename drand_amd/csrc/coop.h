@@ -517,6 +517,19 @@ __device__ __forceinline__ void co_g2_mul_z(CoG2* O, const CoG2* P, CoG2Tmp* s) 
   CO_SERIAL(O->y = fp2_neg(O->y));
 }
 // P <- h_eff P = [z^2 - z - 1]P + [z - 1]psi(P) + psi^2(2P)  (as g2_clear_cofactor, curve.h); t: 4 CoG2
+// psi(P) == [z]P for one window sum of the batched subgroup check (msm.h), cooperatively; *fail = 1 if not
+// (a vector store; several workgroups may write the same 1).  p, zp, pp: LDS points, tmp: LDS scratch.
+template <class S>
+__device__ __forceinline__ void co_subgroup_check(const S* W, CoG2* p, CoG2* zp, CoG2* pp, CoG2Tmp* tmp,
+                                                  uint32_t* fail) {
+  CO_SERIAL({ *p = CoG2{W->x, W->y, W->z}; });
+  co_g2_mul_z(zp, p, tmp);
+  co_g2_psi(pp, p, tmp);
+  CO_SERIAL({
+    if (!jac_eq(G2J{pp->x, pp->y, pp->z}, G2J{zp->x, zp->y, zp->z})) *fail = 1u;
+  });
+}
+
 __device__ __forceinline__ void co_g2_clear_cofactor(CoG2* P, CoG2* t, CoG2Tmp* s) {
   CoG2 *t1 = &t[0], *t2 = &t[1], *t3 = &t[2], *p0 = &t[3];
   CO_SERIAL(*p0 = *P);

@@ -105,6 +105,8 @@ struct Ctx {
   bool msm_jac = getenv("DG_MSM_JAC") != nullptr;
   // batch inversions by the chunked form only (DG_BINV_CHUNKED=1: A/B only) instead of the block tree
   bool binv_chunked = getenv("DG_BINV_CHUNKED") != nullptr;
+  // batched subgroup check as its own launch after the final exponentiation (DG_SUB_SEPARATE=1: A/B only)
+  bool sub_separate = getenv("DG_SUB_SEPARATE") != nullptr;
 };
 
 std::mutex g_mu;
@@ -330,7 +332,7 @@ int bind_seed(const Batch& b, uint64_t seed, hipStream_t st, uint64_t** d_seed) 
 
 // Pippenger MSM (msm.h): out[0] = sum_r alpha_r PA_r, out[1] = sum_r alpha_r PB_r (PB may be null),
 // over the rounds with active[r] != 0.  With `test_windows` side A also gets the MSM_TWIN test windows of
-// the batched subgroup check; *win = its MSM_WT window sums (checked by k_msm_subgroup).
+// the batched subgroup check; *win = its MSM_WT window sums (checked beside the Miller loops, k_pair_miller_coop).
 int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st);
 
 // `affine`: every point of PA and PB has Z = 1 or Z = 0, so the first levels are affine additions (msm.h).
@@ -531,12 +533,16 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
     RET(launch("k_key_combine", k_key_combine, 256, 256, st, b.nslots, seed, b.keys, b.key_status, Xc));
   }
   const uint32_t npairs = b.nslots + (b.nslots > 1 ? 2u : 1u);
-  RET(launch("k_pair_miller_coop", k_pair_miller_coop, 128 * npairs, 128, st, b.nslots, seed, b.keys, K, T,
-             (const G1AStore*)Xc, Kc, f));
-  RET(launch("k_final_coop", k_final_coop, 128, 128, st, npairs, (const Fp12*)f, flag));
-  if (batched_sub)  // every window sum of the signature side: MSM_WT, or MSM_WT per key set
-    RET(launch("k_msm_subgroup", k_msm_subgroup, 128 * MSM_WT * (b.nslots > 1 ? b.nslots : 1u), 128, st,
-               (const G2JStore*)win, flag));
+  // the batched subgroup check's window sums ride in the Miller launch (extra workgroups); k_final_coop folds
+  // their verdict (flag[2]) into the batch's
+  const uint32_t nsub = batched_sub ? MSM_WT * (b.nslots > 1 ? b.nslots : 1u) : 0u;
+  HIPCHK(hipMemsetAsync(flag + 2, 0, 4, st));
+  const bool fuse_sub = !g_ctx.sub_separate;
+  RET(launch("k_pair_miller_coop", k_pair_miller_coop, 128 * (npairs + (fuse_sub ? nsub : 0u)), 128, st, b.nslots, seed,
+             b.keys, K, T, (const G1AStore*)Xc, Kc, f, npairs, (const G2JStore*)win, flag + 2));
+  if (!fuse_sub && nsub)
+    RET(launch("k_msm_subgroup", k_msm_subgroup, 128 * nsub, 128, st, (const G2JStore*)win, flag + 2));
+  RET(launch("k_final_coop", k_final_coop, 128, 128, st, npairs, (const Fp12*)f, flag, (const uint32_t*)flag + 2));
   // isolated items present?  The per-item pass decides on the device (no host round trip), so a batch
   // is one stream-ordered sequence of launches.
   HIPCHK(hipMemsetAsync(flag + 1, 0, 4, st));

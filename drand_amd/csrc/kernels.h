@@ -389,9 +389,12 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_sum_rows(uint32_t rows, u
 // K_s = -C_s and one more pair (Xc, h_eff Kc), Xc = sum_s beta_s X_s: prod_s e(beta_s X_s, h(Kc - C_s)).
 // f[s] = 1 when a side is the identity (every correction pair when all shares are present).
 #if DG_TU_LIB
+// Workgroups npairs.. (when win != null) run the batched subgroup check of window sum win[blockIdx.x - npairs]
+// instead (co_subgroup_check, *sub_fail = 1 on failure): independent of the pairs, so they share the launch.
 DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_pair_miller_coop(uint32_t nslots, const uint64_t* seedp, const G1AStore* keys,
                                                          const G2JStore* K, const G2JStore* T, const G1AStore* Xc,
-                                                         const G2JStore* Kc, Fp12* f) {
+                                                         const G2JStore* Kc, Fp12* f, uint32_t npairs,
+                                                         const G2JStore* win, uint32_t* sub_fail) {
   const uint64_t seed = *seedp;
   __shared__ CoGT gt;
   __shared__ CoML ml;
@@ -400,6 +403,10 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_pair_miller_coop(uint32_t
   __shared__ Fp12W F, L;
   __shared__ uint32_t skip;
   const uint32_t s = blockIdx.x;
+  if (s >= npairs) {
+    co_subgroup_check(win + (s - npairs), &Kp, &tp[0], &tp[1], &g2t, sub_fail);
+    return;
+  }
   if (s < nslots || s == nslots + 1) {
     CO_SERIAL({
       G2J k = load_g2j(s < nslots ? K[s] : Kc[0]);
@@ -445,7 +452,9 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_pair_miller_coop(uint32_t
 
 // product of the npairs Miller values and one final exponentiation on one 128-lane workgroup
 #if DG_TU_LIB
-DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_final_coop(uint32_t npairs, const Fp12* f, uint32_t* ok) {
+// ok = (product of the Miller values, final-exponentiated, is 1) and no subgroup failure (*sub_fail == 0)
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_final_coop(uint32_t npairs, const Fp12* f, uint32_t* ok,
+                                                                  const uint32_t* sub_fail) {
   __shared__ CoGT gt;
   __shared__ Fp12W F, G, S[7];
   const int t = threadIdx.x;
@@ -461,7 +470,7 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_final_coop(uint32_t npair
   if (t == 0) {
     bool one = fp2_eq(F.e[0], fp2_one());
     for (int k = 1; k < 6; ++k) one = one && fp2_is_zero(F.e[k]);
-    *ok = one ? 1u : 0u;
+    *ok = one && *sub_fail == 0u ? 1u : 0u;
   }
 }
 #endif

@@ -439,21 +439,14 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_final_coop(uint32_t n
 }
 
 // batched subgroup check: one 128-lane workgroup per window sum W[w] (the first side's, or every key
-// set's in the keyed MSM) tests psi(P) == [z]P
-// cooperatively (coop.h); any failure clears flag[0] (the batch verdict written by k_final_coop), so the
-// per-item pass runs
-DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_subgroup(const G2JStore* W, uint32_t* flag) {
+// set's in the keyed MSM) tests psi(P) == [z]P cooperatively (coop.h); any failure sets *fail, which
+// k_final_coop folds into the batch verdict, so the per-item pass runs.  The verify path runs these
+// workgroups inside the Miller launch (k_pair_miller_coop), beside the pairs; this standalone form is the
+// DG_SUB_SEPARATE=1 A/B.
+DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_subgroup(const G2JStore* W, uint32_t* fail) {
   __shared__ CoG2Tmp tmp;
   __shared__ CoG2 p, zp, pp;
-  CO_SERIAL({
-    G2J a = load_g2j(W[blockIdx.x]);
-    p = CoG2{a.x, a.y, a.z};
-  });
-  co_g2_mul_z(&zp, &p, &tmp);
-  co_g2_psi(&pp, &p, &tmp);
-  CO_SERIAL({
-    if (!jac_eq(G2J{pp.x, pp.y, pp.z}, G2J{zp.x, zp.y, zp.z})) flag[0] = 0u;
-  });
+  co_subgroup_check(W + blockIdx.x, &p, &zp, &pp, &tmp, fail);
 }
 
 // ---------------------------------------------------------------------------------------------------
