@@ -618,7 +618,8 @@ int decode_key(const uint8_t* pk48_host, hipStream_t st, G1AStore** keys, uint8_
 int batch_inv_chunked(uint32_t n, const Fp* vals, Fp* out, hipStream_t st, Slot slot);
 int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st) {
   constexpr uint32_t PER = BINV_T * BINV_K;
-  if (n <= 2 * PER || g_ctx.binv_chunked) return batch_inv_chunked(n, vals, out, st, S_BINV);
+  if (g_ctx.binv_chunked) return batch_inv_chunked(n, vals, out, st, S_BINV);
+  if (n <= BINV_T * BINV_R) return launch("k_binv_blk_root", k_binv_blk_root, BINV_T, BINV_T, st, n, vals, out);
   // block tree (phases.h k_binv_blk_*): per block of PER values a root; the roots by the chunked form
   const uint32_t nb = (n + PER - 1) / PER;
   Fp *pre, *roots, *rinv;
@@ -626,7 +627,10 @@ int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st) {
   RET(wsT(S_BINV_ROOTS, 2 * (size_t)nb, &roots));
   rinv = roots + nb;
   RET(launch("k_binv_blk_up", k_binv_blk_up, nb * BINV_T, BINV_T, st, n, vals, pre, roots));
-  RET(batch_inv_chunked(nb, roots, rinv, st, S_BINV));
+  if (nb <= BINV_T * BINV_R)
+    RET(launch("k_binv_blk_root", k_binv_blk_root, BINV_T, BINV_T, st, nb, (const Fp*)roots, rinv));
+  else
+    RET(batch_inv_chunked(nb, roots, rinv, st, S_BINV));  // n > 2M values (its own slot: no reentry)
   return launch("k_binv_blk_down", k_binv_blk_down, nb * BINV_T, BINV_T, st, n, vals, (const Fp*)pre, (const Fp*)rinv,
                 out);
 }

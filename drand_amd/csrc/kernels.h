@@ -937,5 +937,5 @@ DG_KERNEL void __launch_bounds__(128) k_sign(uint32_t n, const uint8_t* sc32, co
 
 }  // namespace dg
 
-#include "msm.h"
 #include "phases.h"
+#include "msm.h"

@@ -324,6 +324,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_aff_add(uint32_t l, ui
   const G2A r = g2_aff_sum(p, q, g2_aff_kind(p, q), ninv[t]);
   store_g2a(Aside[i], r);
 }
+
 #elif defined(__HIP__)
 DG_KERNEL void __launch_bounds__(128) k_msm_aff_den(uint32_t l, uint32_t maxg, uint32_t nsides, uint32_t nbk,
                                                     const uint32_t* count, const uint32_t* offset, const uint32_t* gofs,

@@ -44,6 +44,7 @@ struct DecState {
 constexpr uint32_t DEC_PENDING = 1, DEC_SIGN = 2, DEC_INF = 4;
 constexpr uint32_t BINV_C = 32;  // chunk of the batch inversion (k_binv_*)
 constexpr uint32_t BINV_T = 256, BINV_K = 4;  // block-tree batch inversion (k_binv_blk_*): lanes x values per lane
+constexpr uint32_t BINV_R = 8;                // values per lane of the single-workgroup root inversion
 
 // ------------------------------------------------------------------------------ exponentiation
 // x^((p-3)/4) by a width-4 sliding-window schedule (the 8 odd powers x, x^3, .., x^15; 376 squarings and 85
@@ -426,6 +427,45 @@ DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_down(uint32_t n, const Fp* v
   out[a] = fp_is_zero(vals[a]) ? fp_zero() : I;
 }
 
+// the roots of the block trees (n <= BINV_T * BINV_R values) inverted by one workgroup: running products of
+// BINV_R values per lane, the LDS tree, one safegcd on lane 0, back down -- one launch instead of the chunked
+// form's up / root / down chain
+DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_root(uint32_t n, const Fp* vals, Fp* out) {
+  __shared__ Fp T[2 * BINV_T];
+  const uint32_t l = threadIdx.x, a = l * BINV_R;
+  const uint32_t b = a >= n ? a : (a + BINV_R < n ? a + BINV_R : n);
+  Fp pre[BINV_R];
+  Fp acc = fp_one();
+  for (uint32_t i = a; i < b; ++i) {
+    const Fp v = vals[i];
+    acc = fp_mul(acc, fp_is_zero(v) ? fp_one() : v);
+    pre[i - a] = acc;
+  }
+  T[BINV_T + l] = acc;
+  binv_tree_up(T, l);
+  if (l == 0) T[1] = fp_inv(T[1]);
+#pragma unroll 1
+  for (uint32_t s = 1; s < BINV_T; s <<= 1) {
+    __syncthreads();
+    if (l < s) {
+      const uint32_t k = s + l;
+      const Fp I = T[k], left = T[2 * k], right = T[2 * k + 1];
+      T[2 * k] = fp_mul(I, right);
+      T[2 * k + 1] = fp_mul(I, left);
+    }
+  }
+  __syncthreads();
+  if (b == a) return;
+  Fp I = T[BINV_T + l];
+  for (uint32_t i = b - 1; i > a; --i) {
+    const Fp v = vals[i];
+    const bool z = fp_is_zero(v);
+    out[i] = z ? fp_zero() : fp_mul(I, pre[i - 1 - a]);
+    I = z ? I : fp_mul(I, v);
+  }
+  out[a] = fp_is_zero(vals[a]) ? fp_zero() : I;
+}
+
 // decode of every item (96 B at sigs + stride*i + offset); items whose key did not decode are PK_DECODE
 DG_KERNEL void __launch_bounds__(128) k_dec_p1(uint32_t n, const uint8_t* sigs, uint32_t stride, uint32_t offset,
                                                const uint32_t* item_slot, const uint8_t* key_status, DecState* ds,
@@ -494,6 +534,7 @@ DG_KERNEL void __launch_bounds__(128) k_binv_up(uint32_t n, const Fp* vals, Fp* 
 DG_KERNEL void __launch_bounds__(128) k_binv_down(uint32_t n, const Fp* vals, const Fp* pre, const Fp* inv, Fp* out);
 DG_KERNEL void __launch_bounds__(64) k_binv_root(uint32_t n, const Fp* vals, Fp* out);
 DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_up(uint32_t n, const Fp* vals, Fp* pre, Fp* roots);
+DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_root(uint32_t n, const Fp* vals, Fp* out);
 DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_down(uint32_t n, const Fp* vals, const Fp* pre, const Fp* rinv,
                                                          Fp* out);
 DG_KERNEL void __launch_bounds__(128) k_h2c_p2(uint32_t M, H2cMap* st, Fp* ein, const Fp* eout);
