@@ -204,7 +204,7 @@ DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_msm_chunks(uint32_t max_ch
 // Exceptional pairs are exact: P + (-P) = identity, P + P by the tangent (d = 2y; E' has no 2-torsion, h2 is
 // odd), identity operands pass the other one through; they take no inversion (denominator 1).
 constexpr uint32_t MSM_AFF_L = 3;  // affine levels: chunk sums of 2^3 = 8 entries
-DGI G2A aff_src0(const G2JStore& p) { return G2A{p.x, p.y, fp2_is_zero(p.z)}; }
+DGI G2A aff_src0(const G2JStore& p) { return G2A{p.x, p.y, fp_is_zero(p.z.c0)}; }  // Z is 0 or 1
 DGI G2A aff_srcA(const G2AStore& p) { return G2A{p.x, p.y, p.inf != 0}; }
 // group g of level l (groups of 2^(l+1) entries of one bucket) -> its first entry i and bucket end
 DGI bool aff_group(uint32_t nbk, const uint32_t* count, const uint32_t* offset, const uint32_t* gofs, uint32_t l,
@@ -277,17 +277,29 @@ DG_KERNEL void __launch_bounds__(128) k_msm_aff_den(uint32_t l, uint32_t maxg, u
   Fp n = fp_one();
   uint32_t i, end;
   if (g < gofs[side ? MSM_NBK : nbk] && aff_group(nbk, count, offset, gofs, l, g, i, end)) {
+    // read only what the norm needs: the identity flags and x (y only for equal x)
     const uint32_t j = i + (1u << l);
-    G2A p, q;
+    const Fp2 *px, *py, *qx, *qy;
+    bool pinf, qinf;
     if (l == 0) {
       const G2JStore* P = side ? PB : PA;
-      p = aff_src0(P[list[i]]);
-      q = aff_src0(P[list[j]]);
+      const G2JStore &a = P[list[i]], &b = P[list[j]];
+      pinf = fp_is_zero(a.z.c0);  // Z is 0 or 1 (msm_run's precondition)
+      qinf = fp_is_zero(b.z.c0);
+      px = &a.x, py = &a.y, qx = &b.x, qy = &b.y;
     } else {
-      p = aff_srcA(A[(size_t)side * E + i]);
-      q = aff_srcA(A[(size_t)side * E + j]);
+      const G2AStore &a = A[(size_t)side * E + i], &b = A[(size_t)side * E + j];
+      pinf = a.inf != 0;
+      qinf = b.inf != 0;
+      px = &a.x, py = &a.y, qx = &b.x, qy = &b.y;
     }
-    n = g2_aff_den(p, q, g2_aff_kind(p, q));
+    if (!pinf && !qinf) {
+      const Fp2 x1 = *px, x2 = *qx;
+      if (!fp2_eq(x1, x2))
+        n = fp2_norm(fp2_sub(x2, x1));
+      else if (fp2_eq(*py, *qy))
+        n = fp2_norm(fp2_dbl(*py));  // the same as g2_aff_den for kinds 1 and 2
+    }
   }
   den[t] = n;
 }
@@ -338,25 +350,32 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_aff_add(uint32_t l, ui
                                                                  const Fp* ninv);
 #endif
 
-#if defined(__HIP__) && DG_TU_LIB
 // the bucket sums from the affine chunk sums: lane (side, b, q < MSM_BSPLIT) adds chunks q, q + MSM_BSPLIT, ...
-// of bucket b (A[offset[b] + c 2^L]) with mixed additions; the partials are then row-summed as before
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_buckets_aff(uint32_t nsides, uint32_t nbk, const uint32_t* count,
-                                                                       const uint32_t* offset, const G2AStore* A,
-                                                                       uint32_t E, G2JStore* BP) {
+// of bucket b (A[offset[b] + c 2^L]) with mixed additions, the running sum in LDS (g2_madd_lds); the partials
+// are then row-summed as before
+#if defined(__HIP__) && DG_TU_HOT
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_msm_buckets_aff(uint32_t nsides, uint32_t nbk, const uint32_t* count,
+                                                                      const uint32_t* offset, const G2AStore* A,
+                                                                      uint32_t E, G2JStore* BP) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nbk * MSM_BSPLIT * nsides) return;
   uint32_t q = g % MSM_BSPLIT, sb = g / MSM_BSPLIT;
   uint32_t side = sb / nbk, b = sb % nbk;
   const uint32_t nch = side && b >= MSM_NBK ? 0u : (count[b] + (1u << MSM_AFF_L) - 1) >> MSM_AFF_L;
   const G2AStore* As = A + (size_t)side * E + offset[b];
-  G2J acc = jac_infinity<Fp2>();
+  __shared__ G2JStore s_acc[128];
+  G2JStore& acc = s_acc[threadIdx.x];
+  store_g2j(acc, jac_infinity<Fp2>());
   for (uint32_t c = q; c < nch; c += MSM_BSPLIT) {
-    const G2A a = load_g2a(As[c << MSM_AFF_L]);
-    if (!a.inf) acc = jac_add_aff(acc, a.x, a.y);
+    const G2AStore& a = As[c << MSM_AFF_L];
+    if (!a.inf) g2_madd_lds(acc, a.x, a.y);
   }
-  store_g2j(BP[g], acc);
+  BP[g] = acc;
 }
+#elif defined(__HIP__)
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_msm_buckets_aff(uint32_t nsides, uint32_t nbk, const uint32_t* count,
+                                                                      const uint32_t* offset, const G2AStore* A,
+                                                                      uint32_t E, G2JStore* BP);
 #endif
 
 #if defined(__HIP__) && DG_TU_LIB
