@@ -433,13 +433,14 @@ DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_down(uint32_t n, const Fp* v
 DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_root(uint32_t n, const Fp* vals, Fp* out) {
   __shared__ Fp T[2 * BINV_T];
   const uint32_t l = threadIdx.x, a = l * BINV_R;
-  const uint32_t b = a >= n ? a : (a + BINV_R < n ? a + BINV_R : n);
+  // running products with compile-time indices (registers; a runtime-indexed array would live in scratch)
   Fp pre[BINV_R];
   Fp acc = fp_one();
-  for (uint32_t i = a; i < b; ++i) {
-    const Fp v = vals[i];
+#pragma unroll
+  for (uint32_t c = 0; c < BINV_R; ++c) {
+    const Fp v = a + c < n ? vals[a + c] : fp_one();
     acc = fp_mul(acc, fp_is_zero(v) ? fp_one() : v);
-    pre[i - a] = acc;
+    pre[c] = acc;
   }
   T[BINV_T + l] = acc;
   binv_tree_up(T, l);
@@ -455,15 +456,19 @@ DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_root(uint32_t n, const Fp* v
     }
   }
   __syncthreads();
-  if (b == a) return;
   Fp I = T[BINV_T + l];
-  for (uint32_t i = b - 1; i > a; --i) {
-    const Fp v = vals[i];
+#pragma unroll
+  for (int c = BINV_R - 1; c >= 0; --c) {
+    if (a + c >= n) continue;
+    const Fp v = vals[a + c];
     const bool z = fp_is_zero(v);
-    out[i] = z ? fp_zero() : fp_mul(I, pre[i - 1 - a]);
-    I = z ? I : fp_mul(I, v);
+    if (c > 0) {
+      out[a + c] = z ? fp_zero() : fp_mul(I, pre[c - 1]);
+      I = z ? I : fp_mul(I, v);
+    } else {
+      out[a] = z ? fp_zero() : I;
+    }
   }
-  out[a] = fp_is_zero(vals[a]) ? fp_zero() : I;
 }
 
 // decode of every item (96 B at sigs + stride*i + offset); items whose key did not decode are PK_DECODE
