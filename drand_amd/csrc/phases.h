@@ -245,6 +245,9 @@ DGI bool dec_p3(const DecState& ds, const Fp& c, const Fp& t, bool subgroup, G2A
 }
 
 #if defined(__HIP__)
+#ifndef DG_PHASE_WAVES
+#define DG_PHASE_WAVES 2  // min waves per SIMD of p1a, p3, dec_p3 (1 wave: above 256 VGPRs; 2: p3 554 -> 422 us)
+#endif
 #ifndef DG_EXP_WAVES
 #define DG_EXP_WAVES 2
 #endif
@@ -255,7 +258,7 @@ DG_KERNEL void __launch_bounds__(128, DG_EXP_WAVES) k_exp_pm3d4(uint32_t n, cons
   out[i] = fp_pow_pm3d4_sos(in[i]);
 }
 
-DG_KERNEL void __launch_bounds__(128) k_h2c_p1a(uint32_t R, const uint8_t* msgs, uint32_t msg_len, const uint8_t* dst,
+DG_KERNEL void __launch_bounds__(128, DG_PHASE_WAVES) k_h2c_p1a(uint32_t R, const uint8_t* msgs, uint32_t msg_len, const uint8_t* dst,
                                                 uint32_t dst_len, const XmdTail* xmd, H2cMap* st, Fp* nD) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
@@ -292,7 +295,7 @@ DG_KERNEL void __launch_bounds__(128) k_h2c_p2(uint32_t M, H2cMap* st, Fp* ein, 
   st[m].g = s.g;
   ein[m] = c;
 }
-DG_KERNEL void __launch_bounds__(128) k_h2c_p3(uint32_t M, const H2cMap* st, const Fp* ein, const Fp* eout,
+DG_KERNEL void __launch_bounds__(128, DG_PHASE_WAVES) k_h2c_p3(uint32_t M, const H2cMap* st, const Fp* ein, const Fp* eout,
                                                G2JStore* iso) {
   uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
@@ -506,7 +509,7 @@ DG_KERNEL void __launch_bounds__(128) k_dec_p2(uint32_t n, DecState* ds, Fp* ein
 // the sigma of item i into S, with the G2 subgroup check unless the batch checks subgroup membership on the
 // MSM window sums (`subgroup` == 0, msm.h); claim the item's (round, slot) cell -- a taken cell, or a key
 // outside the batch equation, sends the item to the individual check (`isolate`)
-DG_KERNEL void __launch_bounds__(128) k_dec_p3(uint32_t n, uint32_t k, uint32_t nslots, const uint32_t* item_slot,
+DG_KERNEL void __launch_bounds__(128, DG_PHASE_WAVES) k_dec_p3(uint32_t n, uint32_t k, uint32_t nslots, const uint32_t* item_slot,
                                                const DecState* ds, const Fp* ein, const Fp* eout, G2AStore* S,
                                                uint8_t* status, uint32_t* cell, uint8_t* isolate,
                                                uint32_t subgroup) {
@@ -532,7 +535,7 @@ DG_KERNEL void __launch_bounds__(128) k_dec_p3(uint32_t n, uint32_t k, uint32_t 
 }
 #else
 DG_KERNEL void __launch_bounds__(128, DG_EXP_WAVES) k_exp_pm3d4(uint32_t n, const Fp* in, Fp* out);
-DG_KERNEL void __launch_bounds__(128) k_h2c_p1a(uint32_t R, const uint8_t* msgs, uint32_t msg_len, const uint8_t* dst,
+DG_KERNEL void __launch_bounds__(128, DG_PHASE_WAVES) k_h2c_p1a(uint32_t R, const uint8_t* msgs, uint32_t msg_len, const uint8_t* dst,
                                                 uint32_t dst_len, const XmdTail* xmd, H2cMap* st, Fp* nD);
 DG_KERNEL void __launch_bounds__(128) k_h2c_p1b(uint32_t R, H2cMap* st, const Fp* inv_nD, Fp* ein);
 DG_KERNEL void __launch_bounds__(128) k_binv_up(uint32_t n, const Fp* vals, Fp* pre, Fp* up);
@@ -543,7 +546,7 @@ DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_root(uint32_t n, const Fp* v
 DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_down(uint32_t n, const Fp* vals, const Fp* pre, const Fp* rinv,
                                                          Fp* out);
 DG_KERNEL void __launch_bounds__(128) k_h2c_p2(uint32_t M, H2cMap* st, Fp* ein, const Fp* eout);
-DG_KERNEL void __launch_bounds__(128) k_h2c_p3(uint32_t M, const H2cMap* st, const Fp* ein, const Fp* eout,
+DG_KERNEL void __launch_bounds__(128, DG_PHASE_WAVES) k_h2c_p3(uint32_t M, const H2cMap* st, const Fp* ein, const Fp* eout,
                                                G2JStore* iso);
 DG_KERNEL void __launch_bounds__(128) k_h2c_p4a(uint32_t R, const G2JStore* iso, G2JStore* outQ, Fp* nZ);
 DG_KERNEL void __launch_bounds__(128) k_h2c_p4b(uint32_t R, G2JStore* Q, const Fp* inv_nZ);
@@ -551,7 +554,7 @@ DG_KERNEL void __launch_bounds__(128) k_dec_p1(uint32_t n, const uint8_t* sigs, 
                                                const uint32_t* item_slot, const uint8_t* key_status, DecState* ds,
                                                Fp* ein, uint8_t* status);
 DG_KERNEL void __launch_bounds__(128) k_dec_p2(uint32_t n, DecState* ds, Fp* ein, const Fp* eout, uint8_t* status);
-DG_KERNEL void __launch_bounds__(128) k_dec_p3(uint32_t n, uint32_t k, uint32_t nslots, const uint32_t* item_slot,
+DG_KERNEL void __launch_bounds__(128, DG_PHASE_WAVES) k_dec_p3(uint32_t n, uint32_t k, uint32_t nslots, const uint32_t* item_slot,
                                                const DecState* ds, const Fp* ein, const Fp* eout, G2AStore* S,
                                                uint8_t* status, uint32_t* cell, uint8_t* isolate,
                                                uint32_t subgroup);
