@@ -197,6 +197,40 @@ DGI void g2_madd_lds(S& a, const Fp2& qx, const Fp2& qy) {
   a.y = fp2_sub(DG_MADD_MUL(r, fp2_sub(V, X3)), YJ2);
 }
 
+// The full addition (add-2007-bl) with the accumulator in LDS, products as g2_madd_lds; q any Jacobian point.
+// Identical results to jac_add (exceptional cases out of line).
+template <class S>
+DGI void g2_add_lds(S& a, const G2J& q) {
+  if (jac_is_inf(q)) return;
+  if (fp2_is_zero(a.z)) {
+    a.x = q.x;
+    a.y = q.y;
+    a.z = q.z;
+    return;
+  }
+  const Fp2 Z1Z1 = DG_MADD_SQR(a.z);
+  const Fp2 Z2Z2 = DG_MADD_SQR(q.z);
+  const Fp2 U1 = DG_MADD_MUL(a.x, Z2Z2);
+  const Fp2 S1 = DG_MADD_MUL(DG_MADD_MUL(a.y, q.z), Z2Z2);
+  const Fp2 H = fp2_sub(DG_MADD_MUL(q.x, Z1Z1), U1);
+  const Fp2 r = fp2_dbl(fp2_sub(DG_MADD_MUL(DG_MADD_MUL(q.y, a.z), Z1Z1), S1));
+  if (fp2_is_zero(H)) {
+    const G2J t = g2_add_rare(G2J{a.x, a.y, a.z}, q);
+    a.x = t.x;
+    a.y = t.y;
+    a.z = t.z;
+    return;
+  }
+  a.z = DG_MADD_MUL(fp2_sub(fp2_sub(DG_MADD_SQR(fp2_add(a.z, q.z)), Z1Z1), Z2Z2), H);
+  const Fp2 I = DG_MADD_SQR(fp2_dbl(H));
+  const Fp2 J = DG_MADD_MUL(H, I);
+  const Fp2 V = DG_MADD_MUL(U1, I);
+  const Fp2 SJ2 = fp2_dbl(DG_MADD_MUL(S1, J));
+  const Fp2 X3 = fp2_sub(fp2_sub(DG_MADD_SQR(r), J), fp2_dbl(V));
+  a.x = X3;
+  a.y = fp2_sub(DG_MADD_MUL(r, fp2_sub(V, X3)), SJ2);
+}
+
 // Affine pair additions with an externally supplied inverse (the affine levels of the MSM, msm.h; Montgomery's
 // trick over the batch supplies 1 / N(d)).  kind: 0 pass-through (an identity operand), 1 chord (x1 != x2),
 // 2 tangent (P + P), 3 identity result (P + (-P)).  E' has no 2-torsion (h2 is odd), so a tangent has y != 0.

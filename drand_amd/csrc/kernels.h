@@ -16,6 +16,9 @@
 #ifndef DG_BULK_WAVES
 #define DG_BULK_WAVES 1  // min waves per SIMD for the other per-lane group-arithmetic kernels
 #endif
+#ifndef DG_VERIFY_WAVES
+#define DG_VERIFY_WAVES 1  // min waves per SIMD of the per-item pairing checks (k_verify_items / k_verify_groups)
+#endif
 #ifndef DG_COOP_WAVES
 #define DG_COOP_WAVES 1  // min waves per SIMD for the cooperative (latency-bound) kernels
 #endif
@@ -592,7 +595,7 @@ DGN void verify_group(const uint32_t* mem, uint32_t n, uint32_t k, uint64_t seed
   }
 }
 // every decoded item after a failed batch (flag[0] == 0), only the isolated ones after a passed batch
-DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
+DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
                                                     const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
                                                     const uint8_t* isolate, uint8_t* status, uint32_t subgroup) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -603,7 +606,7 @@ DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, cons
 }
 
 // lane g < glist[0]: group g (one member: the item's own check)
-DG_KERNEL void __launch_bounds__(64) k_verify_groups(uint32_t k, const uint32_t* glist, const uint64_t* seedp,
+DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_groups(uint32_t k, const uint32_t* glist, const uint64_t* seedp,
                                                     const G1AStore* keys, const uint32_t* item_slot,
                                                     const G2AStore* H, const G2AStore* S, uint8_t* status,
                                                     uint8_t* fin, uint32_t subgroup, unsigned long long* cnt) {
@@ -617,10 +620,10 @@ DG_KERNEL void __launch_bounds__(64) k_verify_groups(uint32_t k, const uint32_t*
 }
 #elif DG_TU_LIB
 // (defined in kernels_verify.hip)
-DG_KERNEL void __launch_bounds__(64) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
+DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
                                                     const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
                                                     const uint8_t* isolate, uint8_t* status, uint32_t subgroup);
-DG_KERNEL void __launch_bounds__(64) k_verify_groups(uint32_t k, const uint32_t* glist, const uint64_t* seedp,
+DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_groups(uint32_t k, const uint32_t* glist, const uint64_t* seedp,
                                                     const G1AStore* keys, const uint32_t* item_slot,
                                                     const G2AStore* H, const G2AStore* S, uint8_t* status,
                                                     uint8_t* fin, uint32_t subgroup, unsigned long long* cnt);

@@ -612,23 +612,26 @@ DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_chunks(uint32_t max_c
   store_g2j(out[c], acc);
 #endif
 }
+// lane = bucket key: sum of its chunks (identity when empty), the running sum in LDS (g2_add_lds)
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_buckets(uint32_t nkeys, const uint32_t* chunk_off,
+                                                                   const G2JStore* chunks, G2JStore* B) {
+  uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nkeys) return;
+  __shared__ G2JStore s_acc[128];
+  G2JStore& acc = s_acc[threadIdx.x];
+  store_g2j(acc, jac_infinity<Fp2>());
+  for (uint32_t c = chunk_off[b]; c < chunk_off[b + 1]; ++c) g2_add_lds(acc, load_g2j(chunks[c]));
+  B[b] = acc;
+}
 #elif defined(__HIP__)
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_buckets(uint32_t nkeys, const uint32_t* chunk_off,
+                                                                   const G2JStore* chunks, G2JStore* B);
 DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_chunks(uint32_t max_chunks, uint32_t nkeys,
                                                                    const uint32_t* count, const uint32_t* offset,
                                                                    const uint32_t* chunk_off, const uint32_t* list,
                                                                    const G2AStore* S, G2JStore* out);
 #endif
 #if defined(__HIP__) && DG_TU_LIB
-
-// lane = bucket key: sum of its chunks (identity when empty)
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_buckets(uint32_t nkeys, const uint32_t* chunk_off,
-                                                                    const G2JStore* chunks, G2JStore* B) {
-  uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nkeys) return;
-  G2J acc = jac_infinity<Fp2>();
-  for (uint32_t c = chunk_off[b]; c < chunk_off[b + 1]; ++c) acc = jac_add(acc, load_g2j(chunks[c]));
-  store_g2j(B[b], acc);
-}
 
 // lane (set, w, k, c < 16): 8 of the buckets of (set, w) whose digit has bit k set; rows (set, w, k)
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_slices(uint32_t nsets, uint32_t nwin, const G2JStore* B,
