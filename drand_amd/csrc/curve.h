@@ -197,6 +197,20 @@ DGI void g2_madd_lds(S& a, const Fp2& qx, const Fp2& qy) {
   a.y = fp2_sub(DG_MADD_MUL(r, fp2_sub(V, X3)), YJ2);
 }
 
+// dbl-2009-l with the accumulator in LDS, products as g2_madd_lds (the identity stays the identity)
+template <class S>
+DGI void g2_dbl_lds(S& a) {
+  const Fp2 A = DG_MADD_SQR(a.x);
+  const Fp2 B = DG_MADD_SQR(a.y);
+  const Fp2 C = DG_MADD_SQR(B);
+  const Fp2 D = fp2_dbl(fp2_sub(fp2_sub(DG_MADD_SQR(fp2_add(a.x, B)), A), C));
+  const Fp2 E = fp2_add(fp2_dbl(A), A);
+  a.z = fp2_dbl(DG_MADD_MUL(a.y, a.z));
+  const Fp2 X3 = fp2_sub(DG_MADD_SQR(E), fp2_dbl(D));
+  a.x = X3;
+  a.y = fp2_sub(DG_MADD_MUL(E, fp2_sub(D, X3)), fp2_dbl(fp2_dbl(fp2_dbl(C))));
+}
+
 // The full addition (add-2007-bl) with the accumulator in LDS, products as g2_madd_lds; q any Jacobian point.
 // Identical results to jac_add (exceptional cases out of line).
 template <class S>
@@ -390,6 +404,48 @@ DGH G2J g2_mul_u256_psi(const G2A& p, const uint32_t* k) {
     }
   }
   return acc;
+}
+// The same product with the accumulator in LDS (`acc`: one G2JStore slot per lane at the call site,
+// k_recover_terms): doublings and mixed additions as g2_dbl_lds / g2_madd_lds, so the register file holds P,
+// psi(P) and one formula's temporaries (the in-register form spills ~740 VGPRs).  Same result.
+template <class SJ>
+DGI void g2_mul_u256_psi_lds(const G2A& p, const uint32_t* k, SJ& acc) {
+  acc.z = fp2_zero();
+  if (p.inf) return;
+  uint32_t q[8];
+  for (int w = 0; w < 8; ++w) q[w] = k[w];
+  uint64_t d[4];
+  d[0] = u256_divmod_u64(q, Z_ABS);
+  d[1] = u256_divmod_u64(q, Z_ABS);
+  d[2] = u256_divmod_u64(q, Z_ABS);
+  d[3] = (uint64_t)q[1] << 32 | q[0];
+  const Fp2 x0 = p.x, y0 = p.y;
+  Fp2 x1 = p.x, y1 = p.y;
+  g2_psi_aff(x1, y1);
+  auto add_i = [&](int i, bool neg) {
+    const Fp2 x = i == 0 ? x0 : i == 1 ? x1 : fp2_mul_fp(i == 2 ? x0 : x1, fp_const(PSI2_W));
+    const Fp2 y = i == 0 ? y0 : i == 1 ? fp2_neg(y1) : i == 2 ? fp2_neg(y0) : y1;
+    g2_madd_lds(acc, x, neg ? fp2_neg(y) : y);
+  };
+  uint64_t pos[4], neg[4];
+  uint32_t pos64 = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t hl = d[i] + (d[i] << 1), hh = (d[i] >> 63) + (hl < d[i] ? 1u : 0u);
+    pos[i] = ((hl & ~d[i]) >> 1) | (hh << 63);
+    neg[i] = (~hl & d[i]) >> 1;
+    pos64 |= (uint32_t)(hh >> 1) << i;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if ((pos64 >> i) & 1) add_i(i, false);
+  for (int b = 63; b >= 0; --b) {
+    g2_dbl_lds(acc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if ((pos[i] >> b) & 1) add_i(i, false);
+      if ((neg[i] >> b) & 1) add_i(i, true);
+    }
+  }
 }
 // The same product with no branch on the scalar: every bit does the doubling and one mixed addition per
 // digit, kept or dropped by a select.  Where the lanes of a wave hold different scalars (Recover rounds with

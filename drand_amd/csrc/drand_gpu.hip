@@ -857,6 +857,8 @@ int recover_tail(uint32_t R, uint32_t k, uint32_t t, const uint8_t* d_p, const u
   RET(launch("k_recover_select", k_recover_select, R, 128, st, R, k, t, d_p, d_st, d_sel, d_selidx, d_rst, d_sst));
   RET(wsT(S_TERMS, (size_t)R * t, &terms));
   RET(wsT(S_TMP, (size_t)R * t, &tmp));
+  RET(launch("k_recover_terms_u", k_recover_terms_u, R * t, 64, st, R, k, t, (const uint32_t*)d_sel,
+             (const uint32_t*)d_selidx, (const uint8_t*)d_rst, d_S, terms));
   RET(launch("k_recover_terms", k_recover_terms, R * t, 64, st, R, k, t, (const uint32_t*)d_sel,
              (const uint32_t*)d_selidx, (const uint8_t*)d_rst, d_S, terms));
   RET(reduce_rows(terms, tmp, R, t, st));

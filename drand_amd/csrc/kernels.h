@@ -866,34 +866,59 @@ DG_KERNEL void __launch_bounds__(128) k_decode_verified(uint32_t n, const uint8_
 // thread (m, r), rounds fastest: terms[r * t + m] = lambda_m * S_{r, sel[m]} (lambda over the round's t
 // selected indices).  A wave covers 64 rounds of the same position m, so while the rounds select the same
 // index set (every round with no bad share among its first t) its lanes share lambda_m and the scalar
-// multiplication's digit-dependent branches are uniform across the wave.
+// multiplication's digit-dependent branches are uniform across the wave.  Two kernels split the waves:
+// k_recover_terms_u takes the uniform ones (branching Straus, running point in LDS), k_recover_terms the
+// others (sign-aligned column form: 65 doublings + 65 additions whatever the digits, no divergence); each
+// returns at once on the other's waves, so each keeps its own (smaller) private segment.
 // hot translation unit (kernels_hot.hip: flat, 2 waves/SIMD; measured -27% / -36%)
 #if DG_TU_HOT
-DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
-                                                     const uint32_t* selidx, const uint8_t* round_status,
-                                                     const G2AStore* S, G2JStore* terms) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+// the wave's rounds (those with status OK) selected the same index set
+DGI bool recover_wave_uniform(uint32_t R, uint32_t t, const uint32_t* selidx, const uint8_t* round_status, uint32_t r) {
+  const bool ok = r < R && round_status[r] == DG_ST_OK_;
+  const uint64_t okm = __ballot(ok);
+  if (okm == 0) return true;
+  const int ref = __ffsll((unsigned long long)okm) - 1;
+  bool same = true;
+  for (uint32_t j = 0; j < t; ++j) {
+    const uint32_t v = ok ? selidx[(size_t)r * t + j] : 0u;
+    same = same && (!ok || v == (uint32_t)__shfl((int)v, ref));
+  }
+  return __all(same);
+}
+DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms_u(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
+                                                       const uint32_t* selidx, const uint8_t* round_status,
+                                                       const G2AStore* S, G2JStore* terms) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, m = g / R, r = g % R;
+  if (!recover_wave_uniform(R, t, selidx, round_status, g < R * t ? r : R)) return;
   if (g >= R * t) return;
-  uint32_t m = g / R, r = g % R;
-  size_t o = (size_t)r * t + m;
+  const size_t o = (size_t)r * t + m;
   if (round_status[r] != DG_ST_OK_) {
     store_g2j(terms[o], jac_infinity<Fp2>());
     return;
   }
-  Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, m);
-  // one scalar for the whole wave (its rounds selected the same index set): the branching Straus is uniform;
-  // otherwise the sign-aligned column form (65 doublings + 65 additions whatever the digits, no divergence)
-  bool same = true;
-#pragma unroll
-  for (int w = 0; w < 8; ++w) same = same && lam.l[w] == __builtin_amdgcn_readfirstlane(lam.l[w]);
-  const G2A s = load_g2a(S[(size_t)r * k + sel[o]]);
-  #if DG_TERMS_SEL
-  store_g2j(terms[o], __all(same) ? g2_mul_u256_psi(s, lam.l) : g2_mul_u256_psi_sel(s, lam.l));
-#else
-  store_g2j(terms[o], __all(same) ? g2_mul_u256_psi(s, lam.l) : g2_mul_u256_psi_sac(s, lam.l));
-#endif
+  const Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, m);
+  __shared__ G2JStore s_acc[64];
+  g2_mul_u256_psi_lds(load_g2a(S[(size_t)r * k + sel[o]]), lam.l, s_acc[threadIdx.x]);
+  terms[o] = s_acc[threadIdx.x];
+}
+DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
+                                                     const uint32_t* selidx, const uint8_t* round_status,
+                                                     const G2AStore* S, G2JStore* terms) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, m = g / R, r = g % R;
+  if (recover_wave_uniform(R, t, selidx, round_status, g < R * t ? r : R)) return;
+  if (g >= R * t) return;
+  const size_t o = (size_t)r * t + m;
+  if (round_status[r] != DG_ST_OK_) {
+    store_g2j(terms[o], jac_infinity<Fp2>());
+    return;
+  }
+  const Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, m);
+  store_g2j(terms[o], g2_mul_u256_psi_sac(load_g2a(S[(size_t)r * k + sel[o]]), lam.l));
 }
 #else
+DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms_u(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
+                                                       const uint32_t* selidx, const uint8_t* round_status,
+                                                       const G2AStore* S, G2JStore* terms);
 DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
                                                      const uint32_t* selidx, const uint8_t* round_status,
                                                      const G2AStore* S, G2JStore* terms);

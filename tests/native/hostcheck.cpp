@@ -214,3 +214,13 @@ extern "C" int hc_aff_add_check(const uint8_t* sig_a, const uint8_t* sig_b, int 
   if (r.inf != jac_is_inf(want)) return 0;
   return jac_eq(jac_from_aff(r), want) ? 1 : 0;
 }
+
+// [k]P with the accumulator as a memory slot (curve.h g2_mul_u256_psi_lds, LDS on the device) against the
+// register form; 1 if equal
+extern "C" int hc_g2_mul_lds_check(const uint8_t* sig96, const uint32_t* k8) {
+  G2A a;
+  if (!g2_decompress(a, sig96, true)) return -1;
+  G2J acc;
+  g2_mul_u256_psi_lds(a, k8, acc);
+  return jac_eq(acc, g2_mul_u256_psi(a, k8)) ? 1 : 0;
+}

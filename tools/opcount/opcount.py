@@ -85,6 +85,7 @@ def main():
         out["per_unit"][k] = {"mul": m / n, "sqr": s / n, "inv": v / n, "M": (m + s) / n,
                               "macs": (m * MAC_MUL + s * MAC_SQR + v * MAC_INV) / n}
     out["per_unit"]["k_key_accum"] = out["per_unit"]["k_sum_rows"]
+    out["per_unit"]["k_recover_terms_u"] = out["per_unit"]["k_recover_terms"]  # the same Straus, LDS running point
     with open(os.path.join(ROOT, "profiles", "opcounts.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     for k, v in sorted(out["per_unit"].items()):
