@@ -447,60 +447,12 @@ DGI void g2_mul_u256_psi_lds(const G2A& p, const uint32_t* k, SJ& acc) {
     }
   }
 }
-// The same product with no branch on the scalar: every bit does the doubling and one mixed addition per
-// digit, kept or dropped by a select.  Where the lanes of a wave hold different scalars (Recover rounds with
-// different share sets: the C5 adversarial batches), the branching form above executes the union of every
-// lane's additions (~8 per bit); this one executes 4.  Same result as g2_mul_u256_psi.
-DGH G2J g2_mul_u256_psi_sel(const G2A& p, const uint32_t* k) {
-  if (p.inf) return jac_infinity<Fp2>();
-  uint32_t q[8];
-  for (int w = 0; w < 8; ++w) q[w] = k[w];
-  uint64_t d[4];
-  d[0] = u256_divmod_u64(q, Z_ABS);
-  d[1] = u256_divmod_u64(q, Z_ABS);
-  d[2] = u256_divmod_u64(q, Z_ABS);
-  d[3] = (uint64_t)q[1] << 32 | q[0];
-  Fp2 px[4], py[4];
-  px[0] = p.x;
-  py[0] = p.y;
-  for (int i = 1; i < 4; ++i) {
-    px[i] = px[i - 1];
-    py[i] = py[i - 1];
-    g2_psi_aff(px[i], py[i]);
-  }
-  py[1] = fp2_neg(py[1]);
-  py[3] = fp2_neg(py[3]);
-  uint64_t pos[4], neg[4];
-  uint32_t pos64 = 0;
-  for (int i = 0; i < 4; ++i) {
-    const uint64_t hl = d[i] + (d[i] << 1), hh = (d[i] >> 63) + (hl < d[i] ? 1u : 0u);
-    pos[i] = ((hl & ~d[i]) >> 1) | (hh << 63);
-    neg[i] = (~hl & d[i]) >> 1;
-    pos64 |= (uint32_t)(hh >> 1) << i;
-  }
-  G2J acc = jac_infinity<Fp2>();
-  for (int i = 0; i < 4; ++i) {
-    G2J t = g2_madd_lean(acc, px[i], py[i]);
-    const bool on = (pos64 >> i) & 1;
-    acc = G2J{fp2_sel(on, acc.x, t.x), fp2_sel(on, acc.y, t.y), fp2_sel(on, acc.z, t.z)};
-  }
-  for (int b = 63; b >= 0; --b) {
-    acc = jac_dbl(acc);
-    for (int i = 0; i < 4; ++i) {
-      const bool pb = (pos[i] >> b) & 1, nb = (neg[i] >> b) & 1;
-      G2J t = g2_madd_lean(acc, px[i], fp2_sel(nb, py[i], fp2_neg(py[i])));
-      const bool on = pb || nb;
-      acc = G2J{fp2_sel(on, acc.x, t.x), fp2_sel(on, acc.y, t.y), fp2_sel(on, acc.z, t.z)};
-    }
-  }
-  return acc;
-}
 // The same product, regular: the four psi digits in the sign-aligned column form of Faz-Hernandez, Longa and
 // Sanchez ("Efficient and secure algorithms for GLV-based scalar multiplication", GLV-SAC).  With d0 made odd
 // (d0 + 1, corrected by one final subtraction of P), d0 = 2^64 + sum_{j<64} s_j 2^j with s_j = +-1, and every
 // other digit d_i = sum_{j<=64} s_j u_ij 2^j with u_ij in {0, 1}: each column is s_j T[u_1j + 2 u_2j + 4 u_3j],
 // T[u] = P_0 + u_1 P_1 + u_2 P_2 + u_3 P_3 (8 affine points, one batch inversion).  65 doublings and 65 mixed
-// additions whatever the lanes' scalars, against 64 + 256 for the select form: the Recover terms of rounds with
+// additions whatever the lanes' scalars (a per-bit select of every digit's addition took 64 + 256): the Recover terms of rounds with
 // different share sets (divergent waves).  The table is indexed per lane, so it lives in scratch.  P_i are
 // multiples [|z|^i]P with 1 + |z| + |z|^2 + |z|^3 < r, so no table entry is the identity or +- another.
 DGH G2J g2_mul_u256_psi_sac(const G2A& p, const uint32_t* k) {

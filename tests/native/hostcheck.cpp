@@ -164,12 +164,6 @@ extern "C" int hc_dec_phases_check(const uint8_t* in96, int subgroup) {
   return a.inf == b.inf && (a.inf || (fp2_eq(a.x, b.x) && fp2_eq(a.y, b.y))) ? 1 : 0;
 }
 
-// [k]P by the select (branch-free) psi-Straus and the branching one: 1 if they agree
-extern "C" int hc_g2_mul_sel_check(const uint8_t* sig96, const uint32_t* k8) {
-  G2A a;
-  if (!g2_decompress(a, sig96, true)) return -1;
-  return jac_eq(g2_mul_u256_psi_sel(a, k8), g2_mul_u256_psi(a, k8)) ? 1 : 0;
-}
 // the same product by the sign-aligned column form (GLV-SAC): 1 if it agrees with the branching psi-Straus
 extern "C" int hc_g2_mul_sac_check(const uint8_t* sig96, const uint32_t* k8) {
   G2A a;

@@ -75,7 +75,6 @@ def test_g2_mul_psi_decomposition_host_build(hc):
     for k in ks:
         k8 = (ctypes.c_uint32 * 8)(*[(k >> (32 * w)) & 0xFFFFFFFF for w in range(8)])
         assert hc.hc_g2_mul_psi_check(sig, k8) == 1, hex(k)
-        assert hc.hc_g2_mul_sel_check(sig, k8) == 1, hex(k)  # the select form of divergent Recover waves
         assert hc.hc_g2_mul_sac_check(sig, k8) == 1, hex(k)  # the sign-aligned column form
         assert hc.hc_g2_mul_lds_check(sig, k8) == 1, hex(k)  # the LDS-accumulator form of uniform waves
 
