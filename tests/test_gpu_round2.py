@@ -335,3 +335,45 @@ def test_recover_dev_equals_host_and_twin():
     tw = twin.recover_batch(commits, t, n, np.array([list(m) for m in msgs], np.uint8), parts, 8)
     assert np.array_equal(b[1], tw[1]) and np.array_equal(b[2], tw[2])
     assert np.array_equal(b[0][b[1] == 0], tw[0][tw[1] == 0])
+
+
+_AB_CHILD = r"""
+import json, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from drand_amd import tbls
+from tests.fixtures import chain, chain_arrays, hx
+c = chain()
+_, _, _, sigs, msgs = chain_arrays(c)
+s = sigs[:48].copy()
+s[3] = s[4]                      # a valid signature of another round
+s[10, 40] ^= 1                   # a flipped bit
+s[20] = s[21]
+print(json.dumps(tbls.verify_recovered_batch(hx(c["pk"]), msgs[:48], s, seed=5).tolist()))
+"""
+
+
+def test_ab_switches_give_the_same_verdicts():
+    """The library's A/B switches (DG_MSM_JAC: Jacobian chunk sums instead of the affine MSM levels,
+    DG_BINV_CHUNKED: the chunk-of-32 batch inversion, DG_SUB_SEPARATE: the subgroup windows in their own
+    launch) select other kernels for the same computation: in a child process with all three set, the verdicts
+    of a corrupted batch equal the default library's and the CPU twin's."""
+    import json
+    import subprocess
+    import sys
+
+    c = chain()
+    _, _, _, sigs, msgs = chain_arrays(c)
+    pk = hx(c["pk"])
+    s = sigs[:48].copy()
+    s[3] = s[4]
+    s[10, 40] ^= 1
+    s[20] = s[21]
+    here = tbls.verify_recovered_batch(pk, msgs[:48], s, seed=5).tolist()
+    want = [twin.verify(pk, bytes(msgs[i]), bytes(s[i])) for i in range(48)]
+    assert here == want and sum(1 for v in want if v) == 3
+    env = dict(os.environ, DG_MSM_JAC="1", DG_BINV_CHUNKED="1", DG_SUB_SEPARATE="1")
+    r = subprocess.run([sys.executable, "-c", _AB_CHILD, ROOT], env=env, capture_output=True, text=True, timeout=240,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1]) == want
