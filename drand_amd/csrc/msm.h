@@ -203,7 +203,10 @@ DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_msm_chunks(uint32_t max_ch
 // MSM_AFF_L levels A[offset[b] + k 2^L] holds the k-th chunk sum of bucket b, which k_msm_buckets_aff reads.
 // Exceptional pairs are exact: P + (-P) = identity, P + P by the tangent (d = 2y; E' has no 2-torsion, h2 is
 // odd), identity operands pass the other one through; they take no inversion (denominator 1).
-constexpr uint32_t MSM_AFF_L = 3;  // affine levels: chunk sums of 2^3 = 8 entries
+#ifndef DG_MSM_AFF_L
+#define DG_MSM_AFF_L 3
+#endif
+constexpr uint32_t MSM_AFF_L = DG_MSM_AFF_L;  // affine levels: chunk sums of 2^3 = 8 entries (A/B: DG_MSM_AFF_L)
 DGI G2A aff_src0(const G2JStore& p) { return G2A{p.x, p.y, fp_is_zero(p.z.c0)}; }  // Z is 0 or 1
 DGI G2A aff_srcA(const G2AStore& p) { return G2A{p.x, p.y, p.inf != 0}; }
 // group g of level l (groups of 2^(l+1) entries of one bucket) -> its first entry i and bucket end
