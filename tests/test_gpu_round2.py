@@ -377,3 +377,21 @@ def test_ab_switches_give_the_same_verdicts():
                        cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     assert json.loads(r.stdout.strip().splitlines()[-1]) == want
+
+
+def test_repeated_items_pass_on_the_batch_path():
+    """A valid batch whose items repeat (one (message, signature) pair 200 times, then two pairs alternating):
+    every MSM bucket holds copies of one point, so the affine levels take the tangent case (P + P) throughout
+    and the hash side the same.  The batch equation must hold (no per-item fallback) and every verdict is OK;
+    the exact chord / tangent / P + (-P) formulas are also checked on the host
+    (test_host_arith.py::test_affine_pair_addition_matches_jacobian)."""
+    c = chain()
+    _, _, _, sigs, msgs = chain_arrays(c)
+    pk = hx(c["pk"])
+    for idx in ([0] * 200, [0, 1] * 100):
+        m = np.ascontiguousarray(msgs[idx])
+        s = np.ascontiguousarray(sigs[idx])
+        f0 = L.fallback_count()
+        st = tbls.verify_recovered_batch(pk, m, s, seed=9)
+        assert not st.any()
+        assert L.fallback_count() == f0, "a valid batch of repeated items fell back to the per-item pass"
