@@ -14,11 +14,14 @@ RCCL all-gather of the per-round verdict bitmaps.
 
 --gpus N without a torchrun environment starts the N ranks itself (torch.distributed.run as a child
 process, before anything touches the GPU) and exits with their status; a rank whose WORLD_SIZE differs
-from --gpus exits non-zero.  Rank 0 prints ONE JSON line (contract in the task statement).  Beside the
-headline it carries the Recover lines (configs[2] C3 and configs[4] C5, sharded the same way, their
-outputs all-gathered), the live-round latency lines, the syncFrom catch-up line, the
-CPU baselines (rank 0 at N = 1 only) and the roofline objects: algorithmic multiply-adds of the dominant
-kernel (profiles/opcounts.json) over its HIP-event launch time, against the measured v_mad_u64_u32 peak.
+from --gpus exits non-zero.  Rank 0 prints ONE JSON line (contract in the task statement), kept under
+~4 KB so the driver's record holds all of it.  Beside the headline it carries the Recover lines
+(configs[2] C3 and configs[4] C5, sharded the same way, their outputs all-gathered), the live-round
+latency lines, the syncFrom catch-up line, the CPU baselines (rank 0, at every N,
+after the GPU timed regions, on every host core this process may use) and the roofline objects:
+algorithmic multiply-adds of the dominant kernel (profiles/opcounts.json: 300 per Montgomery product,
+BASELINE.md) over its HIP-event launch time, against the v_mad_u64_u32 peak each rank measures on its own
+GPU (tools/microbench/probe.hip).  The per-kernel timing tables go to a side file (--tables-out).
 """
 import argparse
 import ctypes
@@ -43,14 +46,32 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def cpu_threads():
-    """Host threads for the CPU baselines: the CPUs this process may run on, capped by OMP_NUM_THREADS (the
-    GPU box sets it to this GPU's CPU share; nproc there counts the whole machine)."""
-    n = len(os.sched_getaffinity(0))
-    omp = os.environ.get("OMP_NUM_THREADS")
-    if omp and omp.isdigit() and int(omp) > 0:
-        n = min(n, int(omp))
-    return max(1, n)
+def host_cores():
+    """The host cores for the CPU baselines: every CPU this process may run on (its affinity mask, capped by
+    a cgroup CPU quota when one is set -- threads beyond the quota only time-slice), not OMP_NUM_THREADS.
+    Returns (threads used, CPUs of the machine, cgroup quota in CPUs or None)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    use = aff if quota is None else max(1, min(aff, int(quota)))
+    return use, os.cpu_count() or use, quota
+
+
+def cpu_label(cb, threads, machine, quota):
+    """The core-count fields of a cpu_baseline object: the threads used and the machine's CPU count, and a
+    linear estimate for all of the machine's CPUs when the process was held to fewer of them."""
+    cb["cores"] = threads
+    cb["host_cpus"] = machine
+    if quota is not None:
+        cb["cgroup_cpu_quota"] = quota
+    if machine > threads:
+        cb["all_host_cpus_linear_est"] = cb["value"] * machine / threads
+    return cb
 
 
 def traffic_of(kernel, config="head"):
@@ -108,16 +129,38 @@ def roofline_of(kt, kernel_units, peak, extra=None, config="head"):
     if isinstance(u, dict):  # a mix of unit kinds {opcounts key: units}: MACs per unit averaged over the mix
         total = sum(u.values())
         macs = sum(c * oc[k]["macs"] for k, c in u.items()) / max(total, 1)
+        vmad = sum(c * oc[k].get("vmad", 0) for k, c in u.items()) / max(total, 1)
         units = total / kt[name][1]
     else:
         macs = oc[name]["macs"]
+        vmad = oc[name].get("vmad", 0)
         units = u / kt[name][1]
     achieved = macs * units / (us * 1e-6) / 1e12
-    out = {"bound": "valu-int", "achieved": achieved, "peak": peak["tmac_s"], "unit": "TMAC/s",
-           "frac": achieved / peak["tmac_s"], "traffic": traffic_of(name, config), "kernel": name, "kernel_avg_us": us,
-           "units_per_launch": units, "macs_per_unit": macs, "peak_source": peak["source"]}
+    issued = vmad * units / (us * 1e-6) / 1e12
+    # a rank without a measured peak still reports what it achieved (frac null), never a TypeError
+    pk = peak.get("tmac_s") if peak else None
+    out = {"bound": "valu-int", "achieved": achieved, "peak": pk, "unit": "TMAC/s",
+           "frac": achieved / pk if pk else None, "traffic": traffic_of(name, config), "kernel": name,
+           "kernel_avg_us": us, "units_per_launch": units, "macs_per_unit": macs,
+           "vmad_per_unit": vmad, "issue_frac": issued / pk if pk else None,
+           "peak_source": peak.get("source") if peak else None}
     if extra:
         out.update(extra)
+    return out
+
+
+COMPACT_ROOF = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_avg_us", "units_per_launch",
+                "macs_per_unit", "issue_frac", "chip", "overlapped")
+
+
+def compact_roofline(r):
+    """The roofline fields the printed line keeps (the rest goes to the side file)."""
+    if not r:
+        return r
+    out = {k: r[k] for k in COMPACT_ROOF if k in r}
+    for k in ("chip", "overlapped"):
+        if isinstance(out.get(k), dict):
+            out[k] = {q: v for q, v in out[k].items() if q != "note"}
     return out
 
 
@@ -241,9 +284,12 @@ def timed_ranks(fn, world):
 
 def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps=2):
     """BASELINE configs[2]: VerifyPartial on every share + Lagrange Recover for an (n, t) group over
-    R_total rounds of the chain, each rank its contiguous range through dg_recover (host-buffer API: the 98 B
-    partials cross PCIe inside the timed region), then the RCCL all-gather of the recovered signatures, round
-    statuses and share statuses.  Every recovered signature must equal the chain's byte for byte."""
+    R_total rounds of the chain, each rank its contiguous range through dg_recover_dev with the messages and
+    98 B partials already resident in HBM (the headline `value`, like the verify headline), then the RCCL
+    all-gather of the recovered signatures, round statuses and share statuses.  `host_api_value` is the same
+    work through the host-buffer dg_recover (the partials cross PCIe inside the call); round-1 numbers were
+    host-buffer rates, so compare host_api_value with them.  Every recovered signature must equal the
+    chain's byte for byte."""
     a, b = shard.round_range(R_total, world, rank)
     R = b - a
     t0 = time.perf_counter()
@@ -289,9 +335,11 @@ def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps
 def adversarial_bench(L, tbls, shard, chain, R_total, world, rank, peak, t=129, n=256, frac=0.10, n_short=3):
     """BASELINE configs[4]: n = 256, t = 129, ~10% of the (round, share) cells corrupted with the six
     cycling modes of tools/corrupt.py, plus `n_short` rounds with more than n - t corrupted shares (-> "not
-    enough shares"); each rank its contiguous range of R_total rounds through dg_recover (the batch equation
-    fails, so the examined prefix of every round takes the exact per-item check), then the all-gather of the
-    outputs.  Checked without the CPU: recovered signatures equal the chain's, exactly the short rounds
+    enough shares"); each rank its contiguous range of R_total rounds through dg_recover_dev (inputs resident
+    in HBM; the batch equation fails, so the examined prefix of every round takes the per-item pass: group
+    tests of up to 4 shares -- a passed group's members are accepted with error probability <= 2^-64 -- and
+    single pairing checks for the members of failed groups; DG_GROUP=1 makes every check a single one), then
+    the all-gather of the outputs.  Checked without the CPU: recovered signatures equal the chain's, exactly the short rounds
     report NOT_ENOUGH, every examined corrupted share is rejected and every examined clean one accepted
     (per-share parity with the CPU twin is tests/test_gpu_parity.py's job)."""
     from tools import corrupt
@@ -449,6 +497,143 @@ def sync_bench(chain_sigs, R, batch=25000):
             "note": "host Beacon objects -> dg_check_links + dg_verify_beacons per batch (host-buffer API, blocking)"}
 
 
+def max_over_ranks(x, world):
+    """max of a float over the ranks (the device tensor of the rank's GPU; CPU under gloo)."""
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def measure_peak(shard, local, detail=False):
+    """The roofline denominator of this rank's GPU: v_mad_u64_u32 lane-MACs/s with distinct carry destinations
+    after 2 s of launches, and the clock the chip held (in-kernel s_memtime / s_memrealtime).  With `detail`
+    also the other forms (the VCC-shared round-2 probe, the compiler's form, v_mad_u32_u24, v_mul_lo_u32) for
+    the side file.  None (and a log line) if the probe library is missing: callers then report frac null."""
+    try:
+        pk = shard.mad_peak(local)
+    except (OSError, RuntimeError) as e:
+        log("peak probe unavailable:", e)
+        return None
+    if detail:
+        pk["forms"] = {}
+        for kind, name in ((0, "v_mad_u64_u32 vcc"), (2, "v_mad_u64_u32 compiler"), (3, "v_mad_u32_u24"),
+                           (4, "v_mul_lo_u32")):
+            try:
+                pk["forms"][name] = shard.probe_form(local, kind, warm_s=0.5)
+            except (OSError, RuntimeError) as e:
+                log("probe form", name, "failed:", e)
+    return pk
+
+
+def headline_roofline(kt, kt_iso, per, peak, G, steps, world, dt):
+    """Roofline of the headline's dominant kernel (isolated launches of two blocking batches of `per` rounds),
+    its overlapped timing, and the whole-chip MAC rate of the timed steps.  Any rank may call it; a rank
+    without a peak gets frac null."""
+    if not kt_iso:
+        return None
+    oc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["per_unit"]
+    # units over the two blocking batches: rounds for the fused kernels, exponentiations (4 per round of
+    # hash-to-G2, 2 per signature) for k_exp_pm3d4, map items / items for the phases
+    nb2 = 2 * per
+    units = {"k_h2c_uncleared": nb2, "k_decode_items": nb2, "k_exp_pm3d4": 6 * nb2, "k_h2c_p2": 2 * nb2,
+             "k_h2c_p3": 2 * nb2, "k_dec_p1": nb2, "k_dec_p2": nb2, "k_dec_p3": nb2}
+    roof = roofline_of(kt_iso, units, peak,
+                       {"timing": "HIP events on the launch stream, blocking batches right after the timed "
+                                  "region (the kernel alone on the chip)"})
+    if not roof:
+        return None
+    pk = peak.get("tmac_s") if peak else None
+    if roof["kernel"] in kt:
+        o_us = kt[roof["kernel"]][0]
+        a_o = roof["macs_per_unit"] * roof["units_per_launch"] / (o_us * 1e-6) / 1e12
+        roof["overlapped"] = {"kernel_avg_us": o_us, "achieved": a_o, "frac": a_o / pk if pk else None,
+                              "note": "instrumented replay of the timed region: the launch shares the chip "
+                                      "with the other batches in flight"}
+    # whole chip: algorithmic multiply-adds of the per-round work (hash, decode, 16 bucket additions of the two
+    # MSMs + 10 of the subgroup-check test windows, mixed: signatures and hashes are stored with Z = 1) over the
+    # step time; per-batch fixed work not counted
+    per_round = (sum(oc[k]["macs"] for k in ("k_h2c_uncleared", "k_decode_items")) +
+                 26 * oc["k_msm_chunks[mixed add]"]["macs"])
+    if "k_h2c_p1a" in kt_iso:  # the phase kernels (same algorithm, batch inversions)
+        per_round = (6 * oc["k_exp_pm3d4"]["macs"] + oc["k_h2c_p1a+p1b"]["macs"] + 2 * oc["k_h2c_p2"]["macs"] +
+                     2 * oc["k_h2c_p3"]["macs"] + oc["k_h2c_p4a+p4b"]["macs"] +
+                     sum(oc[k]["macs"] for k in ("k_dec_p1", "k_dec_p2", "k_dec_p3")) +
+                     26 * oc["k_msm_chunks[mixed add]"]["macs"])
+    chip = per_round * G * steps / world / dt / 1e12
+    roof["chip"] = {"macs_per_round": per_round, "achieved": chip, "frac": chip / pk if pk else None,
+                    "note": "per GPU"}
+    return roof
+
+
+# keys of a sub-line (recover, adversarial, ...) that go to the side file instead of the printed line
+SIDE_KEYS = ("kernel_avg_us", "kernel_avg_us_isolated", "kernel_time_share", "note", "sample", "partials_generated_s",
+             "setup_s", "checks_by_members", "timing")
+
+
+def report(rank, world, head, roof, cpu, lines, tables, tables_out):
+    """Rank-dependent end of the bench: every rank may pass partial data (a rank off 0 has no CPU baseline and
+    the sub-lines it did not run are None); rank 0 prints the one JSON line and writes the side file.  The
+    printed line keeps the headline, the compact roofline and cpu_baseline, and for each sub-line its value,
+    compact roofline and cpu_baseline; the per-kernel tables, notes and probe details go to `tables_out`."""
+    if rank != 0:
+        return None
+    side = dict(tables)
+    out = {"metric": METRIC, "value": head["value"], "unit": "rounds/s", "n_gpus": world, "steps": head["steps"],
+           "warmup": head["warmup"], "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+           "scaling": head["scaling"], "vs_baseline": None, "dtype": "u32 (381-bit Fp, 12x32-bit limbs)",
+           "data": head["data"], "config": head["config"], "roofline": compact_roofline(roof),
+           "cpu_baseline": cpu, "batch_fallbacks": head.get("batch_fallbacks")}
+    side["roofline"] = roof
+    for name, line in lines.items():
+        if line is None:
+            out[name] = None
+            continue
+        line = dict(line)
+        side[name] = {k: line.pop(k) for k in SIDE_KEYS if k in line}
+        if isinstance(line.get("roofline"), dict):
+            side[name]["roofline"] = line["roofline"]
+            line["roofline"] = compact_roofline(line["roofline"])
+        if isinstance(line.get("cpu_baseline"), dict):
+            side[name]["cpu_baseline"] = line["cpu_baseline"]
+            line["cpu_baseline"] = {k: v for k, v in line["cpu_baseline"].items() if k != "sample"}
+        out[name] = line
+    if isinstance(cpu, dict) and "sample" in cpu:
+        side["cpu_baseline"] = cpu
+    if peak_of(tables):
+        out["peak_clock_mhz"] = peak_of(tables).get("clock_mhz")
+    if tables_out:
+        try:
+            os.makedirs(os.path.dirname(tables_out), exist_ok=True)
+            with open(tables_out, "w") as f:
+                json.dump(side, f, indent=1, default=str)
+        except OSError as e:
+            log("side file not written:", e)
+    line = json.dumps(_round_floats(out))
+    print(line, flush=True)
+    return line
+
+
+def _round_floats(x, sig=5):
+    """floats to `sig` significant digits, recursively (the line's size, not its precision, is the limit)."""
+    if isinstance(x, float):
+        return float("%.*g" % (sig, x))
+    if isinstance(x, dict):
+        return {k: _round_floats(v, sig) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_round_floats(v, sig) for v in x]
+    return x
+
+
+def peak_of(tables):
+    return tables.get("peak") if isinstance(tables, dict) else None
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -469,6 +654,8 @@ def main():
     ap.add_argument("--sync", dest="use_sync", action="store_true",
                     help="blocking dg_verify_beacons_dev per batch (default: dg_verify_beacons_dev_async, so the "
                          "latency-bound tail of one batch overlaps the head of the next)")
+    ap.add_argument("--tables-out", default=os.path.join(ROOT, "gpurun_out", "bench_tables.json"),
+                    help="side file for the per-kernel timing tables and the peak probe details (rank 0)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no per-kernel HIP events after the timed region (no roofline)")
     ap.add_argument("--recover-rounds", type=int, default=100000, help="C3 rounds (all GPUs); 0 disables")
@@ -616,43 +803,11 @@ def main():
         kt_iso = L.timings()
         assert int(d_sts[0][lo:hi].max().item()) == 0
         L.check(lib.dg_set_timing(0))
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    peak = shard.mad_peak(local) if rank == 0 else None
-    roof = None
-    if rank == 0 and kt_iso:
-        oc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["per_unit"]
-        per = bounds[0][1] - bounds[0][0]
-        # units over the two blocking batches: rounds for the fused kernels, exponentiations (4 per round of
-        # hash-to-G2, 2 per signature) for k_exp_pm3d4, map items / items for the phases
-        nb2 = 2 * per
-        units = {"k_h2c_uncleared": nb2, "k_decode_items": nb2, "k_exp_pm3d4": 6 * nb2, "k_h2c_p2": 2 * nb2,
-                 "k_h2c_p3": 2 * nb2, "k_dec_p1": nb2, "k_dec_p2": nb2, "k_dec_p3": nb2}
-        roof = roofline_of(kt_iso, units, peak,
-                           {"timing": "HIP events on the launch stream, blocking batches right after the timed "
-                                      "region (the kernel alone on the chip)"})
-        if roof and roof["kernel"] in kt:
-            o_us = kt[roof["kernel"]][0]
-            a_o = roof["macs_per_unit"] * roof["units_per_launch"] / (o_us * 1e-6) / 1e12
-            roof["overlapped"] = {"kernel_avg_us": o_us, "achieved": a_o, "frac": a_o / peak["tmac_s"],
-                                  "note": "instrumented replay of the timed region: the launch shares the chip "
-                                          "with the other batches in flight"}
-        if roof:
-            # whole chip: algorithmic multiply-adds of the per-round work (hash, decode, 16 bucket additions of
-            # the two MSMs + 10 of the subgroup-check test windows, mixed: signatures and hashes are stored with
-            # Z = 1) over the step time; per-batch fixed work not counted
-            per_round = (sum(oc[k]["macs"] for k in ("k_h2c_uncleared", "k_decode_items")) +
-                         26 * oc["k_msm_chunks[mixed add]"]["macs"])
-            if "k_h2c_p1a" in kt_iso:  # the phase kernels (same algorithm, batch inversions)
-                per_round = (6 * oc["k_exp_pm3d4"]["macs"] + oc["k_h2c_p1a+p1b"]["macs"] + 2 * oc["k_h2c_p2"]["macs"] +
-                             2 * oc["k_h2c_p3"]["macs"] + oc["k_h2c_p4a+p4b"]["macs"] +
-                             sum(oc[k]["macs"] for k in ("k_dec_p1", "k_dec_p2", "k_dec_p3")) +
-                             26 * oc["k_msm_chunks[mixed add]"]["macs"])
-            chip = per_round * G * args.steps / world / dt / 1e12
-            roof["chip"] = {"macs_per_round": per_round, "achieved": chip, "frac": chip / peak["tmac_s"],
-                            "note": "per GPU"}
+    dt = max_over_ranks(dt, world)
+    # every rank measures the v_mad_u64_u32 peak of its own GPU: the Recover lines below price their kernels
+    # against it on every rank
+    peak = measure_peak(shard, local, detail=(rank == 0))
+    roof = headline_roofline(kt, kt_iso, bounds[0][1] - bounds[0][0], peak, G, args.steps, world, dt)
     share = {k: round(v[0] * v[1] / (dt * 1e6), 4) for k, v in kt.items()}
     del d_sts, d_sig, d_ps
     torch.cuda.empty_cache()
@@ -672,38 +827,38 @@ def main():
             c1 = c1_gpu(L, tbls)
             if rec_in is not None:
                 lat = live_latency(L, tbls, rec_in[0], rec_in[1], rec_in[2], 33, 64)
+    # CPU baselines: rank 0 at every N, after every GPU timed region, on all the host cores it may use
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        th = cpu_threads()
+    if rank == 0 and not args.no_cpu_baseline:
+        th, machine, quota = host_cores()
         ns = min(n, 40000)
         m = tbls.beacon_messages(rounds[:ns] - 1, rounds[:ns], prev_sigs[:ns])
-        cpu = cpu_verify(pk, m, np.ascontiguousarray(sigs[:ns]), th)
+        cpu = cpu_label(cpu_verify(pk, m, np.ascontiguousarray(sigs[:ns]), th), th, machine, quota)
         if c1 is not None:
-            c1["cpu_baseline"] = cpu_c1(th)
+            c1["cpu_baseline"] = cpu_label(cpu_c1(th), th, machine, quota)
         if rec_in is not None:
-            rec["cpu_baseline"], _ = cpu_recover(rec_in[0], 33, 64, rec_in[1], rec_in[2], th, label="C3 n=64 t=33")
+            cb, _ = cpu_recover(rec_in[0], 33, 64, rec_in[1], rec_in[2], th, label="C3 n=64 t=33")
+            rec["cpu_baseline"] = cpu_label(cb, th, machine, quota)
         if adv_in is not None:
             cb, (trs, tss, Rs) = cpu_recover(adv_in[0], 129, 256, adv_in[1], adv_in[2], th, seconds=6.0,
                                              label="C5 n=256 t=129 corrupted")
             # the GPU's statuses on the same rounds are the twin's (bit-exact sample check)
             cb["statuses_match_gpu"] = bool(np.array_equal(tss, adv_in[3][:Rs]) and np.array_equal(trs, adv_in[4][:Rs]))
-            adv["cpu_baseline"] = cb
-    if rank == 0:
-        out = {"metric": METRIC, "value": G * args.steps / dt, "unit": "rounds/s", "n_gpus": world,
-               "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
-               "higher_is_better": True, "scaling": "strong" if (world > 1 or args.global_rounds) else "weak",
-               "vs_baseline": None, "dtype": "u32 (381-bit Fp, 12x32-bit limbs)", "data": data,
-               "config": {"workload": ("batch bls.Verify / beacon.VerifyBeacon of the %d-round linked chain per "
-                                       "step, %d contiguous range(s) of <= %d rounds per GPU in batches of <= %d, "
-                                       "one shared group key (BASELINE configs[%d])"
-                                       % (G, world, -(-G // world), args.batch, 1 if G <= 100000 else 3)),
-                          "global_rounds": G, "rounds_per_gpu": n, "batches_per_gpu": nb,
-                          "parallelism": "rounds sharded dp%d" % world},
-               "roofline": roof, "cpu_baseline": cpu, "recover": rec, "adversarial": adv, "c1": c1,
-               "live_latency": lat, "sync": syn, "batch_fallbacks": fallbacks, "kernel_time_share": share,
-               "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
-               "kernel_avg_us_isolated": {k: round(v[0], 1) for k, v in kt_iso.items()}}
-        print(json.dumps(out), flush=True)
+            adv["cpu_baseline"] = cpu_label(cb, th, machine, quota)
+    head = {"value": G * args.steps / dt, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "scaling": "strong" if (world > 1 or args.global_rounds) else "weak", "data": data,
+            "config": {"workload": ("batch bls.Verify / beacon.VerifyBeacon of the %d-round linked chain per "
+                                    "step, %d contiguous range(s) of <= %d rounds per GPU in batches of <= %d, "
+                                    "one shared group key (BASELINE configs[%d])"
+                                    % (G, world, -(-G // world), args.batch, 1 if G <= 100000 else 3)),
+                       "global_rounds": G, "rounds_per_gpu": n, "batches_per_gpu": nb,
+                       "parallelism": "rounds sharded dp%d" % world},
+            "batch_fallbacks": fallbacks}
+    tables = {"kernel_time_share": share, "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
+              "kernel_avg_us_isolated": {k: round(v[0], 1) for k, v in kt_iso.items()}, "peak": peak}
+    report(rank, world, head, roof, cpu, {"recover": rec, "adversarial": adv, "c1": c1, "live_latency": lat,
+                                          "sync": syn}, tables, args.tables_out)
     if world > 1:
         dist.destroy_process_group()
 

@@ -52,6 +52,7 @@ SIGNATURES = {
     "dg_last_batch_flags": ([_P], _I),
     "dg_fallback_count": ([_P], _I),
     "dg_group_counts": ([_P], _I),
+    "dg_set_group_size": ([_U32], _I),
     "dg_recover_dev": ([_P, _U32, _U32, _SZ, _P, _SZ, _U32, _P, _P, _P, _P, _U64], _I),
     "dg_set_timing": ([_I], _I),
     "dg_last_timings": ([_P, _P, _P, _I], _I),

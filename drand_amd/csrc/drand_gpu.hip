@@ -43,15 +43,14 @@ int active_sets() {
   }();
   return n;
 }
-// items per group test in Recover's per-item pass (kernels.h verify_group); DG_GROUP=1: every item alone
-uint32_t group_size() {
-  static const uint32_t n = [] {
-    const char* e = getenv("DG_GROUP");
-    int v = e ? atoi(e) : (int)GRP;
-    return (uint32_t)(v < 1 ? 1 : (v > (int)GRP ? (int)GRP : v));
-  }();
-  return n;
-}
+// items per group test in Recover's per-item pass (kernels.h verify_group); DG_GROUP=1 or dg_set_group_size(1):
+// every item alone
+uint32_t g_group_size = [] {
+  const char* e = getenv("DG_GROUP");
+  int v = e ? atoi(e) : (int)GRP;
+  return (uint32_t)(v < 1 ? 1 : (v > (int)GRP ? (int)GRP : v));
+}();
+uint32_t group_size() { return g_group_size; }
 struct Set {
   hipStream_t stream = nullptr;
   std::vector<void*> pool;  // indexed by Slot
@@ -336,14 +335,17 @@ int bind_seed(const Batch& b, uint64_t seed, hipStream_t st, uint64_t** d_seed) 
 int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st);
 
 // `affine`: every point of PA and PB has Z = 1 or Z = 0, so the first levels are affine additions (msm.h).
+// `bad` (device, affine only): raised when an input breaks that precondition (msm.h aff_input_ok); the caller
+// passes its batch-failure flag, so such a batch falls back to exact per-item checks.
 int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JStore* PA, const G2JStore* PB, bool test_windows,
-            bool affine, G2JStore** out, G2JStore** win, hipStream_t st) {
+            bool affine, G2JStore** out, G2JStore** win, hipStream_t st, uint32_t* bad = nullptr) {
   const uint32_t nsides = PB ? 2 : 1, nwin = test_windows ? MSM_WT : MSM_WIN, nbk = nwin * MSM_NB;
   uint32_t *cnt, *list;
   G2JStore *chunks, *BP, *tmp, *P1, *W;
   RET(wsT(S_MSM_CNT, 4 * nbk + 1 + MSM_AFF_L * (nbk + 1), &cnt));
   uint32_t *offset = cnt + nbk, *cursor = offset + nbk, *chunk_off = cursor + nbk;
   RET(wsT(S_MSM_LIST, (size_t)nwin * R + 1, &list));
+  if (affine && !bad) return fail(DG_E_ARG, "msm_run: the affine levels need a failure flag");
   if (affine && !g_ctx.msm_jac) {
     const size_t E = (size_t)nwin * R;
     if (E * nsides > 0x7fffffffull) return fail(DG_E_ARG, "batch too large for the MSM");
@@ -370,7 +372,7 @@ int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JSt
                  (const uint32_t*)offset, gl, (const uint32_t*)list, PA, PB, (const G2AStore*)A, (uint32_t)E, den));
       RET(batch_inv(n, den, dinv, st));
       RET(launch("k_msm_aff_add", k_msm_aff_add, n, 128, st, l, maxg, nsides, nbk, (const uint32_t*)cnt,
-                 (const uint32_t*)offset, gl, (const uint32_t*)list, PA, PB, A, (uint32_t)E, (const Fp*)dinv));
+                 (const uint32_t*)offset, gl, (const uint32_t*)list, PA, PB, A, (uint32_t)E, (const Fp*)dinv, bad));
     }
     RET(launch("k_msm_buckets_aff", k_msm_buckets_aff, nbk * MSM_BSPLIT * nsides, 128, st, nsides, nbk,
                (const uint32_t*)cnt, (const uint32_t*)offset, (const G2AStore*)A, (uint32_t)E, BP));
@@ -479,6 +481,9 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
   // one item per (round, key): the G2 subgroup checks of the signatures are batched on the MSM's window
   // sums (msm.h) instead of a psi check per item (several items of one key in a round share their digits)
   const uint32_t batched_sub = (b.nslots > 1 || b.k == 1) ? 1u : 0u;
+  // flag[2]: the batch's failure flag beside the equation -- the batched subgroup check's window sums
+  // (k_pair_miller_coop) and the affine MSM levels' input check (msm.h aff_input_ok) raise it
+  HIPCHK(hipMemsetAsync(flag + 2, 0, 4, st));
   if (g_ctx.phased) {
     // phases.h: flags / x, the two roots through k_exp_pm3d4, then y, sign and the cell claim
     DecState* ds;
@@ -507,7 +512,7 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
   G2JStore* win = nullptr;
   if (b.nslots == 1) {
     // T = sum alpha_r V_r and K = sum alpha_r Q_r in one MSM (shared bucket sort)
-    RET(msm_run(b.R, seed, active, V, b.Q, batched_sub != 0, g_ctx.phased && b.k == 1, &msm, &win, st));
+    RET(msm_run(b.R, seed, active, V, b.Q, batched_sub != 0, g_ctx.phased && b.k == 1, &msm, &win, st, flag + 2));
     T = msm;
     K = msm + 1;
   } else {
@@ -527,7 +532,7 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
     K = Kp;
     // Kc = sum over the active rounds of alpha_r Q_r (one MSM), Xc = sum_s beta_s X_s
     G2JStore* kmsm;
-    RET(msm_run(b.R, seed, active, b.Q, nullptr, false, g_ctx.phased, &kmsm, nullptr, st));
+    RET(msm_run(b.R, seed, active, b.Q, nullptr, false, g_ctx.phased, &kmsm, nullptr, st, flag + 2));
     Kc = kmsm;
     RET(wsT(S_XC, 1, &Xc));
     RET(launch("k_key_combine", k_key_combine, 256, 256, st, b.nslots, seed, b.keys, b.key_status, Xc));
@@ -536,7 +541,6 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
   // the batched subgroup check's window sums ride in the Miller launch (extra workgroups); k_final_coop folds
   // their verdict (flag[2]) into the batch's
   const uint32_t nsub = batched_sub ? MSM_WT * (b.nslots > 1 ? b.nslots : 1u) : 0u;
-  HIPCHK(hipMemsetAsync(flag + 2, 0, 4, st));
   const bool fuse_sub = !g_ctx.sub_separate;
   RET(launch("k_pair_miller_coop", k_pair_miller_coop, 128 * (npairs + (fuse_sub ? nsub : 0u)), 128, st, b.nslots, seed,
              b.keys, K, T, (const G1AStore*)Xc, Kc, f, npairs, (const G2JStore*)win, flag + 2));
@@ -1217,6 +1221,13 @@ int dg_group_counts(uint64_t* out4) {
   unsigned long long v[GRP];
   HIPCHK(hipMemcpy(v, g_ctx.gcount, sizeof(v), hipMemcpyDeviceToHost));
   for (uint32_t m = 0; m < GRP; ++m) out4[m] = v[m];
+  return 0;
+}
+
+int dg_set_group_size(uint32_t m) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (m < 1 || m > GRP) return fail(DG_E_ARG, "group size must be 1..4");
+  g_group_size = m;
   return 0;
 }
 

@@ -207,7 +207,11 @@ DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_msm_chunks(uint32_t max_ch
 #define DG_MSM_AFF_L 3
 #endif
 constexpr uint32_t MSM_AFF_L = DG_MSM_AFF_L;  // affine levels: chunk sums of 2^3 = 8 entries (A/B: DG_MSM_AFF_L)
-DGI G2A aff_src0(const G2JStore& p) { return G2A{p.x, p.y, fp_is_zero(p.z.c0)}; }  // Z is 0 or 1
+DGI G2A aff_src0(const G2JStore& p) { return G2A{p.x, p.y, fp_is_zero(p.z.c0)}; }  // Z is 0 or 1 (checked below)
+// msm_run's precondition for the affine levels: every input point has Z = 0 (identity) or Z = 1.  Level 0 checks
+// it on every entry it reads and raises *bad otherwise: the caller's batch equation then fails and every item
+// takes its own exact check, so a Jacobian input can never be summed wrong silently.
+DGI bool aff_input_ok(const G2JStore& p) { return fp2_is_zero(p.z) || fp2_eq(p.z, fp2_one()); }
 DGI G2A aff_srcA(const G2AStore& p) { return G2A{p.x, p.y, p.inf != 0}; }
 // group g of level l (groups of 2^(l+1) entries of one bucket) -> its first entry i and bucket end
 DGI bool aff_group(uint32_t nbk, const uint32_t* count, const uint32_t* offset, const uint32_t* gofs, uint32_t l,
@@ -314,7 +318,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_aff_add(uint32_t l, ui
                                                                  const uint32_t* offset, const uint32_t* gofs,
                                                                  const uint32_t* list, const G2JStore* PA,
                                                                  const G2JStore* PB, G2AStore* A, uint32_t E,
-                                                                 const Fp* ninv) {
+                                                                 const Fp* ninv, uint32_t* bad) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= maxg * nsides) return;
   const uint32_t side = t / maxg, g = t % maxg;
@@ -326,12 +330,16 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_aff_add(uint32_t l, ui
   G2A p, q;
   if (l == 0) {
     const G2JStore* P = side ? PB : PA;
-    p = aff_src0(P[list[i]]);
+    const G2JStore& a = P[list[i]];
+    if (!aff_input_ok(a)) atomicOr(bad, 1u);
+    p = aff_src0(a);
     if (!pair) {
       store_g2a(Aside[i], p);
       return;
     }
-    q = aff_src0(P[list[i + 1]]);
+    const G2JStore& b = P[list[i + 1]];
+    if (!aff_input_ok(b)) atomicOr(bad, 1u);
+    q = aff_src0(b);
   } else {
     p = aff_srcA(Aside[i]);
     q = aff_srcA(Aside[i + (1u << l)]);
@@ -350,7 +358,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_aff_add(uint32_t l, ui
                                                                  const uint32_t* offset, const uint32_t* gofs,
                                                                  const uint32_t* list, const G2JStore* PA,
                                                                  const G2JStore* PB, G2AStore* A, uint32_t E,
-                                                                 const Fp* ninv);
+                                                                 const Fp* ninv, uint32_t* bad);
 #endif
 
 // the bucket sums from the affine chunk sums: lane (side, b, q < MSM_BSPLIT) adds chunks q, q + MSM_BSPLIT, ...

@@ -95,15 +95,31 @@ def unpack_bits(bitmap, sizes):
     return np.concatenate([b[r * m:r * m + s] for r, s in enumerate(sizes)])
 
 
-def mad_peak(device=0):
-    """Measured v_mad_u64_u32 lane-MAC rate (the integer-VALU roofline denominator)."""
+def probe_form(device, kind, warm_s=2.0):
+    """One form of the peak probe (tools/microbench/probe.hip kinds): lane-ops/s after warm_s seconds of
+    launches, the in-kernel clock, and the SIMD cycles per wave64 instruction that implies."""
     lib = ctypes.CDLL(PROBE)
     rate = ctypes.c_double()
+    mhz = ctypes.c_double()
     cus = ctypes.c_int()
-    clk = ctypes.c_int()
-    rc = lib.probe_mad_rate(device, ctypes.byref(rate), ctypes.byref(cus), ctypes.byref(clk))
+    rc = lib.probe_run(device, kind, ctypes.c_double(warm_s), ctypes.byref(rate), ctypes.byref(mhz),
+                       ctypes.byref(cus))
     if rc != 0:
-        raise RuntimeError("probe_mad_rate failed")
-    return {"tmac_s": rate.value / 1e12, "cus": cus.value, "clock_khz": clk.value,
-            "source": "measured: dependency-free v_mad_u64_u32 streams (tools/microbench/probe.hip), "
-                      "%d CUs" % cus.value}
+        raise RuntimeError("probe_run failed")
+    simd_cycles = cus.value * 4 * mhz.value * 1e6
+    return {"tops": rate.value / 1e12, "clock_mhz": mhz.value, "cus": cus.value,
+            "cycles_per_wave_instr": simd_cycles / (rate.value / 64.0) if rate.value else None}
+
+
+def mad_peak(device=0):
+    """Measured v_mad_u64_u32 lane-MAC rate (the integer-VALU roofline denominator): eight independent chains
+    per lane with distinct carry destinations, timed after 2 s of back-to-back launches, with the clock the
+    chip held; and the spec-rate ceiling at 2.4 GHz for the measured cycles per instruction."""
+    f = probe_form(device, 1, warm_s=2.0)
+    cyc = f["cycles_per_wave_instr"]
+    spec = f["cus"] * 4 * 2.4e9 * 64 / round(cyc) / 1e12 if cyc else None
+    return {"tmac_s": f["tops"], "cus": f["cus"], "clock_mhz": f["clock_mhz"], "cycles_per_wave_instr": cyc,
+            "spec_tmac_s_at_2400mhz": spec,
+            "source": "measured: 8 independent v_mad_u64_u32 chains per lane, distinct SGPR carry destinations, "
+                      "after 2 s of launches (tools/microbench/probe.hip kind 1), %d CUs at %.0f MHz in-kernel"
+                      % (f["cus"], f["clock_mhz"])}

@@ -1,3 +1,5 @@
+//go:build drandgpu
+
 package gpu
 
 /*
@@ -19,19 +21,24 @@ type Beacon struct {
 	Signature     []byte // 96 B
 }
 
-func beaconArrays(bs []*Beacon) (pr, rr []uint64, ps []byte, off []uint32, sigs []byte, err error) {
+// beaconArrays flattens a batch for the C-ABI.  A signature that is not 96 B becomes 96 zero bytes, which
+// does not decode (no compression flag), so that beacon gets the reference's decode error while the rest of
+// the batch is still checked (bad[i] marks it; kyber's VerifyRecovered fails on such a signature too).
+func beaconArrays(bs []*Beacon) (pr, rr []uint64, ps []byte, off []uint32, sigs []byte, bad []bool) {
 	n := len(bs)
 	pr, rr = make([]uint64, n), make([]uint64, n)
 	off = make([]uint32, n+1)
-	sigs = make([]byte, 0, 96*n)
+	sigs = make([]byte, 96*n)
+	bad = make([]bool, n)
 	for i, b := range bs {
-		if len(b.Signature) != 96 {
-			return nil, nil, nil, nil, nil, fmt.Errorf("gpu: round %d: signature of %d bytes", b.Round, len(b.Signature))
-		}
 		pr[i], rr[i] = b.PreviousRound, b.Round
 		ps = append(ps, b.PreviousSig...)
 		off[i+1] = uint32(len(ps))
-		sigs = append(sigs, b.Signature...)
+		if len(b.Signature) == 96 {
+			copy(sigs[96*i:], b.Signature)
+		} else {
+			bad[i] = true
+		}
 	}
 	return
 }
@@ -60,10 +67,7 @@ func VerifyBeacons(groupKey []byte, bs []*Beacon) ([]error, error) {
 	if len(groupKey) != 48 {
 		return nil, errors.New("gpu: group key of the wrong length")
 	}
-	pr, rr, ps, off, sigs, err := beaconArrays(bs)
-	if err != nil {
-		return nil, err
-	}
+	pr, rr, ps, off, sigs, bad := beaconArrays(bs)
 	st := notRun(n)
 	if rc := C.dg_verify_beacons(ptr(groupKey), C.size_t(n), u64p(pr), u64p(rr), ptr(ps), u32p(off), ptr(sigs),
 		ptr(st), 0); rc != 0 {
@@ -71,7 +75,9 @@ func VerifyBeacons(groupKey []byte, bs []*Beacon) ([]error, error) {
 	}
 	out := make([]error, n)
 	for i, v := range st {
-		if v != C.DG_ST_OK {
+		if bad[i] {
+			out[i] = fmt.Errorf("gpu: round %d: signature of %d bytes", bs[i].Round, len(bs[i].Signature))
+		} else if v != C.DG_ST_OK {
 			out[i] = fmt.Errorf("gpu: round %d: invalid beacon (status %d)", bs[i].Round, v)
 		}
 	}
@@ -80,16 +86,15 @@ func VerifyBeacons(groupKey []byte, bs []*Beacon) ([]error, error) {
 
 // SyncBatch is one batch of syncFrom's loop (beacon/beacon.go:557-602) for rounds streamed by one peer:
 // the link check against the last stored round (:561-573) and VerifyRecovered of every round (:575).  It
-// returns how many leading beacons may be stored: the reference stops at the first bad reply.
+// returns how many leading beacons may be stored: the reference stores every reply before the first bad
+// one and stops there (:575-587), so a malformed reply (a signature that is not 96 B) ends the prefix at
+// its own position instead of failing the whole batch.
 func SyncBatch(groupKey []byte, curRound uint64, curSig []byte, bs []*Beacon) (int, error) {
 	n := len(bs)
 	if n == 0 {
 		return 0, nil
 	}
-	pr, rr, ps, off, sigs, err := beaconArrays(bs)
-	if err != nil {
-		return 0, err
-	}
+	pr, rr, ps, off, sigs, _ := beaconArrays(bs)
 	links := notRun(n)
 	if rc := C.dg_check_links(C.uint64_t(curRound), ptr(curSig), C.size_t(len(curSig)), C.size_t(n), u64p(pr), u64p(rr),
 		ptr(ps), u32p(off), ptr(sigs), ptr(links)); rc != 0 {

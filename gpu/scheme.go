@@ -1,3 +1,5 @@
+//go:build drandgpu
+
 // Package gpu is the drop-in of libdrandgpu.so (include/drand_gpu.h) behind drand's signature scheme:
 // it implements kyber's sign.ThresholdScheme, the interface key.Scheme has (key/curve.go:30) and
 // beacon.Config.Scheme receives (beacon/beacon.go:33; core/drand.go:335), plus batch methods with no
@@ -8,8 +10,10 @@
 // the CPU kyber scheme (latency: a GPU batch is milliseconds); batches of at least MinBatch items go to the
 // GPU.
 //
-// Go is not installed in the image this was written in: compile-checked against the header by
-// tests/native/abi_caller.cpp (the same C signatures), not by cgo.
+// EXPERIMENTAL, behind the `drandgpu` build tag: Go is not installed in the image this was written in, so
+// the package has never been compiled by cgo nor checked against sign.ThresholdScheme at the kyber version
+// go.mod pins; only its C calls are compile-checked, against the header, by tests/native/abi_caller.cpp.
+// Build it with `go build -tags drandgpu` once it has been compiled and tested against the reference.
 package gpu
 
 /*
@@ -21,6 +25,7 @@ package gpu
 import "C"
 
 import (
+	"bytes"
 	"errors"
 	"fmt"
 	"sync"
@@ -271,11 +276,21 @@ func (s *Scheme) RecoverBatch(public *share.PubPoly, msgs [][]byte, partials [][
 	return splitRecover(sig, rs, R)
 }
 
+// Verdict is a VerifyPartial verdict ProcessBeacon already holds for a partial (beacon/beacon.go:148), with
+// the message it was computed against: the message of the packet's own PreviousSig (:146).
+type Verdict struct {
+	Err error  // nil = valid
+	Msg []byte // the message the verdict is for
+}
+
 // RecoverVerified is the live round (beacon/beacon.go:472-494): ProcessBeacon already ran VerifyPartial on
 // every partial the round cache holds (beacon/beacon.go:148, round_cache.go:113-119), and kyber's Recover
-// (:488) would verify each of them again.  verified[j] is that verdict (nil = valid); invalid ones are
-// skipped as Recover skips them.  No pairing is computed; the caller vouches for the verdicts.
-func (s *Scheme) RecoverVerified(partials [][]byte, verified []error, t, n int) ([]byte, error) {
+// (:488) would verify each of them again, against the node's own msg.  A verdict is reused only when it was
+// computed against msg: the round cache admits a partial on PreviousRound alone (round_cache.go:40-48), so a
+// packet built on another PreviousSig carries a verdict for another message; such partials are verified
+// here against msg (kyber, CPU: the rare case), as Recover would.  Invalid ones are skipped as Recover skips
+// them.  No pairing runs on the GPU.
+func (s *Scheme) RecoverVerified(public *share.PubPoly, msg []byte, partials [][]byte, verified []Verdict, t, n int) ([]byte, error) {
 	k := len(partials)
 	if k != len(verified) {
 		return nil, errors.New("gpu: partials and verdicts differ in length")
@@ -292,7 +307,11 @@ func (s *Scheme) RecoverVerified(partials [][]byte, verified []error, t, n int) 
 			continue
 		}
 		p = append(p, x...)
-		if verified[j] != nil {
+		err := verified[j].Err
+		if !bytes.Equal(verified[j].Msg, msg) {
+			err = s.cpu.VerifyPartial(public, msg, x) // a verdict for another message is no verdict for msg
+		}
+		if err != nil {
 			vst[j] = C.DG_ST_BAD_SIG
 		}
 	}

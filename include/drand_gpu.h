@@ -18,6 +18,11 @@
  *     without a device every compute entry point returns DG_E_NODEV.
  *   - `msg_len` is the per-item message length (drand: 32 B SHA-256 outputs); all items of one call
  *     share it.  Messages are laid out back to back (n x msg_len bytes).
+ *   - Verdicts of the batch paths are exact for every rejected item and probabilistic for accepted ones:
+ *     a batch (or a Recover group test of up to 4 shares) that passes its random-linear-combination
+ *     equation accepts all its members, and a bad member survives with probability <= 2^-63 (64-bit
+ *     coefficients bound to the batch contents).  A failed equation sends every member to
+ *     its own pairing check.  dg_set_group_size(1) makes Recover's per-item pass use single checks only.
  */
 #ifndef DRAND_GPU_H
 #define DRAND_GPU_H
@@ -106,7 +111,9 @@ int dg_verify_partials(const uint8_t* commits48, uint32_t t, size_t rounds, cons
 /* A6 -- tbls.Recover batch (beacon/beacon.go:488): per round, the first t partials (input order) that
  * pass VerifyPartial, deduplicated by index, Lagrange-interpolated at 0 on G2.  round_status[r] is
  * DG_ST_OK or DG_ST_NOT_ENOUGH; share_status[r*k + j] is the VerifyPartial status of partials Recover
- * examined and DG_ST_NOT_EXAMINED for the rest. */
+ * examined and DG_ST_NOT_EXAMINED for the rest.  After a failed batch equation the examined prefix is
+ * checked by group tests (see Conventions: an accepted member is valid except with probability <= 2^-63;
+ * rejected members and every member of a failed group get their own exact check). */
 int dg_recover(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t rounds, const uint8_t* msgs,
                size_t msg_len, uint32_t k, const uint8_t* partials98, uint8_t* out_sig96, uint8_t* round_status,
                uint8_t* share_status, uint64_t seed);
@@ -116,7 +123,11 @@ int dg_recover(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t ro
  * (beacon/round_cache.go:113-119) kept it, and kyber's Recover (:488) verifies each again.  verified_status[r*k + j]
  * is that verdict (DG_ST_OK = valid); a non-OK partial is skipped exactly as Recover skips a failing one.
  * Per round: the first t partials with an OK verdict (input order), deduplicated by index, Lagrange-interpolated
- * at 0 on G2; no pairing is computed.  Outputs as dg_recover.  The caller vouches for the verdicts. */
+ * at 0 on G2; no pairing is computed.  Outputs as dg_recover.  The caller vouches for the verdicts, and each
+ * must have been computed against THIS round's message: ProcessBeacon verifies a packet against the message
+ * built from the packet's own PreviousSig (beacon/beacon.go:146-148) while the round cache admits partials
+ * by PreviousRound alone (round_cache.go:40-48), so a verdict for another prev-sig is not a verdict for this
+ * message -- the Go wrapper (gpu.Scheme.RecoverVerified) re-verifies such partials before calling this. */
 int dg_recover_verified(uint32_t t, uint32_t nshares, size_t rounds, uint32_t k, const uint8_t* partials98,
                         const uint8_t* verified_status, uint8_t* out_sig96, uint8_t* round_status,
                         uint8_t* share_status);
@@ -155,6 +166,9 @@ int dg_fallback_count(uint64_t* out);
 /* Recover's per-item pass since dg_init (waits for batches in flight): out4[m - 1] = checks of m shares of
  * one round at once (m = 1: a share's own bls.Verify; m = 2..4: a random-linear-combination group test). */
 int dg_group_counts(uint64_t* out4);
+/* Shares per group test in Recover's per-item pass: 1..4 (default 4, or the DG_GROUP environment variable);
+ * 1 = every examined share gets its own exact pairing check.  Process-wide. */
+int dg_set_group_size(uint32_t m);
 /* Wait for every batch enqueued by the asynchronous entry points. */
 int dg_wait_all(void);
 

@@ -41,6 +41,7 @@ EXPECT_TYPE(dg_verify_beacons_dev_async, int (*)(const uint8_t*, size_t, const u
 EXPECT_TYPE(dg_last_batch_flags, int (*)(uint32_t*));
 EXPECT_TYPE(dg_fallback_count, int (*)(uint64_t*));
 EXPECT_TYPE(dg_group_counts, int (*)(uint64_t*));
+EXPECT_TYPE(dg_set_group_size, int (*)(uint32_t));
 EXPECT_TYPE(dg_recover_dev, int (*)(const uint8_t*, uint32_t, uint32_t, size_t, const uint8_t*, size_t, uint32_t,
                                     const uint8_t*, uint8_t*, uint8_t*, uint8_t*, uint64_t));
 EXPECT_TYPE(dg_wait_all, int (*)(void));
@@ -96,6 +97,10 @@ int main() {
   expect("dg_get_hash_dst", dg_get_hash_dst(out, sizeof out, &len), 0);
   expect("switched DST", (int)len == 3 && memcmp(out, "ABC", 3) == 0, 1);
   expect("dst too long", dg_set_hash_dst(out, 256), DG_E_ARG);
+  expect("dg_set_group_size", dg_set_group_size(1), 0);
+  expect("group size 0", dg_set_group_size(0), DG_E_ARG);
+  expect("group size 5", dg_set_group_size(5), DG_E_ARG);
+  expect("dg_set_group_size 4", dg_set_group_size(4), 0);
   expect("reset DST", dg_set_hash_dst(nullptr, 0), 0);
   expect("error text", dg_last_error() != nullptr, 1);
   dg_shutdown();

@@ -1,8 +1,11 @@
 """Per-unit Montgomery multiplication/squaring counts of each verify-path kernel, from the instrumented
 host build of the device arithmetic (liboc.so), averaged over the committed 64-round chain fixture.
 Writes profiles/opcounts.json, which bench.py reads to convert kernel time into multiply-adds/s.
-MACs: one fp_mul = 288, one fp_sqr = 222 -- the 32x32-bit multiply-adds of a 12-limb Montgomery product
-(the algorithmic unit; the radix-2^28 kernels of fp28.h execute 392 / 301 narrower ones)."""
+MACs (the algorithmic unit): one Montgomery multiplication or squaring M = 300 32x32-bit
+multiply-adds, 2 * 12^2 + 12 for 12-limb CIOS, a squaring counted as a multiplication.  vmad (the issue
+unit): the v_mad_u64_u32 the radix-2^28 kernels of fp28.h execute, 392 per multiplication and 301 per
+squaring (14 x 14 column products + 14 x 14 reduction products; the squaring doubles the off-diagonal
+terms), counted in the disassembly (profiles/r3_vmad_counts.txt)."""
 import ctypes
 import hashlib
 import json
@@ -13,7 +16,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
-MAC_MUL, MAC_SQR = 288, 222
+MAC_MUL, MAC_SQR = 300, 300
+VMAD_MUL, VMAD_SQR = 392, 301
 # one safegcd inversion (field.h fp_inv): 37 batches x 13 limbs x (6 + 4) signed 32x32->64 multiply-adds
 MAC_INV = 37 * 13 * 10
 DST = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"
@@ -79,11 +83,13 @@ def main():
                 add("k_verify_groups[%d]" % m)
             L.oc_batch_final(pk, sig, nxt, o)
             add("k_pair_miller+k_final_check")
-    out = {"mac_per_mul": MAC_MUL, "mac_per_sqr": MAC_SQR, "mac_per_inv": MAC_INV, "sample": "tests/golden/chain_t3n5.json (64 rounds)",
-           "per_unit": {}}
+    out = {"mac_per_mul": MAC_MUL, "mac_per_sqr": MAC_SQR, "mac_per_inv": MAC_INV, "vmad_per_mul": VMAD_MUL,
+           "vmad_per_sqr": VMAD_SQR, "basis": "BASELINE.md: 300 multiply-adds per Montgomery product M",
+           "sample": "tests/golden/chain_t3n5.json (64 rounds)", "per_unit": {}}
     for k, (m, s, v, n) in acc.items():
         out["per_unit"][k] = {"mul": m / n, "sqr": s / n, "inv": v / n, "M": (m + s) / n,
-                              "macs": (m * MAC_MUL + s * MAC_SQR + v * MAC_INV) / n}
+                              "macs": (m * MAC_MUL + s * MAC_SQR + v * MAC_INV) / n,
+                              "vmad": (m * VMAD_MUL + s * VMAD_SQR + v * MAC_INV) / n}
     out["per_unit"]["k_key_accum"] = out["per_unit"]["k_sum_rows"]
     out["per_unit"]["k_recover_terms_u"] = out["per_unit"]["k_recover_terms"]  # the same Straus, LDS running point
     with open(os.path.join(ROOT, "profiles", "opcounts.json"), "w") as f:
