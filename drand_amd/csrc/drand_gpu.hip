@@ -130,7 +130,8 @@ enum Slot {
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
   S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_BINV, S_NV, S_NVINV,
-  S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_BINV_PRE, S_BINV_ROOTS, S_COUNT
+  S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_BINV_PRE, S_BINV_ROOTS, S_RC_UNI, S_RC_REF, S_RC_LAM,
+  S_RC_DIG, S_RC_NAF, S_RC_EV, S_RC_TAB, S_RC_D, S_RC_PINF, S_RC_DEN, S_RC_A, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -261,13 +262,15 @@ int wsT(Slot s, size_t count, T** out) {
 // Collapse each of `rows` rows of `cols` Jacobian points (row-major in buf) to its sum, left in buf[row].
 // Pairwise levels by default (one dependent addition per lane per launch): these launches run on a nearly
 // empty chip, so their time is the depth of the addition chain, not the number of additions.
-int reduce_rows(G2JStore* buf, G2JStore* tmp, uint32_t rows, uint32_t cols, hipStream_t st, uint32_t max_chunk = 2) {
+// skip (device, may be null): rows of a block of 64 with skip[row / 64] != 0 are not summed (their result is garbage).
+int reduce_rows(G2JStore* buf, G2JStore* tmp, uint32_t rows, uint32_t cols, hipStream_t st, uint32_t max_chunk = 2,
+                const uint8_t* skip = nullptr) {
   G2JStore* src = buf;
   G2JStore* dst = tmp;
   while (cols > 1) {
     uint32_t chunk = cols < max_chunk ? cols : max_chunk;
     uint32_t ocols = (cols + chunk - 1) / chunk;
-    RET(launch("k_sum_rows", k_sum_rows, rows * ocols, 128, st, rows, cols, chunk, (const G2JStore*)src, dst));
+    RET(launch("k_sum_rows", k_sum_rows, rows * ocols, 128, st, rows, cols, chunk, (const G2JStore*)src, dst, skip));
     cols = ocols;
     std::swap(src, dst);
   }
@@ -849,23 +852,92 @@ int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const 
 // Recover after the VerifyPartial statuses are known (d_st): per round the first t valid partials, xyCommit
 // dedupe, Lagrange terms lambda_j S_j, row sums, compression; results copied to the output buffers (host or
 // device memory: hipMemcpyDefault).
+// Recover's per-round MSM over the uniform blocks (recover.h): lambda / digit schedules per block, the odd-multiple
+// tables (affine levels with batch inversions), the four psi-component Straus lanes per round, the combination
+// into out[r].  ub: the U uniform blocks that hold an OK round (device).
+int recover_msm(uint32_t R, uint32_t k, uint32_t t, uint32_t U, const uint32_t* ub, const uint32_t* ref,
+                const uint32_t* d_selidx, const uint32_t* d_sel, const uint8_t* d_rst, const G2AStore* d_S,
+                G2JStore* out, hipStream_t st) {
+  const uint32_t Ru = U * RC_BLK, maxev = t * RC_EV_PER_SHARE;
+  const size_t nel = (size_t)t * Ru;
+  if (nel > 0x7fffffffull) return fail(DG_E_ARG, "Recover batch too large for the MSM tables");
+  Fr *lam, *pre;
+  uint64_t* dig;
+  int8_t* naf;
+  uint32_t *ev, *hdr;
+  uint4 *T4, *D4;
+  uint8_t* pinf;
+  Fp *den, *dinv;
+  G2JStore* A;
+  RET(wsT(S_RC_LAM, (size_t)2 * U * t, &lam));
+  pre = lam + (size_t)U * t;
+  RET(wsT(S_RC_DIG, (size_t)4 * U * t, &dig));
+  RET(wsT(S_RC_NAF, (size_t)U * t * RC_NAF, &naf));
+  RET(wsT(S_RC_EV, (size_t)4 * U * maxev + (size_t)8 * U, &ev));
+  hdr = ev + (size_t)4 * U * maxev;
+  RET(wsT(S_RC_TAB, nel * RC_TAB * RC_Q, &T4));
+  RET(wsT(S_RC_D, nel * RC_Q, &D4));
+  RET(wsT(S_RC_PINF, nel, &pinf));
+  RET(wsT(S_RC_DEN, 2 * nel, &den));
+  dinv = den + nel;
+  RET(wsT(S_RC_A, (size_t)4 * Ru, &A));
+  RET(launch("k_rc_digits", k_rc_digits, U, 64, st, U, t, maxev, ub, ref, d_selidx, lam, pre, dig, naf, ev, hdr));
+  for (uint32_t l = 0; l < RC_TAB; ++l) {
+    RET(launch("k_rc_tab_den", k_rc_tab_den, (uint32_t)nel, 128, st, l, R, Ru, k, t, ub, d_rst, d_sel, d_S,
+               (const uint4*)T4, (const uint4*)D4, pinf, den));
+    RET(batch_inv((uint32_t)nel, den, dinv, st));
+    RET(launch("k_rc_tab_add", k_rc_tab_add, (uint32_t)nel, 128, st, l, R, Ru, k, t, ub, d_rst, d_sel, d_S, T4, D4,
+               (const uint8_t*)pinf, (const Fp*)dinv));
+  }
+  RET(launch("k_rc_straus", k_rc_straus, 4 * Ru, 64, st, R, Ru, maxev, ub, d_rst, (const uint32_t*)ev,
+             (const uint32_t*)hdr, (const uint4*)T4, (const uint8_t*)pinf, A));
+  return launch("k_rc_combine", k_rc_combine, Ru, 128, st, R, Ru, ub, d_rst, (const G2JStore*)A, out);
+}
+
+// Recover after the VerifyPartial statuses are known (d_st): per round the first t valid partials, xyCommit
+// dedupe; blocks of 64 rounds that selected one index set take the per-round MSM (recover.h), the others the
+// Lagrange terms lambda_j S_j and row sums; compression; results copied to the output buffers (host or device
+// memory: hipMemcpyDefault).
 int recover_tail(uint32_t R, uint32_t k, uint32_t t, const uint8_t* d_p, const uint8_t* d_st, const G2AStore* d_S,
                  uint8_t* out_sig96, uint8_t* round_status, uint8_t* share_status, hipStream_t st) {
-  uint8_t *d_rst, *d_sst, *d_out;
-  uint32_t *d_sel, *d_selidx;
+  uint8_t *d_rst, *d_sst, *d_out, *d_uni;
+  uint32_t *d_sel, *d_selidx, *d_ref, *d_ub;
   G2JStore *terms, *tmp;
+  const uint32_t nblk = (R + RC_BLK - 1) / RC_BLK, Rp = nblk * RC_BLK;
   RET(wsT(S_SEL, (size_t)R * t, &d_sel));
   RET(wsT(S_SELIDX, (size_t)R * t, &d_selidx));
   RET(wsT(S_RST, R, &d_rst));
   RET(wsT(S_SST, (size_t)R * k, &d_sst));
   RET(launch("k_recover_select", k_recover_select, R, 128, st, R, k, t, d_p, d_st, d_sel, d_selidx, d_rst, d_sst));
-  RET(wsT(S_TERMS, (size_t)R * t, &terms));
-  RET(wsT(S_TMP, (size_t)R * t, &tmp));
-  RET(launch("k_recover_terms_u", k_recover_terms_u, R * t, 64, st, R, k, t, (const uint32_t*)d_sel,
-             (const uint32_t*)d_selidx, (const uint8_t*)d_rst, d_S, terms));
-  RET(launch("k_recover_terms", k_recover_terms, R * t, 64, st, R, k, t, (const uint32_t*)d_sel,
-             (const uint32_t*)d_selidx, (const uint8_t*)d_rst, d_S, terms));
-  RET(reduce_rows(terms, tmp, R, t, st));
+  RET(wsT(S_RC_UNI, nblk, &d_uni));
+  RET(wsT(S_RC_REF, 2 * (size_t)nblk, &d_ref));
+  d_ub = d_ref + nblk;
+  RET(launch("k_rc_blocks", k_rc_blocks, nblk * RC_BLK, 64, st, R, t, (const uint32_t*)d_selidx, (const uint8_t*)d_rst,
+             d_uni, d_ref));
+  // the host orders the work: which blocks are uniform (and hold an OK round) decides the launch sizes
+  std::vector<uint8_t> uni(nblk);
+  std::vector<uint32_t> ref(nblk);
+  HIPCHK(hipMemcpyAsync(uni.data(), d_uni, nblk, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(ref.data(), d_ref, 4 * (size_t)nblk, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  std::vector<uint32_t> ub;
+  uint32_t nonuni = 0;
+  for (uint32_t b = 0; b < nblk; ++b) {
+    if (!uni[b]) ++nonuni;
+    else if (ref[b] != ~0u) ub.push_back(b);
+  }
+  const uint32_t U = (uint32_t)ub.size();
+  RET(wsT(S_TERMS, (size_t)(nonuni ? R : 1) * (nonuni ? t : 1) + R, &terms));
+  if (nonuni) {
+    RET(wsT(S_TMP, (size_t)R * t, &tmp));
+    RET(launch("k_recover_terms", k_recover_terms, t * Rp, 64, st, R, Rp, k, t, (const uint32_t*)d_sel,
+               (const uint32_t*)d_selidx, (const uint8_t*)d_rst, (const uint8_t*)d_uni, d_S, terms));
+    RET(reduce_rows(terms, tmp, R, t, st, 2, d_uni));
+  }
+  if (U) {
+    HIPCHK(hipMemcpyAsync(d_ub, ub.data(), 4 * (size_t)U, hipMemcpyHostToDevice, st));
+    RET(recover_msm(R, k, t, U, d_ub, d_ref, d_selidx, d_sel, d_rst, d_S, terms, st));
+  }
   RET(wsT(S_OUT0, (size_t)R * 96, &d_out));
   RET(launch("k_compress_g2", k_compress_g2, R, 128, st, R, (const G2JStore*)terms, (const uint8_t*)d_rst, d_out));
   HIPCHK(hipMemcpyAsync(out_sig96, d_out, (size_t)R * 96, hipMemcpyDefault, st));

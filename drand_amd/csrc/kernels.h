@@ -372,12 +372,14 @@ DG_KERNEL void __launch_bounds__(256) k_key_combine(uint32_t nslots, const uint6
 
 // 2-D segmented sum: out[row * ocols + j] = sum_{c in [j*chunk, (j+1)*chunk) and < cols} in[row * cols + c]
 #if DG_TU_LIB
+// (rows of a block with skip[row / 64] != 0 are left alone: skip may be null)
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_sum_rows(uint32_t rows, uint32_t cols, uint32_t chunk, const G2JStore* in,
-                                                 G2JStore* out) {
+                                                 G2JStore* out, const uint8_t* skip) {
   uint32_t ocols = (cols + chunk - 1) / chunk;
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= rows * ocols) return;
   uint32_t row = g / ocols, j = g % ocols;
+  if (skip && skip[row / 64]) return;
   uint32_t a = j * chunk, b = a + chunk < cols ? a + chunk : cols;
   const G2JStore* p = in + (size_t)row * cols;
   G2J acc = load_g2j(p[a]);
@@ -863,50 +865,18 @@ DG_KERNEL void __launch_bounds__(128) k_decode_verified(uint32_t n, const uint8_
 }
 #endif
 
-// thread (m, r), rounds fastest: terms[r * t + m] = lambda_m * S_{r, sel[m]} (lambda over the round's t
-// selected indices).  A wave covers 64 rounds of the same position m, so while the rounds select the same
-// index set (every round with no bad share among its first t) its lanes share lambda_m and the scalar
-// multiplication's digit-dependent branches are uniform across the wave.  Two kernels split the waves:
-// k_recover_terms_u takes the uniform ones (branching Straus, running point in LDS), k_recover_terms the
-// others (sign-aligned column form: 65 doublings + 65 additions whatever the digits, no divergence); each
-// returns at once on the other's waves, so each keeps its own (smaller) private segment.
-// hot translation unit (kernels_hot.hip: flat, 2 waves/SIMD; measured -27% / -36%)
+// The per-term path of Recover, for the blocks of 64 rounds whose rounds selected different index sets
+// (recover.h k_rc_blocks: uni[b] == 0; the uniform blocks take the per-round MSM of recover.h): lane (m, r), rounds
+// fastest over the padded count Rp = 64 * blocks, terms[r * t + m] = lambda_m S_{r, sel[m]} by the sign-aligned
+// column form (g2_mul_u256_psi_sac: 65 doublings + 65 additions whatever the digits, no divergence).  The row sums
+// (k_sum_rows, skipping the uniform blocks) follow.  Hot translation unit (kernels_hot.hip: flat, 2 waves/SIMD).
 #if DG_TU_HOT
-// the wave's rounds (those with status OK) selected the same index set
-DGI bool recover_wave_uniform(uint32_t R, uint32_t t, const uint32_t* selidx, const uint8_t* round_status, uint32_t r) {
-  const bool ok = r < R && round_status[r] == DG_ST_OK_;
-  const uint64_t okm = __ballot(ok);
-  if (okm == 0) return true;
-  const int ref = __ffsll((unsigned long long)okm) - 1;
-  bool same = true;
-  for (uint32_t j = 0; j < t; ++j) {
-    const uint32_t v = ok ? selidx[(size_t)r * t + j] : 0u;
-    same = same && (!ok || v == (uint32_t)__shfl((int)v, ref));
-  }
-  return __all(same);
-}
-DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms_u(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
-                                                       const uint32_t* selidx, const uint8_t* round_status,
-                                                       const G2AStore* S, G2JStore* terms) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, m = g / R, r = g % R;
-  if (!recover_wave_uniform(R, t, selidx, round_status, g < R * t ? r : R)) return;
-  if (g >= R * t) return;
-  const size_t o = (size_t)r * t + m;
-  if (round_status[r] != DG_ST_OK_) {
-    store_g2j(terms[o], jac_infinity<Fp2>());
-    return;
-  }
-  const Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, m);
-  __shared__ G2JStore s_acc[64];
-  g2_mul_u256_psi_lds(load_g2a(S[(size_t)r * k + sel[o]]), lam.l, s_acc[threadIdx.x]);
-  terms[o] = s_acc[threadIdx.x];
-}
-DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
-                                                     const uint32_t* selidx, const uint8_t* round_status,
+DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms(uint32_t R, uint32_t Rp, uint32_t k, uint32_t t,
+                                                     const uint32_t* sel, const uint32_t* selidx,
+                                                     const uint8_t* round_status, const uint8_t* uni,
                                                      const G2AStore* S, G2JStore* terms) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, m = g / R, r = g % R;
-  if (recover_wave_uniform(R, t, selidx, round_status, g < R * t ? r : R)) return;
-  if (g >= R * t) return;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, m = g / Rp, r = g % Rp;
+  if (m >= t || uni[r / 64] || r >= R) return;
   const size_t o = (size_t)r * t + m;
   if (round_status[r] != DG_ST_OK_) {
     store_g2j(terms[o], jac_infinity<Fp2>());
@@ -916,11 +886,9 @@ DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms(uint32_t R,
   store_g2j(terms[o], g2_mul_u256_psi_sac(load_g2a(S[(size_t)r * k + sel[o]]), lam.l));
 }
 #else
-DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms_u(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
-                                                       const uint32_t* selidx, const uint8_t* round_status,
-                                                       const G2AStore* S, G2JStore* terms);
-DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms(uint32_t R, uint32_t k, uint32_t t, const uint32_t* sel,
-                                                     const uint32_t* selidx, const uint8_t* round_status,
+DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms(uint32_t R, uint32_t Rp, uint32_t k, uint32_t t,
+                                                     const uint32_t* sel, const uint32_t* selidx,
+                                                     const uint8_t* round_status, const uint8_t* uni,
                                                      const G2AStore* S, G2JStore* terms);
 #endif
 
@@ -967,3 +935,4 @@ DG_KERNEL void __launch_bounds__(128) k_sign(uint32_t n, const uint8_t* sc32, co
 
 #include "phases.h"
 #include "msm.h"
+#include "recover.h"

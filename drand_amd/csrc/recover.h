@@ -1,0 +1,338 @@
+// Recover as one multi-scalar multiplication per round (A6: kyber tbls.Recover at beacon/beacon.go:488 ->
+// share.RecoverCommit; north_star: "Lagrange-in-the-exponent Recover as a ... multi-scalar multiplication").
+//
+//   sigma_r = sum_j lambda_j S_{r,j}            (t selected shares, lambda_j = prod_{m != j} x_m / (x_m - x_j))
+//
+// Every lambda_j < r is split into base-|z| digits (psi acts on G2 as [z], z = -|z|, r < |z|^4):
+//   lambda_j = d0 + d1 |z| + d2 |z|^2 + d3 |z|^3   ->   [lambda_j]P = [d0]P - [d1]psi(P) + [d2]psi^2(P) - [d3]psi^3(P)
+// so sigma_r = A0 - psi(A1) + psi^2(A2) - psi^3(A3) with A_i = sum_j [d_i(lambda_j)] S_{r,j}: four MSMs of t points
+// with 64-bit scalars, one lane each, sharing ONE 64-doubling chain over all t points (Straus) instead of the
+// t separate chains of t scalar multiplications (round 2).  The scalars are width-5 signed digits (wNAF: odd
+// digits in [-15, 15], at most one non-zero in any 5 consecutive positions, ~11 per 64-bit digit), added from a
+// table of the odd multiples 1P, 3P, ..., 15P of every share.
+//
+// Rounds are grouped in blocks of 64 (one wave).  A block whose OK rounds all selected the same index set --
+// every round of a valid chain -- shares lambda, so its digit schedule (the ordered list of additions and
+// doublings) is one wave-uniform list read with scalar loads: no divergence, no per-lane scalar.  Work per
+// round: the tables (1 tangent + 7 chord affine additions per share, the denominators of each level inverted
+// together over the whole batch: ~15 Fp products per addition), 4 x 64 doublings and ~11 t x 4 mixed additions,
+// against 64 doublings + ~86 mixed additions PER SHARE before.
+//   k_rc_blocks    per block: uniform?  first OK round (the block's lambda source)
+//   k_rc_digits    per uniform block: lambda (one Fr inversion for all t), base-|z| digits, wNAF schedules
+//   k_rc_tab_den / batch inversion / k_rc_tab_add     per level: the odd-multiple tables, affine (SoA in HBM)
+//   k_rc_straus    lane (component i, round): A_i by the block's schedule, running point in LDS
+//   k_rc_combine   per round: sigma = A0 - psi(A1) + psi^2(A2) - psi^3(A3)
+// Blocks whose rounds selected different index sets (corrupted shares, C5) keep the per-term path
+// (k_recover_terms, sign-aligned column form) and the row sums.
+#pragma once
+// included from kernels.h (uses the G2AStore / G2JStore layouts, the Fr helpers and DG_ST_OK_ defined there)
+
+#if !defined(__HIP__)
+struct uint4 {  // the HIP vector type, for the host builds of this header (tests/native, tools/opcount)
+  uint32_t x, y, z, w;
+};
+#endif
+
+namespace dg {
+
+constexpr uint32_t RC_W = 5;                                       // signed-digit width
+constexpr uint32_t RC_TAB = 1u << (RC_W - 2);                      // 8 odd multiples per share
+constexpr uint32_t RC_BLK = 64;                                    // rounds per block (one wave)
+constexpr uint32_t RC_NAF = 65;                                    // digit positions of a 64-bit scalar
+constexpr uint32_t RC_EV_PER_SHARE = (RC_NAF + RC_W - 1) / RC_W;   // at most 13 non-zero digits per scalar
+constexpr uint32_t RC_Q = 12;                                      // uint4 words of one affine table entry
+
+// schedule event: bits 0..15 share j, 16..18 table entry e (the multiple 2e + 1), 19 subtract, 20..27 doublings
+// to run before this addition
+DGI uint32_t rc_event(uint32_t j, uint32_t e, uint32_t neg, uint32_t dbl) { return j | e << 16 | neg << 19 | dbl << 20; }
+DGI uint32_t rc_ev_j(uint32_t v) { return v & 0xffffu; }
+DGI uint32_t rc_ev_e(uint32_t v) { return (v >> 16) & 7u; }
+DGI bool rc_ev_neg(uint32_t v) { return (v >> 19) & 1u; }
+DGI uint32_t rc_ev_dbl(uint32_t v) { return v >> 20; }
+
+// width-RC_W non-adjacent form of a 64-bit scalar, positions 0..64 (65-bit arithmetic for the carry)
+DGI void rc_wnaf(uint64_t d, int8_t* naf) {
+  uint64_t lo = d, hi = 0;
+  for (uint32_t b = 0; b < RC_NAF; ++b) {
+    int z = 0;
+    if (lo & 1u) {
+      const int m = (int)(lo & ((1u << RC_W) - 1));
+      z = m >= (1 << (RC_W - 1)) ? m - (1 << RC_W) : m;
+      if (z > 0) {
+        lo -= (uint64_t)z;  // lo mod 2^w = z: no borrow
+      } else {
+        const uint64_t s = lo + (uint64_t)(-z);
+        hi += s < lo ? 1u : 0u;
+        lo = s;
+      }
+    }
+    naf[b] = (int8_t)z;
+    lo = (lo >> 1) | (hi << 63);
+    hi >>= 1;
+  }
+}
+
+// The schedule of sum_j [d_j] P_j (Horner over the digit positions, top down; within a position by share):
+// events ev[0..n), and `tail` doublings after the last one.  naf: t x RC_NAF scratch.
+DGI uint32_t rc_schedule(const uint64_t* d, uint32_t t, int8_t* naf, uint32_t* ev, uint32_t& tail) {
+  for (uint32_t j = 0; j < t; ++j) rc_wnaf(d[j], naf + (size_t)RC_NAF * j);
+  uint32_t n = 0;
+  int last = -1;
+  for (int b = (int)RC_NAF - 1; b >= 0; --b)
+    for (uint32_t j = 0; j < t; ++j) {
+      const int z = naf[(size_t)RC_NAF * j + b];
+      if (!z) continue;
+      const uint32_t a = (uint32_t)(z < 0 ? -z : z);
+      ev[n++] = rc_event(j, (a - 1) / 2, z < 0 ? 1u : 0u, last < 0 ? 0u : (uint32_t)(last - b));
+      last = b;
+    }
+  tail = last < 0 ? 0u : (uint32_t)last;
+  return n;
+}
+
+// lambda_j (plain, 8 little-endian limbs) for j < t over the interpolation points x_m = idx[m] + 1 (kyber
+// lagrangeBasis at 0), all t with one Fr inversion: den_j = x_j prod_{m != j} (x_m - x_j), inverted together
+// (Montgomery's trick; `pre` holds the prefix products), lambda_j = (prod_m x_m) / den_j.
+DGI void rc_lambdas(const uint32_t* idx, uint32_t t, Fr* lam, Fr* pre) {
+  Fr num = fr_const(FR_ONE);
+  for (uint32_t j = 0; j < t; ++j) {
+    const Fr xj = fr_from_u32(idx[j] + 1);
+    num = fr_mul(num, xj);
+    Fr den = xj;
+    for (uint32_t m = 0; m < t; ++m)
+      if (m != j) den = fr_mul(den, fr_sub(fr_from_u32(idx[m] + 1), xj));
+    lam[j] = den;
+  }
+  Fr acc = fr_const(FR_ONE);
+  for (uint32_t j = 0; j < t; ++j) {
+    pre[j] = acc;
+    acc = fr_mul(acc, lam[j]);
+  }
+  Fr inv = fr_inv(acc);
+  for (uint32_t j = t; j-- > 0;) {
+    const Fr dj = lam[j];
+    lam[j] = fr_to_plain(fr_mul(num, fr_mul(inv, pre[j])));  // 1 / den_j = inv(all) * prefix(j)
+    inv = fr_mul(inv, dj);
+  }
+}
+
+// base-|z| digits of a plain scalar k < r: d[0..3] (g2_mul_u256_psi's split)
+DGI void rc_psi_digits(const Fr& k, uint64_t* d) {
+  uint32_t q[8];
+  for (int w = 0; w < 8; ++w) q[w] = k.l[w];
+  d[0] = u256_divmod_u64(q, Z_ABS);
+  d[1] = u256_divmod_u64(q, Z_ABS);
+  d[2] = u256_divmod_u64(q, Z_ABS);
+  d[3] = (uint64_t)q[1] << 32 | q[0];
+}
+
+// sigma = A0 - psi(A1) + psi^2(A2) - psi^3(A3), Horner in psi: psi(psi(psi(-A3) + A2) - A1) + A0
+DGI G2J rc_combine(const G2J& a0, const G2J& a1, const G2J& a2, const G2J& a3) {
+  G2J s = g2_psi(jac_neg(a3));
+  s = g2_psi(jac_add(s, a2));
+  s = g2_psi(jac_add(s, jac_neg(a1)));
+  return jac_add(s, a0);
+}
+
+// SoA table access: one affine point as RC_Q uint4 words, word q at base[q * stride]
+DGI void rc_ld(const uint4* base, size_t stride, Fp2& x, Fp2& y) {
+  uint32_t w[48];
+#pragma unroll
+  for (uint32_t q = 0; q < RC_Q; ++q) {
+    const uint4 v = base[q * stride];
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    x.c0.l[i] = w[i];
+    x.c1.l[i] = w[12 + i];
+    y.c0.l[i] = w[24 + i];
+    y.c1.l[i] = w[36 + i];
+  }
+}
+DGI void rc_st(uint4* base, size_t stride, const Fp2& x, const Fp2& y) {
+  uint32_t w[48];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    w[i] = x.c0.l[i];
+    w[12 + i] = x.c1.l[i];
+    w[24 + i] = y.c0.l[i];
+    w[36 + i] = y.c1.l[i];
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < RC_Q; ++q) base[q * stride] = uint4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+}
+
+#if defined(__HIP__) && DG_TU_LIB
+// one wave per block of 64 rounds: uni[b] = 1 if every OK round of the block selected the same index set,
+// ref[b] = the first OK round (~0u: the block has none)
+DG_KERNEL void __launch_bounds__(64) k_rc_blocks(uint32_t R, uint32_t t, const uint32_t* selidx, const uint8_t* rst,
+                                                 uint8_t* uni, uint32_t* ref) {
+  const uint32_t b = blockIdx.x, r = b * RC_BLK + threadIdx.x;
+  const bool ok = r < R && rst[r] == DG_ST_OK_;
+  const uint64_t okm = __ballot(ok);
+  if (okm == 0) {
+    if (threadIdx.x == 0) {
+      uni[b] = 1;
+      ref[b] = ~0u;
+    }
+    return;
+  }
+  const int lead = __ffsll((unsigned long long)okm) - 1;
+  bool same = true;
+  for (uint32_t j = 0; j < t; ++j) {
+    const uint32_t v = ok ? selidx[(size_t)r * t + j] : 0u;
+    same = same && (!ok || v == (uint32_t)__shfl((int)v, lead));
+  }
+  const bool all = __all(same);
+  if (threadIdx.x == 0) {
+    uni[b] = all ? 1 : 0;
+    ref[b] = b * RC_BLK + (uint32_t)lead;
+  }
+}
+
+// lane u < U (the u-th uniform block, ub[u]): lambda of its reference round, the four digit vectors and their
+// schedules ev[(u * 4 + i) * maxev ..], hdr[(u * 4 + i) * 2 + {0, 1}] = (events, tail doublings).  lam / pre:
+// t Fr of scratch per lane, naf: t x RC_NAF bytes, dig: 4 t digits.
+DG_KERNEL void __launch_bounds__(64) k_rc_digits(uint32_t U, uint32_t t, uint32_t maxev, const uint32_t* ub,
+                                                 const uint32_t* ref, const uint32_t* selidx, Fr* lam, Fr* pre,
+                                                 uint64_t* dig, int8_t* naf, uint32_t* ev, uint32_t* hdr) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  const uint32_t r = ref[ub[u]];
+  Fr* L = lam + (size_t)u * t;
+  rc_lambdas(selidx + (size_t)r * t, t, L, pre + (size_t)u * t);
+  uint64_t* D = dig + (size_t)u * 4 * t;
+  for (uint32_t j = 0; j < t; ++j) {
+    uint64_t d[4];
+    rc_psi_digits(L[j], d);
+    for (int i = 0; i < 4; ++i) D[(size_t)i * t + j] = d[i];
+  }
+  for (uint32_t i = 0; i < 4; ++i) {
+    uint32_t tail;
+    const uint32_t n = rc_schedule(D + (size_t)i * t, t, naf + (size_t)u * t * RC_NAF, ev + ((size_t)u * 4 + i) * maxev,
+                                   tail);
+    hdr[((size_t)u * 4 + i) * 2] = n;
+    hdr[((size_t)u * 4 + i) * 2 + 1] = tail;
+  }
+}
+
+// per round r of a uniform block: sigma = A0 - psi(A1) + psi^2(A2) - psi^3(A3) into out[r] (A: 4 x Ru, rounds in
+// uniform-block order); rounds without status OK are left alone (k_compress_g2 writes zeros for them)
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_rc_combine(uint32_t R, uint32_t Ru, const uint32_t* ub,
+                                                                  const uint8_t* rst, const G2JStore* A, G2JStore* out) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= Ru) return;
+  const uint32_t r = ub[u / RC_BLK] * RC_BLK + u % RC_BLK;
+  if (r >= R || rst[r] != DG_ST_OK_) return;
+  store_g2j(out[r], rc_combine(load_g2j(A[u]), load_g2j(A[(size_t)Ru + u]), load_g2j(A[2 * (size_t)Ru + u]),
+                               load_g2j(A[3 * (size_t)Ru + u])));
+}
+#endif
+
+#if defined(__HIP__) && DG_TU_HOT
+// The tables, one level per launch pair with a batch inversion between them.  Lane g < t * Ru: share j = g / Ru
+// of uniform round u = g % Ru.  Level 0: T[0] = P = S of the share, D = 2P (tangent); level l = 1..7:
+// T[l] = T[l-1] + D (chord).  P in G2 has order r, so (2l - 1)P != +-2P: no exceptional pair; an identity share
+// (possible only for an identity key) is flagged in pinf and skipped everywhere.
+DGI bool rc_lane(uint32_t g, uint32_t t, uint32_t R, uint32_t Ru, const uint32_t* ub, const uint8_t* rst,
+                 uint32_t& j, uint32_t& u, uint32_t& r) {
+  if (g >= t * Ru) return false;
+  j = g / Ru;
+  u = g % Ru;
+  r = ub[u / RC_BLK] * RC_BLK + u % RC_BLK;
+  return r < R && rst[r] == DG_ST_OK_;
+}
+DG_KERNEL void __launch_bounds__(128) k_rc_tab_den(uint32_t l, uint32_t R, uint32_t Ru, uint32_t k, uint32_t t,
+                                                   const uint32_t* ub, const uint8_t* rst, const uint32_t* sel,
+                                                   const G2AStore* S, const uint4* T4, const uint4* D4, uint8_t* pinf,
+                                                   Fp* den) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= t * Ru) return;
+  uint32_t j, u, r;
+  Fp n = fp_one();
+  if (rc_lane(g, t, R, Ru, ub, rst, j, u, r)) {
+    if (l == 0) {
+      const G2AStore& p = S[(size_t)r * k + sel[(size_t)r * t + j]];
+      pinf[g] = p.inf ? 1 : 0;
+      if (!p.inf) n = fp2_norm(fp2_dbl(p.y));
+    } else if (!pinf[g]) {
+      Fp2 tx, ty, dx, dy;
+      rc_ld(T4 + ((size_t)j * RC_TAB + (l - 1)) * RC_Q * Ru + u, Ru, tx, ty);
+      rc_ld(D4 + (size_t)j * RC_Q * Ru + u, Ru, dx, dy);
+      n = fp2_norm(fp2_sub(dx, tx));
+    }
+  }
+  den[g] = n;
+}
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_rc_tab_add(uint32_t l, uint32_t R, uint32_t Ru, uint32_t k, uint32_t t,
+                                                                 const uint32_t* ub, const uint8_t* rst,
+                                                                 const uint32_t* sel, const G2AStore* S, uint4* T4,
+                                                                 uint4* D4, const uint8_t* pinf, const Fp* ninv) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t j, u, r;
+  if (!rc_lane(g, t, R, Ru, ub, rst, j, u, r) || pinf[g]) return;
+  if (l == 0) {
+    const G2A p = load_g2a(S[(size_t)r * k + sel[(size_t)r * t + j]]);
+    rc_st(T4 + (size_t)j * RC_TAB * RC_Q * Ru + u, Ru, p.x, p.y);
+    const G2A d = g2_aff_sum(p, p, 2, ninv[g]);
+    rc_st(D4 + (size_t)j * RC_Q * Ru + u, Ru, d.x, d.y);
+  } else {
+    G2A a{}, d{};
+    rc_ld(T4 + ((size_t)j * RC_TAB + (l - 1)) * RC_Q * Ru + u, Ru, a.x, a.y);
+    rc_ld(D4 + (size_t)j * RC_Q * Ru + u, Ru, d.x, d.y);
+    a.inf = d.inf = false;
+    const G2A s = g2_aff_sum(a, d, 1, ninv[g]);
+    rc_st(T4 + ((size_t)j * RC_TAB + l) * RC_Q * Ru + u, Ru, s.x, s.y);
+  }
+}
+
+// One 64-lane workgroup per (component i, uniform block): lane = round of the block; A_i of the round by the
+// block's schedule (wave-uniform: scalar loads, uniform branches), the running point in LDS (g2_madd_lds /
+// g2_dbl_lds: the register file holds one table entry and one formula's temporaries).
+DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rc_straus(uint32_t R, uint32_t Ru, uint32_t maxev, const uint32_t* ub,
+                                                                 const uint8_t* rst, const uint32_t* ev,
+                                                                 const uint32_t* hdr, const uint4* T4,
+                                                                 const uint8_t* pinf, G2JStore* A) {
+  const uint32_t U = Ru / RC_BLK, w = blockIdx.x, i = w / U, ubk = w % U;  // uniform
+  const uint32_t u = ubk * RC_BLK + threadIdx.x, r = ub[ubk] * RC_BLK + threadIdx.x;
+  const bool live = r < R && rst[r] == DG_ST_OK_;
+  const uint32_t* e = ev + ((size_t)ubk * 4 + i) * maxev;
+  const uint32_t n = hdr[((size_t)ubk * 4 + i) * 2], tail = hdr[((size_t)ubk * 4 + i) * 2 + 1];
+  __shared__ G2JStore s_acc[RC_BLK];
+  G2JStore& acc = s_acc[threadIdx.x];
+  acc.x = fp2_zero();
+  acc.y = fp2_zero();
+  acc.z = fp2_zero();
+  for (uint32_t q = 0; q < n; ++q) {
+    const uint32_t v = e[q];
+    for (uint32_t d = rc_ev_dbl(v); d > 0; --d) g2_dbl_lds(acc);
+    const uint32_t j = rc_ev_j(v);
+    if (live && !pinf[(size_t)j * Ru + u]) {
+      Fp2 x, y;
+      rc_ld(T4 + ((size_t)j * RC_TAB + rc_ev_e(v)) * RC_Q * Ru + u, Ru, x, y);
+      g2_madd_lds(acc, x, rc_ev_neg(v) ? fp2_neg(y) : y);
+    }
+  }
+  for (uint32_t d = tail; d > 0; --d) g2_dbl_lds(acc);
+  if (live) A[(size_t)i * Ru + u] = acc;
+}
+#elif defined(__HIP__)
+DG_KERNEL void __launch_bounds__(128) k_rc_tab_den(uint32_t l, uint32_t R, uint32_t Ru, uint32_t k, uint32_t t,
+                                                   const uint32_t* ub, const uint8_t* rst, const uint32_t* sel,
+                                                   const G2AStore* S, const uint4* T4, const uint4* D4, uint8_t* pinf,
+                                                   Fp* den);
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_rc_tab_add(uint32_t l, uint32_t R, uint32_t Ru, uint32_t k, uint32_t t,
+                                                                 const uint32_t* ub, const uint8_t* rst,
+                                                                 const uint32_t* sel, const G2AStore* S, uint4* T4,
+                                                                 uint4* D4, const uint8_t* pinf, const Fp* ninv);
+DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rc_straus(uint32_t R, uint32_t Ru, uint32_t maxev, const uint32_t* ub,
+                                                                 const uint8_t* rst, const uint32_t* ev,
+                                                                 const uint32_t* hdr, const uint4* T4,
+                                                                 const uint8_t* pinf, G2JStore* A);
+#endif
+
+}  // namespace dg

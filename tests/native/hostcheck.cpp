@@ -1,9 +1,10 @@
 // Host build of the HIP kernels' device arithmetic (drand_amd/csrc/*.h) for step-by-step debugging
 // against oracle/ on CPU.  TEST TOOL ONLY: never linked into the product library.
 #include <string.h>
-#include "../../drand_amd/csrc/pairing.h"
-#include "../../drand_amd/csrc/h2c.h"
-#include "../../drand_amd/csrc/phases.h"
+
+#include <vector>
+
+#include "../../drand_amd/csrc/kernels.h"
 using namespace dg;
 extern "C" {
 void hc_fp_mul(const uint8_t* a48, const uint8_t* b48, uint8_t* out48) {
@@ -217,4 +218,76 @@ extern "C" int hc_g2_mul_lds_check(const uint8_t* sig96, const uint32_t* k8) {
   G2J acc;
   g2_mul_u256_psi_lds(a, k8, acc);
   return jac_eq(acc, g2_mul_u256_psi(a, k8)) ? 1 : 0;
+}
+
+// Recover's per-round MSM (recover.h) on the host: lambdas with one Fr inversion (rc_lambdas) against
+// lagrange_at_zero, the odd-multiple tables by the device's affine formulas (g2_aff_den / g2_aff_sum with exact
+// inverses), the four wNAF schedules and the psi combination, against sum_j g2_mul_u256_psi(S_j, lambda_j).
+// sigs: t compressed G2 points (any may be the identity), idx: t distinct share indices.  1 if equal.
+extern "C" int hc_recover_msm_check(const uint8_t* sigs96, const uint32_t* idx, uint32_t t) {
+  std::vector<Fr> lam(t), pre(t);
+  rc_lambdas(idx, t, lam.data(), pre.data());
+  std::vector<G2A> P(t);
+  G2J want = jac_infinity<Fp2>();
+  for (uint32_t j = 0; j < t; ++j) {
+    if (!g2_decompress(P[j], sigs96 + 96 * j, false)) return -1;
+    const Fr l = lagrange_at_zero(idx, t, j);
+    for (int w = 0; w < 8; ++w)
+      if (l.l[w] != lam[j].l[w]) return 0;
+    want = jac_add(want, g2_mul_u256_psi(P[j], lam[j].l));
+  }
+  // tables: T[j][0] = P, D = 2P (tangent), T[j][e] = T[j][e-1] + D (chord)
+  std::vector<G2A> T((size_t)t * RC_TAB);
+  for (uint32_t j = 0; j < t; ++j) {
+    if (P[j].inf) continue;
+    const G2A d = g2_aff_sum(P[j], P[j], 2, fp_inv(g2_aff_den(P[j], P[j], 2)));
+    T[(size_t)j * RC_TAB] = P[j];
+    for (uint32_t e = 1; e < RC_TAB; ++e) {
+      const G2A& a = T[(size_t)j * RC_TAB + e - 1];
+      T[(size_t)j * RC_TAB + e] = g2_aff_sum(a, d, 1, fp_inv(g2_aff_den(a, d, 1)));
+    }
+  }
+  std::vector<uint64_t> dig((size_t)4 * t);
+  for (uint32_t j = 0; j < t; ++j) {
+    uint64_t d[4];
+    rc_psi_digits(lam[j], d);
+    for (int i = 0; i < 4; ++i) dig[(size_t)i * t + j] = d[i];
+  }
+  std::vector<int8_t> naf((size_t)t * RC_NAF);
+  std::vector<uint32_t> ev((size_t)t * RC_EV_PER_SHARE);
+  G2J A[4];
+  for (int i = 0; i < 4; ++i) {
+    uint32_t tail;
+    const uint32_t n = rc_schedule(dig.data() + (size_t)i * t, t, naf.data(), ev.data(), tail);
+    if (n > t * RC_EV_PER_SHARE) return 0;
+    G2JStore acc{fp2_zero(), fp2_zero(), fp2_zero()};
+    for (uint32_t q = 0; q < n; ++q) {
+      const uint32_t v = ev[q];
+      for (uint32_t d = rc_ev_dbl(v); d > 0; --d) g2_dbl_lds(acc);
+      const uint32_t j = rc_ev_j(v);
+      if (P[j].inf) continue;
+      const G2A& e = T[(size_t)j * RC_TAB + rc_ev_e(v)];
+      g2_madd_lds(acc, e.x, rc_ev_neg(v) ? fp2_neg(e.y) : e.y);
+    }
+    for (uint32_t d = tail; d > 0; --d) g2_dbl_lds(acc);
+    A[i] = G2J{acc.x, acc.y, acc.z};
+  }
+  return jac_eq(rc_combine(A[0], A[1], A[2], A[3]), want) ? 1 : 0;
+}
+
+// the width-5 signed digits of a 64-bit scalar evaluate back to it and keep their spacing; 1 if so
+extern "C" int hc_wnaf_check(uint64_t d) {
+  int8_t naf[RC_NAF];
+  rc_wnaf(d, naf);
+  unsigned __int128 v = 0;
+  int last = -100;
+  for (int b = (int)RC_NAF - 1; b >= 0; --b) {
+    v = v * 2 + (__int128)naf[b];
+    if (naf[b]) {
+      if ((naf[b] & 1) == 0 || naf[b] > 15 || naf[b] < -15) return 0;
+      if (last - b < (int)RC_W && last >= 0) return 0;
+      last = b;
+    }
+  }
+  return v == (unsigned __int128)d ? 1 : 0;
 }

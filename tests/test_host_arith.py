@@ -193,3 +193,29 @@ def test_affine_pair_addition_matches_jacobian(hc):
     for i in range(len(sigs) - 1):
         for mode in range(6):
             assert hc.hc_aff_add_check(sigs[i], sigs[i + 1], mode) == 1, (i, mode)
+
+
+def test_wnaf_digits_host_build(hc):
+    """recover.h rc_wnaf: width-5 signed digits (odd, |d| <= 15, >= 5 apart) that evaluate back to the scalar,
+    including the 65th position a carry can reach."""
+    rng = random.Random(11)
+    vals = [0, 1, 15, 16, 17, 31, (1 << 63) - 1, 1 << 63, 0xd201000000010000 - 1, (1 << 64) - 1]
+    vals += [rng.getrandbits(64) for _ in range(500)]
+    for d in vals:
+        assert hc.hc_wnaf_check(ctypes.c_uint64(d)) == 1, hex(d)
+
+
+@pytest.mark.parametrize("t,seed", [(1, 0), (3, 1), (33, 2), (33, 3), (12, 4)])
+def test_recover_msm_host_build(hc, t, seed):
+    """recover.h on the host: one Straus MSM per round over the t selected shares (lambdas with one Fr inversion,
+    affine odd-multiple tables, four psi-component wNAF schedules, psi combination) equals the sum of the
+    per-share products lambda_j S_j (g2_mul_u256_psi), and the lambdas equal lagrange_at_zero's; shares are
+    signatures of the committed chain, one of them the identity when t > 3."""
+    rounds = load("chain_t3n5.json")["rounds"]
+    rng = random.Random(seed)
+    sigs = [hx(rounds[rng.randrange(len(rounds))]["sig"]) for _ in range(t)]
+    if t > 3:
+        sigs[2] = bytes([0xc0]) + bytes(95)  # the identity (a share whose key is the identity)
+    idx = sorted(rng.sample(range(300), t))
+    arr = (ctypes.c_uint32 * t)(*idx)
+    assert hc.hc_recover_msm_check(b"".join(sigs), arr, t) == 1

@@ -7,6 +7,7 @@
 //   2  the compiler's own form of (uint64_t)a * b + acc (what fp28.h compiles to)
 //   3  v_mad_u32_u24 (24-bit operands, 32-bit result: the alternative limb form SURVEY.md §7 asked about)
 //   4  v_mul_lo_u32,  5  v_mul_hi_u32 (the two halves of a 32 x 32 -> 64 product done separately)
+//   6  v_add_u32, 7 v_fma_f32 (full-rate calibration: the issue rate of the probe's own structure)
 // Each workgroup stamps s_memtime / s_memrealtime (scalar counter reads) around its loop, so the clock the
 // chip held during the measured launches is known (MI355X_MICROARCH.md 'DVFS give-back' item 6): the
 // in-kernel clock is the median over workgroups of d(memtime) / d(realtime) x 100 MHz.  The rate is timed
@@ -46,8 +47,12 @@ __global__ void __launch_bounds__(256) k_probe(uint64_t* out, uint64_t* clk, uin
         asm volatile("v_mad_u32_u24 %0, %0, %1, %0" : "+v"(acc32[c]) : "v"(b));
       else if (KIND == 4)
         asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(acc32[c]) : "v"(b));
-      else
+      else if (KIND == 5)
         asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(acc32[c]) : "v"(b));
+      else if (KIND == 6)
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(acc32[c]) : "v"(b));
+      else
+        asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(acc32[c]) : "v"(b));
     }
     if (KIND == 2) asm volatile("" : "+v"(a));  // opaque per iteration: the chains cannot be folded into one product
   }
@@ -71,7 +76,9 @@ static ProbeFn probe_fn(int kind) {
     case 2: return k_probe<2>;
     case 3: return k_probe<3>;
     case 4: return k_probe<4>;
-    default: return k_probe<5>;
+    case 5: return k_probe<5>;
+    case 6: return k_probe<6>;
+    default: return k_probe<7>;
   }
 }
 
