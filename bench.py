@@ -317,8 +317,9 @@ def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps
     tbls.recover_batch_dev(pub, d_msgs, d_parts, t, n, seed=9)
     kt = L.timings()
     L.check(L.lib().dg_set_timing(0))
-    units = {"k_decode_items": R * n, "k_recover_terms": R * t, "k_recover_terms_u": R * t, "k_h2c_uncleared": R, "k_exp_pm3d4": 4 * R + 2 * R * n,
-             "k_dec_p1": R * n, "k_dec_p2": R * n, "k_dec_p3": R * n}
+    # k_rc_straus: one unit = one round (its four psi-component lanes), priced at the C3 index set 0..32
+    units = {"k_decode_items": R * n, "k_recover_terms": R * t, "k_rc_straus": R, "k_h2c_uncleared": R,
+             "k_exp_pm3d4": 4 * R + 2 * R * n, "k_dec_p1": R * n, "k_dec_p2": R * n, "k_dec_p3": R * n}
     roof = roofline_of(kt, units, peak, {"timing": "HIP events on the launch stream, one dg_recover call"}, "c3")
     out = {"metric": "Recover/s at n=%d t=%d (all %d shares VerifyPartial'd, first t valid interpolated)" % (n, t, n),
            "value": R_total / (dt + gdt), "unit": "recovers/s", "n_gpus": world, "rounds": R_total,

@@ -56,6 +56,7 @@ struct Set {
   std::vector<void*> pool;  // indexed by Slot
   std::vector<size_t> pool_size;
   hipEvent_t done = nullptr;
+  hipEvent_t to_fb = nullptr, from_fb = nullptr;  // hand-over to / back from the per-item stream
   bool busy = false;
 };
 
@@ -63,6 +64,12 @@ struct Ctx {
   int device = -1;
   bool ready = false;
   Set sets[kSets];
+  // The per-item pairing kernels (k_verify_items, k_verify_groups: ~14.5 KB of private segment per lane) run on
+  // this one stream, whatever set the batch uses: a hardware queue reserves scratch for the largest private
+  // segment dispatched on it, so only this stream's queue holds that reservation and the workspace sets'
+  // queues stay at the ~8.5 KB of k_recover_terms (with 8 hardware queues, every queue holding 14.5 KB failed
+  // with HSA_STATUS_ERROR_OUT_OF_RESOURCES).  Only failed or isolating batches reach it.
+  hipStream_t fb_stream = nullptr;
   int cur = 0, next = 0;
   bool timing = false;
   std::vector<Timing> timings;
@@ -130,8 +137,8 @@ enum Slot {
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
   S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_BINV, S_NV, S_NVINV,
-  S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_BINV_PRE, S_BINV_ROOTS, S_RC_UNI, S_RC_REF, S_RC_LAM,
-  S_RC_DIG, S_RC_NAF, S_RC_EV, S_RC_TAB, S_RC_D, S_RC_PINF, S_RC_DEN, S_RC_A, S_COUNT
+  S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_BINV_PRE, S_BINV_ROOTS, S_RC_UNI, S_RC_REF,
+  S_RC_NAF, S_RC_EV, S_RC_TAB, S_RC_D, S_RC_PINF, S_RC_DEN, S_RC_A, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -557,6 +564,12 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
   G2AStore* H;
   RET(wsT(S_H, b.R, &H));
   RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, (const uint32_t*)flag, b.Q, H));
+  // the per-item pass on the per-item stream (g_ctx.fb_stream), ordered after and before this set's stream
+  Set& set = cur_set();
+  const hipStream_t batch_st = st;
+  HIPCHK(hipEventRecord(set.to_fb, batch_st));
+  st = g_ctx.fb_stream;
+  HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
   if (b.prefix_t == 0) {
     RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
                (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status, batched_sub));
@@ -586,6 +599,9 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
                  b.item_slot, (const G2AStore*)H, (const G2AStore*)b.S, b.status, fin, batched_sub, g_ctx.gcount));
     }
   }
+  HIPCHK(hipEventRecord(set.from_fb, st));
+  st = batch_st;
+  HIPCHK(hipStreamWaitEvent(st, set.from_fb, 0));
   RET(launch("k_count_fallback", k_count_fallback, 1, 64, st, (const uint32_t*)flag, g_ctx.fallbacks));
   return 0;
 }
@@ -861,18 +877,13 @@ int recover_msm(uint32_t R, uint32_t k, uint32_t t, uint32_t U, const uint32_t* 
   const uint32_t Ru = U * RC_BLK, maxev = t * RC_EV_PER_SHARE;
   const size_t nel = (size_t)t * Ru;
   if (nel > 0x7fffffffull) return fail(DG_E_ARG, "Recover batch too large for the MSM tables");
-  Fr *lam, *pre;
-  uint64_t* dig;
   int8_t* naf;
   uint32_t *ev, *hdr;
   uint4 *T4, *D4;
   uint8_t* pinf;
   Fp *den, *dinv;
   G2JStore* A;
-  RET(wsT(S_RC_LAM, (size_t)2 * U * t, &lam));
-  pre = lam + (size_t)U * t;
-  RET(wsT(S_RC_DIG, (size_t)4 * U * t, &dig));
-  RET(wsT(S_RC_NAF, (size_t)U * t * RC_NAF, &naf));
+  RET(wsT(S_RC_NAF, (size_t)4 * U * t * RC_NAF, &naf));
   RET(wsT(S_RC_EV, (size_t)4 * U * maxev + (size_t)8 * U, &ev));
   hdr = ev + (size_t)4 * U * maxev;
   RET(wsT(S_RC_TAB, nel * RC_TAB * RC_Q, &T4));
@@ -881,7 +892,7 @@ int recover_msm(uint32_t R, uint32_t k, uint32_t t, uint32_t U, const uint32_t* 
   RET(wsT(S_RC_DEN, 2 * nel, &den));
   dinv = den + nel;
   RET(wsT(S_RC_A, (size_t)4 * Ru, &A));
-  RET(launch("k_rc_digits", k_rc_digits, U, 64, st, U, t, maxev, ub, ref, d_selidx, lam, pre, dig, naf, ev, hdr));
+  RET(launch("k_rc_digits", k_rc_digits, U * RC_BLK, RC_BLK, st, U, t, maxev, ub, ref, d_selidx, naf, ev, hdr));
   for (uint32_t l = 0; l < RC_TAB; ++l) {
     RET(launch("k_rc_tab_den", k_rc_tab_den, (uint32_t)nel, 128, st, l, R, Ru, k, t, ub, d_rst, d_sel, d_S,
                (const uint4*)T4, (const uint4*)D4, pinf, den));
@@ -968,7 +979,10 @@ int dg_init(int device) {
   for (Set& x : g_ctx.sets) {
     if (!x.stream) HIPCHK(hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking));
     if (!x.done) HIPCHK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
+    if (!x.to_fb) HIPCHK(hipEventCreateWithFlags(&x.to_fb, hipEventDisableTiming));
+    if (!x.from_fb) HIPCHK(hipEventCreateWithFlags(&x.from_fb, hipEventDisableTiming));
   }
+  if (!g_ctx.fb_stream) HIPCHK(hipStreamCreateWithFlags(&g_ctx.fb_stream, hipStreamNonBlocking));
   if (!g_ctx.fallbacks) {
     HIPCHK(hipMalloc(&g_ctx.fallbacks, sizeof(unsigned long long)));
     HIPCHK(hipMemset(g_ctx.fallbacks, 0, sizeof(unsigned long long)));
@@ -979,29 +993,35 @@ int dg_init(int device) {
   }
   // A hardware queue's scratch (private segment) grows on the first dispatch that needs more.  On MI355X
   // that growth, when it first happened inside an overlapped batch (the per-item kernels: ~14 KB per
-  // lane), stalled every queue for ~0.5 s (rocprofv3 trace).  Dispatch the largest-scratch kernels once per
-  // workspace stream here, with zero items (every lane returns at once), so the growth happens now -- the
-  // largest first: a dispatch that needs a larger private segment than the queue's current one, right
-  // behind it, failed with HSA_STATUS_ERROR_OUT_OF_RESOURCES on the box.
-  // (largest first, by the private segment sizes of the code objects)
+  // lane), stalled every queue for ~0.5 s (rocprofv3 trace).  Dispatch the largest-scratch kernels once here,
+  // with zero items (every lane returns at once), so the growth happens now -- the largest first: a dispatch
+  // that needs a larger private segment than the queue's current one, right behind it, failed with
+  // HSA_STATUS_ERROR_OUT_OF_RESOURCES on the box.  The per-item kernels go to the per-item stream only; every
+  // workspace stream gets k_recover_terms, the largest private segment of the kernels that run there
+  // (tests/test_abi.py checks both orderings against the code-object metadata).
   hipFuncAttributes fa_items{}, fa_groups{};
   HIPCHK(hipFuncGetAttributes(&fa_items, reinterpret_cast<const void*>(k_verify_items)));
   HIPCHK(hipFuncGetAttributes(&fa_groups, reinterpret_cast<const void*>(k_verify_groups)));
   const bool items_first = fa_items.localSizeBytes > fa_groups.localSizeBytes;
-  for (Set& x : g_ctx.sets) {
-    for (int pass = 0; pass < 2; ++pass) {
-      if ((pass == 0) == items_first) {
-        hipLaunchKernelGGL(k_verify_items, dim3(1), dim3(64), 0, x.stream, 0u, 1u, (const uint32_t*)nullptr,
-                           (const G1AStore*)nullptr, (const uint32_t*)nullptr, (const G2AStore*)nullptr,
-                           (const G2AStore*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, 0u);
-      } else {
-        // glist[0] = 0 (the zeroed fallback counter): no groups
-        hipLaunchKernelGGL(k_verify_groups, dim3(1), dim3(64), 0, x.stream, 1u, (const uint32_t*)g_ctx.fallbacks,
-                           (const uint64_t*)nullptr, (const G1AStore*)nullptr, (const uint32_t*)nullptr,
-                           (const G2AStore*)nullptr, (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr,
-                           0u, g_ctx.gcount);
-      }
+  for (int pass = 0; pass < 2; ++pass) {
+    if ((pass == 0) == items_first) {
+      hipLaunchKernelGGL(k_verify_items, dim3(1), dim3(64), 0, g_ctx.fb_stream, 0u, 1u, (const uint32_t*)nullptr,
+                         (const G1AStore*)nullptr, (const uint32_t*)nullptr, (const G2AStore*)nullptr,
+                         (const G2AStore*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, 0u);
+    } else {
+      // glist[0] = 0 (the zeroed fallback counter): no groups
+      hipLaunchKernelGGL(k_verify_groups, dim3(1), dim3(64), 0, g_ctx.fb_stream, 1u, (const uint32_t*)g_ctx.fallbacks,
+                         (const uint64_t*)nullptr, (const G1AStore*)nullptr, (const uint32_t*)nullptr,
+                         (const G2AStore*)nullptr, (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr,
+                         0u, g_ctx.gcount);
     }
+  }
+  HIPCHK(hipGetLastError());
+  for (Set& x : g_ctx.sets) {
+    // t = 0: every lane returns (m >= t)
+    hipLaunchKernelGGL(k_recover_terms, dim3(1), dim3(64), 0, x.stream, 0u, 64u, 1u, 0u, (const uint32_t*)nullptr,
+                       (const uint32_t*)nullptr, (const uint8_t*)nullptr, (const uint8_t*)nullptr,
+                       (const G2AStore*)nullptr, (G2JStore*)nullptr);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipDeviceSynchronize());
@@ -1022,8 +1042,16 @@ void dg_shutdown(void) {
     x.busy = false;
     if (x.stream) (void)hipStreamDestroy(x.stream);
     if (x.done) (void)hipEventDestroy(x.done);
+    if (x.to_fb) (void)hipEventDestroy(x.to_fb);
+    if (x.from_fb) (void)hipEventDestroy(x.from_fb);
     x.stream = nullptr;
     x.done = nullptr;
+    x.to_fb = x.from_fb = nullptr;
+  }
+  if (g_ctx.fb_stream) {
+    (void)hipStreamSynchronize(g_ctx.fb_stream);
+    (void)hipStreamDestroy(g_ctx.fb_stream);
+    g_ctx.fb_stream = nullptr;
   }
   if (g_ctx.pk_dev) (void)hipFree(g_ctx.pk_dev);
   if (g_ctx.pk_status) (void)hipFree(g_ctx.pk_status);

@@ -72,10 +72,10 @@ DGI void rc_wnaf(uint64_t d, int8_t* naf) {
   }
 }
 
-// The schedule of sum_j [d_j] P_j (Horner over the digit positions, top down; within a position by share):
-// events ev[0..n), and `tail` doublings after the last one.  naf: t x RC_NAF scratch.
-DGI uint32_t rc_schedule(const uint64_t* d, uint32_t t, int8_t* naf, uint32_t* ev, uint32_t& tail) {
-  for (uint32_t j = 0; j < t; ++j) rc_wnaf(d[j], naf + (size_t)RC_NAF * j);
+// The schedule of sum_j [d_j] P_j from the signed digits naf[j * RC_NAF + b] (Horner over the positions, top down;
+// within a position by share): events ev[0..n), and `tail` doublings after the last one.  (k_rc_digits builds
+// the same list with one lane per share and ballots.)
+DGI uint32_t rc_schedule_naf(const int8_t* naf, uint32_t t, uint32_t* ev, uint32_t& tail) {
   uint32_t n = 0;
   int last = -1;
   for (int b = (int)RC_NAF - 1; b >= 0; --b)
@@ -88,6 +88,22 @@ DGI uint32_t rc_schedule(const uint64_t* d, uint32_t t, int8_t* naf, uint32_t* e
     }
   tail = last < 0 ? 0u : (uint32_t)last;
   return n;
+}
+
+// (r - 1) / 2, little-endian limbs
+DG_CONST uint32_t FR_HALF[8] = {0x80000000u, 0x7fffffffu, 0x7fff2dffu, 0xa9ded201u,
+                                0x04d0ec02u, 0x199cec04u, 0x94cebea4u, 0x39f6d3a9u};
+// Signed scalar: a plain k > (r - 1) / 2 is replaced by r - k and the share's point negated ([k]P = [r - k](-P)).
+// For random k no gain; Lagrange coefficients of a run of consecutive indices are binomials +-C(t, j) (x_m = 1..t),
+// whose negative half is r - C: as r - k they are small, and their digits d1..d3 vanish.  Returns the negation.
+DGI bool rc_signed(Fr& k) {
+  uint32_t br = 0;
+  for (int i = 0; i < 8; ++i) (void)subb32(FR_HALF[i], k.l[i], br, &br);
+  if (!br) return false;  // k <= (r - 1) / 2
+  Fr z;
+  for (int i = 0; i < 8; ++i) z.l[i] = 0;
+  k = fr_sub(z, k);  // r - k (plain in, plain out: the subtraction is representation-free)
+  return true;
 }
 
 // lambda_j (plain, 8 little-endian limbs) for j < t over the interpolation points x_m = idx[m] + 1 (kyber
@@ -194,29 +210,65 @@ DG_KERNEL void __launch_bounds__(64) k_rc_blocks(uint32_t R, uint32_t t, const u
   }
 }
 
-// lane u < U (the u-th uniform block, ub[u]): lambda of its reference round, the four digit vectors and their
-// schedules ev[(u * 4 + i) * maxev ..], hdr[(u * 4 + i) * 2 + {0, 1}] = (events, tail doublings).  lam / pre:
-// t Fr of scratch per lane, naf: t x RC_NAF bytes, dig: 4 t digits.
+// One 64-lane workgroup per uniform block u (ub[u]), lanes over the shares j (t > 64: in chunks of 64): lambda_j
+// of the block's reference round (each lane inverts its own denominator), signed (rc_signed), its base-|z| digits
+// and their width-5 signed digits (naf: per (u, component, j) RC_NAF bytes of scratch, negated for a negated
+// share); then per component the schedule, position-major and by share within a position, by one ballot per
+// (position, chunk): ev[(u * 4 + i) * maxev ..], hdr[(u * 4 + i) * 2 + {0, 1}] = (events, tail doublings).
 DG_KERNEL void __launch_bounds__(64) k_rc_digits(uint32_t U, uint32_t t, uint32_t maxev, const uint32_t* ub,
-                                                 const uint32_t* ref, const uint32_t* selidx, Fr* lam, Fr* pre,
-                                                 uint64_t* dig, int8_t* naf, uint32_t* ev, uint32_t* hdr) {
-  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+                                                 const uint32_t* ref, const uint32_t* selidx, int8_t* naf, uint32_t* ev,
+                                                 uint32_t* hdr) {
+  const uint32_t u = blockIdx.x, lane = threadIdx.x;
   if (u >= U) return;
-  const uint32_t r = ref[ub[u]];
-  Fr* L = lam + (size_t)u * t;
-  rc_lambdas(selidx + (size_t)r * t, t, L, pre + (size_t)u * t);
-  uint64_t* D = dig + (size_t)u * 4 * t;
-  for (uint32_t j = 0; j < t; ++j) {
+  const uint32_t* idx = selidx + (size_t)ref[ub[u]] * t;
+  Fr num = fr_const(FR_ONE);
+  for (uint32_t m = 0; m < t; ++m) num = fr_mul(num, fr_from_u32(idx[m] + 1));
+  for (uint32_t j = lane; j < t; j += RC_BLK) {
+    const Fr xj = fr_from_u32(idx[j] + 1);
+    Fr den = xj;
+    for (uint32_t m = 0; m < t; ++m)
+      if (m != j) den = fr_mul(den, fr_sub(fr_from_u32(idx[m] + 1), xj));
+    Fr lam = fr_to_plain(fr_mul(num, fr_inv(den)));
+    const bool neg = rc_signed(lam);
     uint64_t d[4];
-    rc_psi_digits(L[j], d);
-    for (int i = 0; i < 4; ++i) D[(size_t)i * t + j] = d[i];
+    rc_psi_digits(lam, d);
+    for (uint32_t i = 0; i < 4; ++i) {
+      int8_t* z = naf + (((size_t)u * 4 + i) * t + j) * RC_NAF;
+      rc_wnaf(d[i], z);
+      if (neg)
+        for (uint32_t b = 0; b < RC_NAF; ++b) z[b] = (int8_t)-z[b];
+    }
   }
+  __syncthreads();  // (the naf bytes are read back by other lanes: global memory, same workgroup)
+  __threadfence_block();
+  const uint64_t below = (1ull << lane) - 1;
   for (uint32_t i = 0; i < 4; ++i) {
-    uint32_t tail;
-    const uint32_t n = rc_schedule(D + (size_t)i * t, t, naf + (size_t)u * t * RC_NAF, ev + ((size_t)u * 4 + i) * maxev,
-                                   tail);
-    hdr[((size_t)u * 4 + i) * 2] = n;
-    hdr[((size_t)u * 4 + i) * 2 + 1] = tail;
+    const int8_t* zi = naf + ((size_t)u * 4 + i) * t * RC_NAF;
+    uint32_t* e = ev + ((size_t)u * 4 + i) * maxev;
+    uint32_t n = 0;
+    int last = -1;
+    for (int b = (int)RC_NAF - 1; b >= 0; --b) {
+      bool first = true;  // the first event at this position carries the doublings since the previous one
+      for (uint32_t c = 0; c < t; c += RC_BLK) {
+        const uint32_t j = c + lane;
+        const int z = j < t ? zi[(size_t)j * RC_NAF + b] : 0;
+        const uint64_t mask = __ballot(z != 0);
+        if (!mask) continue;
+        if (z) {
+          const uint32_t pos = n + (uint32_t)__popcll(mask & below);
+          const bool lead = first && (mask & below) == 0;
+          const uint32_t a = (uint32_t)(z < 0 ? -z : z);
+          e[pos] = rc_event(j, (a - 1) / 2, z < 0 ? 1u : 0u, lead && last >= 0 ? (uint32_t)(last - b) : 0u);
+        }
+        n += (uint32_t)__popcll(mask);
+        first = false;
+        last = b;
+      }
+    }
+    if (lane == 0) {
+      hdr[((size_t)u * 4 + i) * 2] = n;
+      hdr[((size_t)u * 4 + i) * 2 + 1] = last < 0 ? 0u : (uint32_t)last;
+    }
   }
 }
 

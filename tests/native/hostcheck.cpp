@@ -247,18 +247,25 @@ extern "C" int hc_recover_msm_check(const uint8_t* sigs96, const uint32_t* idx, 
       T[(size_t)j * RC_TAB + e] = g2_aff_sum(a, d, 1, fp_inv(g2_aff_den(a, d, 1)));
     }
   }
-  std::vector<uint64_t> dig((size_t)4 * t);
+  // signed scalars (rc_signed), their digits, and the per-component signed digits (negated for a negated share)
+  std::vector<int8_t> naf((size_t)4 * t * RC_NAF);
   for (uint32_t j = 0; j < t; ++j) {
+    Fr l = lam[j];
+    const bool neg = rc_signed(l);
     uint64_t d[4];
-    rc_psi_digits(lam[j], d);
-    for (int i = 0; i < 4; ++i) dig[(size_t)i * t + j] = d[i];
+    rc_psi_digits(l, d);
+    for (int i = 0; i < 4; ++i) {
+      int8_t* z = naf.data() + ((size_t)i * t + j) * RC_NAF;
+      rc_wnaf(d[i], z);
+      if (neg)
+        for (uint32_t b = 0; b < RC_NAF; ++b) z[b] = (int8_t)-z[b];
+    }
   }
-  std::vector<int8_t> naf((size_t)t * RC_NAF);
   std::vector<uint32_t> ev((size_t)t * RC_EV_PER_SHARE);
   G2J A[4];
   for (int i = 0; i < 4; ++i) {
     uint32_t tail;
-    const uint32_t n = rc_schedule(dig.data() + (size_t)i * t, t, naf.data(), ev.data(), tail);
+    const uint32_t n = rc_schedule_naf(naf.data() + (size_t)i * t * RC_NAF, t, ev.data(), tail);
     if (n > t * RC_EV_PER_SHARE) return 0;
     G2JStore acc{fp2_zero(), fp2_zero(), fp2_zero()};
     for (uint32_t q = 0; q < n; ++q) {

@@ -205,17 +205,18 @@ def test_wnaf_digits_host_build(hc):
         assert hc.hc_wnaf_check(ctypes.c_uint64(d)) == 1, hex(d)
 
 
-@pytest.mark.parametrize("t,seed", [(1, 0), (3, 1), (33, 2), (33, 3), (12, 4)])
+@pytest.mark.parametrize("t,seed", [(1, 0), (3, 1), (33, 2), (33, 3), (12, 4), (33, -1), (70, -1)])
 def test_recover_msm_host_build(hc, t, seed):
     """recover.h on the host: one Straus MSM per round over the t selected shares (lambdas with one Fr inversion,
     affine odd-multiple tables, four psi-component wNAF schedules, psi combination) equals the sum of the
     per-share products lambda_j S_j (g2_mul_u256_psi), and the lambdas equal lagrange_at_zero's; shares are
     signatures of the committed chain, one of them the identity when t > 3."""
     rounds = load("chain_t3n5.json")["rounds"]
-    rng = random.Random(seed)
+    rng = random.Random(seed + 100)
     sigs = [hx(rounds[rng.randrange(len(rounds))]["sig"]) for _ in range(t)]
     if t > 3:
         sigs[2] = bytes([0xc0]) + bytes(95)  # the identity (a share whose key is the identity)
-    idx = sorted(rng.sample(range(300), t))
+    # seed -1: the indices 0..t-1 (lambda = +-binomials: the signed digits of the negative ones are small)
+    idx = list(range(t)) if seed < 0 else sorted(rng.sample(range(300), t))
     arr = (ctypes.c_uint32 * t)(*idx)
     assert hc.hc_recover_msm_check(b"".join(sigs), arr, t) == 1

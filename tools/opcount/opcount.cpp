@@ -4,6 +4,8 @@
 // Tooling only -- never linked into the product library.
 #include <string.h>
 
+#include <vector>
+
 #include "../../drand_amd/csrc/kernels.h"
 
 namespace dg {
@@ -246,4 +248,62 @@ extern "C" void oc_verify_group(const uint8_t* pk48s, const uint8_t* msg, const 
   bool ok = fp12_is_one(final_exp_cubed(miller_loop<2>(P, Q, 2)));
   (void)ok;
   take(out);
+}
+
+// Recover's per-round MSM (recover.h) for one round of t shares with index set idx: out[0..2] the odd-multiple
+// tables (per share 1 tangent + 7 chord affine additions; the batch inversion's share counted as its 3 products
+// per value, the inversion itself not), out[3..5] the four Straus components (k_rc_straus), out[6..8] the psi
+// combination (k_rc_combine).
+extern "C" void oc_recover_msm(const uint8_t* sigs96, const uint32_t* idx, uint32_t t, uint64_t* out) {
+  std::vector<Fr> lam(t), pre(t);
+  rc_lambdas(idx, t, lam.data(), pre.data());
+  std::vector<G2A> P(t), T((size_t)t * RC_TAB);
+  for (uint32_t j = 0; j < t; ++j) g2_decompress(P[j], sigs96 + 96 * j, false);
+  reset();
+  for (uint32_t j = 0; j < t; ++j) {
+    Fp n = g2_aff_den(P[j], P[j], 2);
+    g_fp_mul_count += 3;
+    const G2A d = g2_aff_sum(P[j], P[j], 2, n);  // (the value of nv does not change the count)
+    T[(size_t)j * RC_TAB] = P[j];
+    for (uint32_t e = 1; e < RC_TAB; ++e) {
+      const G2A& a = T[(size_t)j * RC_TAB + e - 1];
+      n = g2_aff_den(a, d, 1);
+      g_fp_mul_count += 3;
+      T[(size_t)j * RC_TAB + e] = g2_aff_sum(a, d, 1, n);
+    }
+  }
+  take(out);
+  std::vector<int8_t> naf((size_t)4 * t * RC_NAF);
+  for (uint32_t j = 0; j < t; ++j) {
+    Fr l = lam[j];
+    const bool neg = rc_signed(l);
+    uint64_t d[4];
+    rc_psi_digits(l, d);
+    for (int i = 0; i < 4; ++i) {
+      int8_t* z = naf.data() + ((size_t)i * t + j) * RC_NAF;
+      rc_wnaf(d[i], z);
+      if (neg)
+        for (uint32_t b = 0; b < RC_NAF; ++b) z[b] = (int8_t)-z[b];
+    }
+  }
+  std::vector<uint32_t> ev((size_t)t * RC_EV_PER_SHARE);
+  G2J A[4];
+  reset();
+  for (int i = 0; i < 4; ++i) {
+    uint32_t tail;
+    const uint32_t n = rc_schedule_naf(naf.data() + (size_t)i * t * RC_NAF, t, ev.data(), tail);
+    G2JStore acc{fp2_zero(), fp2_zero(), fp2_zero()};
+    for (uint32_t q = 0; q < n; ++q) {
+      const uint32_t v = ev[q];
+      for (uint32_t d = rc_ev_dbl(v); d > 0; --d) g2_dbl_lds(acc);
+      const G2A& e = T[(size_t)rc_ev_j(v) * RC_TAB + rc_ev_e(v)];
+      g2_madd_lds(acc, e.x, rc_ev_neg(v) ? fp2_neg(e.y) : e.y);
+    }
+    for (uint32_t d = tail; d > 0; --d) g2_dbl_lds(acc);
+    A[i] = G2J{acc.x, acc.y, acc.z};
+  }
+  take(out + 3);
+  reset();
+  (void)rc_combine(A[0], A[1], A[2], A[3]);
+  take(out + 6);
 }

@@ -10,6 +10,7 @@ import ctypes
 import hashlib
 import json
 import os
+import random
 import subprocess
 import sys
 
@@ -83,6 +84,16 @@ def main():
                 add("k_verify_groups[%d]" % m)
             L.oc_batch_final(pk, sig, nxt, o)
             add("k_pair_miller+k_final_check")
+    # Recover's per-round MSM at n = 64, t = 33: the C3 index set (0..32: every share valid, input order) and a
+    # random set of 33 of 64 (lambda without structure); per round
+    rng = random.Random(5)
+    sig33 = b"".join(bytes.fromhex(rounds[q % len(rounds)]["sig"]) for q in range(33))
+    for name, idx in (("", list(range(33))), ("[random set]", sorted(rng.sample(range(64), 33)))):
+        rc = (ctypes.c_uint64 * 9)()
+        L.oc_recover_msm(sig33, (ctypes.c_uint32 * 33)(*idx), 33, rc)
+        for q, kname in ((0, "k_rc_tables"), (1, "k_rc_straus"), (2, "k_rc_combine")):
+            o[0], o[1], o[2] = rc[3 * q], rc[3 * q + 1], rc[3 * q + 2]
+            add(kname + name)
     out = {"mac_per_mul": MAC_MUL, "mac_per_sqr": MAC_SQR, "mac_per_inv": MAC_INV, "vmad_per_mul": VMAD_MUL,
            "vmad_per_sqr": VMAD_SQR, "basis": "BASELINE.md: 300 multiply-adds per Montgomery product M",
            "sample": "tests/golden/chain_t3n5.json (64 rounds)", "per_unit": {}}
@@ -91,7 +102,6 @@ def main():
                               "macs": (m * MAC_MUL + s * MAC_SQR + v * MAC_INV) / n,
                               "vmad": (m * VMAD_MUL + s * VMAD_SQR + v * MAC_INV) / n}
     out["per_unit"]["k_key_accum"] = out["per_unit"]["k_sum_rows"]
-    out["per_unit"]["k_recover_terms_u"] = out["per_unit"]["k_recover_terms"]  # the same Straus, LDS running point
     with open(os.path.join(ROOT, "profiles", "opcounts.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     for k, v in sorted(out["per_unit"].items()):
