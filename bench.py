@@ -318,7 +318,7 @@ def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps
     kt = L.timings()
     L.check(L.lib().dg_set_timing(0))
     # k_rc_straus: one unit = one round (its four psi-component lanes), priced at the C3 index set 0..32
-    units = {"k_decode_items": R * n, "k_recover_terms": R * t, "k_rc_straus": R, "k_h2c_uncleared": R,
+    units = {"k_decode_items": R * n, "k_rc_straus": R, "k_h2c_uncleared": R,
              "k_exp_pm3d4": 4 * R + 2 * R * n, "k_dec_p1": R * n, "k_dec_p2": R * n, "k_dec_p3": R * n}
     roof = roofline_of(kt, units, peak, {"timing": "HIP events on the launch stream, one dg_recover call"}, "c3")
     out = {"metric": "Recover/s at n=%d t=%d (all %d shares VerifyPartial'd, first t valid interpolated)" % (n, t, n),
@@ -399,7 +399,8 @@ def adversarial_bench(L, tbls, shard, chain, R_total, world, rank, peak, t=129, 
     g1 = L.group_counts()
     L.check(L.lib().dg_set_timing(0))
     checks = {"k_verify_groups[%d]" % (m + 1): g1[m] - g0[m] for m in range(4)}
-    roof = roofline_of(kt, {"k_verify_groups": checks, "k_recover_terms": R * t}, peak,
+    # k_rs_sac: one unit = one round's joint column MSM (priced at t = 129 over a scattered index set)
+    roof = roofline_of(kt, {"k_verify_groups": checks, "k_rs_sac": R}, peak,
                        {"timing": "HIP events on the launch stream, one dg_recover call",
                         "checks_by_members": checks}, "c5")
     ncorrupt = np.array([len(items)], np.int64)

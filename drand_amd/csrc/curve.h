@@ -406,7 +406,7 @@ DGH G2J g2_mul_u256_psi(const G2A& p, const uint32_t* k) {
   return acc;
 }
 // The same product with the accumulator in LDS (`acc`: one G2JStore slot per lane at the call site,
-// k_recover_terms): doublings and mixed additions as g2_dbl_lds / g2_madd_lds, so the register file holds P,
+// hostcheck): doublings and mixed additions as g2_dbl_lds / g2_madd_lds, so the register file holds P,
 // psi(P) and one formula's temporaries (the in-register form spills ~740 VGPRs).  Same result.
 template <class SJ>
 DGI void g2_mul_u256_psi_lds(const G2A& p, const uint32_t* k, SJ& acc) {

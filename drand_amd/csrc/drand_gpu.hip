@@ -67,7 +67,7 @@ struct Ctx {
   // The per-item pairing kernels (k_verify_items, k_verify_groups: ~14.5 KB of private segment per lane) run on
   // this one stream, whatever set the batch uses: a hardware queue reserves scratch for the largest private
   // segment dispatched on it, so only this stream's queue holds that reservation and the workspace sets'
-  // queues stay at the ~8.5 KB of k_recover_terms (with 8 hardware queues, every queue holding 14.5 KB failed
+  // queues stay at the ~5.7 KB of k_sign (with 8 hardware queues, every queue holding 14.5 KB failed
   // with HSA_STATUS_ERROR_OUT_OF_RESOURCES).  Only failed or isolating batches reach it.
   hipStream_t fb_stream = nullptr;
   int cur = 0, next = 0;
@@ -137,7 +137,7 @@ enum Slot {
   S_IN4, S_OUT0, S_PK1, S_PK1ST, S_PK1RAW, S_ACTIVE, S_MSM_CNT, S_MSM_LIST, S_MSM_CHUNKS, S_MSM_B, S_MSM_G,
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
   S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_BINV, S_NV, S_NVINV,
-  S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_BINV_PRE, S_BINV_ROOTS, S_RC_UNI, S_RC_REF,
+  S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_BINV_PRE, S_BINV_ROOTS, S_RC_UNI, S_RC_REF, S_RC_LIST, S_RS_DIG,
   S_RC_NAF, S_RC_EV, S_RC_TAB, S_RC_D, S_RC_PINF, S_RC_DEN, S_RC_A, S_COUNT
 };
 
@@ -430,8 +430,8 @@ int msm_run_keyed(const Batch& b, const uint64_t* seed, const uint8_t* iso, bool
   uint32_t *offset = cnt + nkeys, *cursor = offset + nkeys, *chunk_off = cursor + nkeys;  // chunk_off: nkeys + 1
   RET(wsT(S_KMSM_TOT, (size_t)2 * nblocks, &tot));
   RET(wsT(S_KMSM_LIST, (size_t)nwin * N + 1, &list));
-  // sum of ceil(count / 8) <= nwin N / 8 + nkeys
-  const size_t max_chunks_sz = ((size_t)nwin * N) / MSM_CHUNK + 1 + nkeys;
+  // sum of ceil(count / KMSM_CHUNK) <= nwin N / KMSM_CHUNK + nkeys
+  const size_t max_chunks_sz = ((size_t)nwin * N) / KMSM_CHUNK + 1 + nkeys;
   if (max_chunks_sz > 0xffffffffull) return fail(DG_E_ARG, "batch too large for the keyed MSM");
   const uint32_t max_chunks = (uint32_t)max_chunks_sz;
   RET(wsT(S_KMSM_CHUNKS, max_chunks, &chunks));
@@ -865,6 +865,37 @@ int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const 
   return 0;
 }
 
+// Recover's divergent rounds (recover.h k_rs_*): the rounds nl[0..Rn) of the blocks whose rounds selected different
+// index sets, one sign-aligned joint MSM per round in lanes of RS_G shares, sums into out[r].
+int recover_sac(uint32_t R, uint32_t k, uint32_t t, uint32_t Rn, const uint32_t* nl, const uint32_t* d_selidx,
+                const uint32_t* d_sel, const uint8_t* d_rst, const G2AStore* d_S, G2JStore* out, hipStream_t st) {
+  const size_t n = (size_t)t * Rn;
+  if (3 * n > 0x7fffffffull) return fail(DG_E_ARG, "Recover batch too large for the column tables");
+  const uint32_t ngroups = (t + RS_G - 1) / RS_G;
+  RsDigits* dig;
+  uint4* T4;
+  uint8_t* pinf;
+  Fp *den, *dinv;
+  G2JStore* Aps;
+  RET(wsT(S_RS_DIG, n, &dig));
+  RET(wsT(S_RC_TAB, n * 8 * RC_Q, &T4));
+  RET(wsT(S_RC_PINF, n, &pinf));
+  RET(wsT(S_RC_DEN, 6 * n, &den));
+  dinv = den + 3 * n;
+  RET(wsT(S_RC_A, (size_t)ngroups * Rn, &Aps));
+  RET(launch("k_rs_digits", k_rs_digits, (uint32_t)n, 64, st, R, Rn, t, nl, d_selidx, d_rst, dig));
+  for (uint32_t l = 0; l < 3; ++l) {
+    RET(launch("k_rs_tab_den", k_rs_tab_den, (uint32_t)(3 * n), 128, st, l, R, Rn, k, t, nl, d_rst, d_sel, d_S,
+               (const uint4*)T4, pinf, den));
+    RET(batch_inv((uint32_t)(3 * n), den, dinv, st));
+    RET(launch("k_rs_tab_add", k_rs_tab_add, (uint32_t)(3 * n), 128, st, l, R, Rn, k, t, nl, d_rst, d_sel, d_S, T4,
+               (const uint8_t*)pinf, (const Fp*)dinv));
+  }
+  RET(launch("k_rs_sac", k_rs_sac, ngroups * Rn, 64, st, R, Rn, t, ngroups, nl, d_rst, (const RsDigits*)dig,
+             (const uint4*)T4, (const uint8_t*)pinf, Aps));
+  return launch("k_rs_combine", k_rs_combine, Rn, 128, st, R, Rn, ngroups, nl, d_rst, (const G2JStore*)Aps, out);
+}
+
 // Recover after the VerifyPartial statuses are known (d_st): per round the first t valid partials, xyCommit
 // dedupe, Lagrange terms lambda_j S_j, row sums, compression; results copied to the output buffers (host or
 // device memory: hipMemcpyDefault).
@@ -912,17 +943,16 @@ int recover_msm(uint32_t R, uint32_t k, uint32_t t, uint32_t U, const uint32_t* 
 int recover_tail(uint32_t R, uint32_t k, uint32_t t, const uint8_t* d_p, const uint8_t* d_st, const G2AStore* d_S,
                  uint8_t* out_sig96, uint8_t* round_status, uint8_t* share_status, hipStream_t st) {
   uint8_t *d_rst, *d_sst, *d_out, *d_uni;
-  uint32_t *d_sel, *d_selidx, *d_ref, *d_ub;
-  G2JStore *terms, *tmp;
-  const uint32_t nblk = (R + RC_BLK - 1) / RC_BLK, Rp = nblk * RC_BLK;
+  uint32_t *d_sel, *d_selidx, *d_ref, *d_ub = nullptr;
+  G2JStore* terms;
+  const uint32_t nblk = (R + RC_BLK - 1) / RC_BLK;
   RET(wsT(S_SEL, (size_t)R * t, &d_sel));
   RET(wsT(S_SELIDX, (size_t)R * t, &d_selidx));
   RET(wsT(S_RST, R, &d_rst));
   RET(wsT(S_SST, (size_t)R * k, &d_sst));
   RET(launch("k_recover_select", k_recover_select, R, 128, st, R, k, t, d_p, d_st, d_sel, d_selidx, d_rst, d_sst));
   RET(wsT(S_RC_UNI, nblk, &d_uni));
-  RET(wsT(S_RC_REF, 2 * (size_t)nblk, &d_ref));
-  d_ub = d_ref + nblk;
+  RET(wsT(S_RC_REF, nblk, &d_ref));
   RET(launch("k_rc_blocks", k_rc_blocks, nblk * RC_BLK, 64, st, R, t, (const uint32_t*)d_selidx, (const uint8_t*)d_rst,
              d_uni, d_ref));
   // the host orders the work: which blocks are uniform (and hold an OK round) decides the launch sizes
@@ -931,24 +961,23 @@ int recover_tail(uint32_t R, uint32_t k, uint32_t t, const uint8_t* d_p, const u
   HIPCHK(hipMemcpyAsync(uni.data(), d_uni, nblk, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(ref.data(), d_ref, 4 * (size_t)nblk, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  std::vector<uint32_t> ub;
-  uint32_t nonuni = 0;
-  for (uint32_t b = 0; b < nblk; ++b) {
-    if (!uni[b]) ++nonuni;
-    else if (ref[b] != ~0u) ub.push_back(b);
+  // ub: the uniform blocks holding an OK round (the block-uniform MSM); nl: every round of the other blocks (the
+  // divergent-round form); one host list, uploaded once
+  std::vector<uint32_t> lists;
+  for (uint32_t b = 0; b < nblk; ++b)
+    if (uni[b] && ref[b] != ~0u) lists.push_back(b);
+  const uint32_t U = (uint32_t)lists.size();
+  for (uint32_t b = 0; b < nblk; ++b)
+    if (!uni[b])
+      for (uint32_t r = b * RC_BLK; r < (b + 1) * RC_BLK && r < R; ++r) lists.push_back(r);
+  const uint32_t Rn = (uint32_t)lists.size() - U;
+  RET(wsT(S_TERMS, R, &terms));
+  if (!lists.empty()) {
+    RET(wsT(S_RC_LIST, lists.size(), &d_ub));
+    HIPCHK(hipMemcpyAsync(d_ub, lists.data(), 4 * lists.size(), hipMemcpyHostToDevice, st));
   }
-  const uint32_t U = (uint32_t)ub.size();
-  RET(wsT(S_TERMS, (size_t)(nonuni ? R : 1) * (nonuni ? t : 1) + R, &terms));
-  if (nonuni) {
-    RET(wsT(S_TMP, (size_t)R * t, &tmp));
-    RET(launch("k_recover_terms", k_recover_terms, t * Rp, 64, st, R, Rp, k, t, (const uint32_t*)d_sel,
-               (const uint32_t*)d_selidx, (const uint8_t*)d_rst, (const uint8_t*)d_uni, d_S, terms));
-    RET(reduce_rows(terms, tmp, R, t, st, 2, d_uni));
-  }
-  if (U) {
-    HIPCHK(hipMemcpyAsync(d_ub, ub.data(), 4 * (size_t)U, hipMemcpyHostToDevice, st));
-    RET(recover_msm(R, k, t, U, d_ub, d_ref, d_selidx, d_sel, d_rst, d_S, terms, st));
-  }
+  if (Rn) RET(recover_sac(R, k, t, Rn, d_ub + U, d_selidx, d_sel, d_rst, d_S, terms, st));
+  if (U) RET(recover_msm(R, k, t, U, d_ub, d_ref, d_selidx, d_sel, d_rst, d_S, terms, st));
   RET(wsT(S_OUT0, (size_t)R * 96, &d_out));
   RET(launch("k_compress_g2", k_compress_g2, R, 128, st, R, (const G2JStore*)terms, (const uint8_t*)d_rst, d_out));
   HIPCHK(hipMemcpyAsync(out_sig96, d_out, (size_t)R * 96, hipMemcpyDefault, st));
@@ -997,7 +1026,7 @@ int dg_init(int device) {
   // with zero items (every lane returns at once), so the growth happens now -- the largest first: a dispatch
   // that needs a larger private segment than the queue's current one, right behind it, failed with
   // HSA_STATUS_ERROR_OUT_OF_RESOURCES on the box.  The per-item kernels go to the per-item stream only; every
-  // workspace stream gets k_recover_terms, the largest private segment of the kernels that run there
+  // workspace stream gets k_sign, the largest private segment of the kernels that run there
   // (tests/test_abi.py checks both orderings against the code-object metadata).
   hipFuncAttributes fa_items{}, fa_groups{};
   HIPCHK(hipFuncGetAttributes(&fa_items, reinterpret_cast<const void*>(k_verify_items)));
@@ -1018,10 +1047,9 @@ int dg_init(int device) {
   }
   HIPCHK(hipGetLastError());
   for (Set& x : g_ctx.sets) {
-    // t = 0: every lane returns (m >= t)
-    hipLaunchKernelGGL(k_recover_terms, dim3(1), dim3(64), 0, x.stream, 0u, 64u, 1u, 0u, (const uint32_t*)nullptr,
-                       (const uint32_t*)nullptr, (const uint8_t*)nullptr, (const uint8_t*)nullptr,
-                       (const G2AStore*)nullptr, (G2JStore*)nullptr);
+    // n = 0: every lane returns
+    hipLaunchKernelGGL(k_sign, dim3(1), dim3(128), 0, x.stream, 0u, (const uint8_t*)nullptr, (const uint16_t*)nullptr,
+                       (const uint8_t*)nullptr, 0u, (const uint8_t*)nullptr, 0u, (uint8_t*)nullptr);
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipDeviceSynchronize());

@@ -11,7 +11,7 @@
 #define DG_HOT_WAVES 2  // min waves per SIMD for the hot kernels: 256 VGPRs each (measured: 2 beats 1 by 6%)
 #endif
 #ifndef DG_TERMS_WAVES
-#define DG_TERMS_WAVES DG_HOT_WAVES  // min waves per SIMD of k_recover_terms
+#define DG_TERMS_WAVES DG_HOT_WAVES  // min waves per SIMD of Recover's MSM lanes (k_rc_straus, k_rs_sac)
 #endif
 #ifndef DG_BULK_WAVES
 #define DG_BULK_WAVES 1  // min waves per SIMD for the other per-lane group-arithmetic kernels
@@ -863,33 +863,6 @@ DG_KERNEL void __launch_bounds__(128) k_decode_verified(uint32_t n, const uint8_
   store_g2a(S[i], a);
   status[i] = st;
 }
-#endif
-
-// The per-term path of Recover, for the blocks of 64 rounds whose rounds selected different index sets
-// (recover.h k_rc_blocks: uni[b] == 0; the uniform blocks take the per-round MSM of recover.h): lane (m, r), rounds
-// fastest over the padded count Rp = 64 * blocks, terms[r * t + m] = lambda_m S_{r, sel[m]} by the sign-aligned
-// column form (g2_mul_u256_psi_sac: 65 doublings + 65 additions whatever the digits, no divergence).  The row sums
-// (k_sum_rows, skipping the uniform blocks) follow.  Hot translation unit (kernels_hot.hip: flat, 2 waves/SIMD).
-#if DG_TU_HOT
-DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms(uint32_t R, uint32_t Rp, uint32_t k, uint32_t t,
-                                                     const uint32_t* sel, const uint32_t* selidx,
-                                                     const uint8_t* round_status, const uint8_t* uni,
-                                                     const G2AStore* S, G2JStore* terms) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, m = g / Rp, r = g % Rp;
-  if (m >= t || uni[r / 64] || r >= R) return;
-  const size_t o = (size_t)r * t + m;
-  if (round_status[r] != DG_ST_OK_) {
-    store_g2j(terms[o], jac_infinity<Fp2>());
-    return;
-  }
-  const Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, m);
-  store_g2j(terms[o], g2_mul_u256_psi_sac(load_g2a(S[(size_t)r * k + sel[o]]), lam.l));
-}
-#else
-DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_recover_terms(uint32_t R, uint32_t Rp, uint32_t k, uint32_t t,
-                                                     const uint32_t* sel, const uint32_t* selidx,
-                                                     const uint8_t* round_status, const uint8_t* uni,
-                                                     const G2AStore* S, G2JStore* terms);
 #endif
 
 // compress points (zeros where status != OK)

@@ -43,6 +43,13 @@ DGI uint32_t kmsm_key(uint32_t w, uint32_t d, uint32_t set, uint32_t nsets) { re
 #define DG_MSM_WAVES DG_HOT_WAVES  // min waves per SIMD of the chunk sums
 #endif
 constexpr uint32_t MSM_CHUNK = 8;   // points per first-level lane
+// points per chunk of the keyed MSM: its buckets hold ~400 points each at C3 (100k rounds: 6.4M items x 18
+// windows over 256 digits x 64 key sets), so longer mixed-addition chunks (29 Fp products per point) leave fewer
+// chunk sums for the bucket lanes' full Jacobian additions (43 per chunk)
+#ifndef DG_KMSM_CHUNK
+#define DG_KMSM_CHUNK 32
+#endif
+constexpr uint32_t KMSM_CHUNK = DG_KMSM_CHUNK;
 constexpr uint32_t MSM_BSPLIT = 32;  // lanes per bucket at the second level
 constexpr uint32_t MSM_SLICE_LANES = 64;  // lanes per (side, window, bit slice) in k_msm_slices
 
@@ -508,7 +515,7 @@ DG_KERNEL void __launch_bounds__(256) k_kmsm_count(uint32_t N, uint32_t k, uint3
   }
 }
 
-// block b of KSCAN_B keys: exclusive scans of count and of ceil(count / MSM_CHUNK) within the block,
+// block b of KSCAN_B keys: exclusive scans of count and of ceil(count / KMSM_CHUNK) within the block,
 // block totals into tot[b], tot[nblocks + b]
 DG_KERNEL void __launch_bounds__(256) k_kscan_local(uint32_t nkeys, const uint32_t* count, uint32_t* offset,
                                                     uint32_t* chunk_off, uint32_t* tot) {
@@ -520,7 +527,7 @@ DG_KERNEL void __launch_bounds__(256) k_kscan_local(uint32_t nkeys, const uint32
     c[j] = sc;
     kk[j] = sk;
     sc += v;
-    sk += (v + MSM_CHUNK - 1) / MSM_CHUNK;
+    sk += (v + KMSM_CHUNK - 1) / KMSM_CHUNK;
   }
   s_c[t] = sc;
   s_k[t] = sk;
@@ -580,7 +587,7 @@ DG_KERNEL void __launch_bounds__(256) k_kmsm_scatter(uint32_t N, uint32_t k, uin
   }
 }
 
-// lane c: the c-th chunk (<= MSM_CHUNK affine points of one bucket)
+// lane c: the c-th chunk (<= KMSM_CHUNK affine points of one bucket)
 #endif
 // hot translation unit (kernels_hot.hip: flat, 2 waves/SIMD; measured -27% / -36%)
 #if defined(__HIP__) && DG_TU_HOT
@@ -598,9 +605,9 @@ DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_chunks(uint32_t max_c
     else
       hi = mid;
   }
-  uint32_t first = offset[lo] + (c - chunk_off[lo]) * MSM_CHUNK;
+  uint32_t first = offset[lo] + (c - chunk_off[lo]) * KMSM_CHUNK;
   uint32_t last = offset[lo] + count[lo];
-  if (last > first + MSM_CHUNK) last = first + MSM_CHUNK;
+  if (last > first + KMSM_CHUNK) last = first + KMSM_CHUNK;
 #if DG_MSM_LDS
 #if DG_MSM_LDS == 1
   __shared__ G2JStore s_acc[128];

@@ -22,8 +22,8 @@
 //   k_rc_tab_den / batch inversion / k_rc_tab_add     per level: the odd-multiple tables, affine (SoA in HBM)
 //   k_rc_straus    lane (component i, round): A_i by the block's schedule, running point in LDS
 //   k_rc_combine   per round: sigma = A0 - psi(A1) + psi^2(A2) - psi^3(A3)
-// Blocks whose rounds selected different index sets (corrupted shares, C5) keep the per-term path
-// (k_recover_terms, sign-aligned column form) and the row sums.
+// Blocks whose rounds selected different index sets (corrupted shares, C5) take the divergent-round form below
+// (k_rs_*: one sign-aligned joint MSM per round, regular control flow whatever each lane's scalars).
 #pragma once
 // included from kernels.h (uses the G2AStore / G2JStore layouts, the Fr helpers and DG_ST_OK_ defined there)
 
@@ -385,6 +385,212 @@ DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rc_straus(uint32_t R, uin
                                                                  const uint8_t* rst, const uint32_t* ev,
                                                                  const uint32_t* hdr, const uint4* T4,
                                                                  const uint8_t* pinf, G2JStore* A);
+#endif
+
+// ---------------------------------------------------------------------------------------------------
+// Divergent rounds (blocks whose rounds selected different index sets: corrupted shares, C5): one joint MSM per
+// round in the sign-aligned column form (GLV-SAC, curve.h g2_mul_u256_psi_sac) -- every lane runs the same
+// column loop whatever its scalars, so lanes holding different rounds never diverge.  Per share j, with its
+// psi digits d0..d3 (d0 made odd, corrected by one final subtraction of P_j), column c adds s_c T_j[u_c],
+// T_j[u] = P0 + u1 P1 + u2 P2 + u3 P3 (P0 = P, P1 = -psi(P), P2 = psi^2(P), P3 = -psi^3(P)): 65 columns.  A lane
+// takes RS_G shares of one round and shares ONE doubling per column among them (the round-2 per-term form paid 65
+// doublings per share); the RS_G-share partial sums of a round are added at the end.  The tables are affine,
+// built in three batched levels (T1, T2, T4 = P0 + P1, P0 + P2, P0 + P3; T3, T5, T6 = T1 + P2, T1 + P3, T2 + P3;
+// T7 = T3 + P3) with the denominators of each level inverted together.  P_i are [|z|^i]P up to sign with
+// 1 + |z| + |z|^2 + |z|^3 < r, so for P != O no table addition is exceptional.
+//   k_rs_digits    lane (share, round): lambda_j, psi digits, sign-aligned recoding (RsDigits)
+//   k_rs_tab_den / batch inversion / k_rs_tab_add     three levels of the 8-entry tables
+//   k_rs_sac       lane (share group, round): the group's joint column loop, running point in LDS
+//   k_rs_combine   per round: the sum of its group partial sums
+constexpr uint32_t RS_G = 8;  // shares per lane
+
+// sign-aligned recoding of one share's psi digits (g2_mul_u256_psi_sac): bit c of sgn set = +T in column c
+// (c < 64; column 64 is always +), um[i] bit c = u_{i+1, c}, top = the column-64 entry, even: d0 was even (add
+// 1, subtract P at the end)
+struct RsDigits {
+  uint64_t sgn, um[3];
+  uint32_t top, even;
+};
+DGI RsDigits rs_recode(const uint64_t (&d)[4]) {
+  RsDigits o;
+  o.even = (d[0] & 1) == 0 ? 1u : 0u;
+  const uint64_t k0 = d[0] + (o.even ? 1u : 0u);
+  o.sgn = k0 >> 1;
+  o.top = 0;
+  for (int i = 0; i < 3; ++i) {
+    uint64_t a = d[i + 1], m = 0;
+    for (int j = 0; j < 64; ++j) {
+      const uint64_t bit = a & 1u;
+      m |= bit << j;
+      a = (a >> 1) + (bit & ~(o.sgn >> j) & 1u);
+    }
+    o.um[i] = m;
+    o.top |= (uint32_t)a << i;
+  }
+  return o;
+}
+// P0..P3 of a share (the same signs as g2_mul_u256_psi_sac: P1 = -psi(P), P2 = psi^2(P) = (w x, -y),
+// P3 = -psi^3(P) = (w psi(P).x, psi(P).y))
+DGI void rs_points(const G2A& p, Fp2 (&px)[4], Fp2 (&py)[4]) {
+  Fp2 qx = p.x, qy = p.y;
+  g2_psi_aff(qx, qy);
+  const Fp w = fp_const(PSI2_W);
+  px[0] = p.x;
+  py[0] = p.y;
+  px[1] = qx;
+  py[1] = fp2_neg(qy);
+  px[2] = fp2_mul_fp(p.x, w);
+  py[2] = fp2_neg(p.y);
+  px[3] = fp2_mul_fp(qx, w);
+  py[3] = qy;
+}
+// table level l (0..2), element e (0..2): the pair (a index, b point) it adds and the entry it writes
+//   l0: T1 = T0 + P1, T2 = T0 + P2, T4 = T0 + P3;  l1: T3 = T1 + P2, T5 = T1 + P3, T6 = T2 + P3;  l2: T7 = T3 + P3
+DGI bool rs_level(uint32_t l, uint32_t e, uint32_t& src, uint32_t& pb, uint32_t& dst) {
+  constexpr uint8_t S[3][3] = {{0, 0, 0}, {1, 1, 2}, {3, 0, 0}};
+  constexpr uint8_t B[3][3] = {{1, 2, 3}, {2, 3, 3}, {3, 0, 0}};
+  constexpr uint8_t D[3][3] = {{1, 2, 4}, {3, 5, 6}, {7, 0, 0}};
+  if (l == 2 && e > 0) return false;
+  src = S[l][e];
+  pb = B[l][e];
+  dst = D[l][e];
+  return true;
+}
+
+#if defined(__HIP__) && DG_TU_LIB
+// lane g < t * Rn: share j = g / Rn of divergent round u = g % Rn (round nl[u]); lambda_j of the round's own
+// selected set, its psi digits and their sign-aligned recoding, dig[g]
+DG_KERNEL void __launch_bounds__(64) k_rs_digits(uint32_t R, uint32_t Rn, uint32_t t, const uint32_t* nl,
+                                                 const uint32_t* selidx, const uint8_t* rst, RsDigits* dig) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= t * Rn) return;
+  const uint32_t j = g / Rn, r = nl[g % Rn];
+  if (r >= R || rst[r] != DG_ST_OK_) return;
+  const Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, j);
+  uint64_t d[4];
+  rc_psi_digits(lam, d);
+  dig[g] = rs_recode(d);
+}
+
+// per divergent round u: sigma = the sum of its ngroups group partial sums (Aps[q * Rn + u]) into out[r]
+DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_rs_combine(uint32_t R, uint32_t Rn, uint32_t ngroups,
+                                                                  const uint32_t* nl, const uint8_t* rst,
+                                                                  const G2JStore* Aps, G2JStore* out) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= Rn) return;
+  const uint32_t r = nl[u];
+  if (r >= R || rst[r] != DG_ST_OK_) return;
+  G2J acc = load_g2j(Aps[u]);
+  for (uint32_t q = 1; q < ngroups; ++q) acc = jac_add(acc, load_g2j(Aps[(size_t)q * Rn + u]));
+  store_g2j(out[r], acc);
+}
+#endif
+
+#if defined(__HIP__) && DG_TU_HOT
+DGI bool rs_lane(uint32_t g, uint32_t t, uint32_t R, uint32_t Rn, const uint32_t* nl, const uint8_t* rst,
+                 uint32_t& j, uint32_t& u, uint32_t& r) {
+  if (g >= t * Rn) return false;
+  j = g / Rn;
+  u = g % Rn;
+  r = nl[u];
+  return r < R && rst[r] == DG_ST_OK_;
+}
+// lane g < 3 t Rn: element e = g / (t Rn) of level l for (share j, round u); pinf[j * Rn + u] is set at level 0
+DG_KERNEL void __launch_bounds__(128) k_rs_tab_den(uint32_t l, uint32_t R, uint32_t Rn, uint32_t k, uint32_t t,
+                                                   const uint32_t* nl, const uint8_t* rst, const uint32_t* sel,
+                                                   const G2AStore* S, const uint4* T4, uint8_t* pinf, Fp* den) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, n = t * Rn;
+  if (g >= 3 * n) return;
+  const uint32_t e = g / n;
+  uint32_t j, u, r, src, pb, dst;
+  Fp v = fp_one();
+  if (rs_lane(g % n, t, R, Rn, nl, rst, j, u, r) && rs_level(l, e, src, pb, dst)) {
+    const G2A p = load_g2a(S[(size_t)r * k + sel[(size_t)r * t + j]]);
+    if (l == 0 && e == 0) pinf[g % n] = p.inf ? 1 : 0;
+    if (!p.inf) {
+      Fp2 px[4], py[4];
+      rs_points(p, px, py);
+      Fp2 ax = px[0], ay;
+      if (src) rc_ld(T4 + ((size_t)j * 8 + src) * RC_Q * Rn + u, Rn, ax, ay);
+      v = fp2_norm(fp2_sub(px[pb], ax));
+    }
+  }
+  den[g] = v;
+}
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_rs_tab_add(uint32_t l, uint32_t R, uint32_t Rn, uint32_t k, uint32_t t,
+                                                                 const uint32_t* nl, const uint8_t* rst,
+                                                                 const uint32_t* sel, const G2AStore* S, uint4* T4,
+                                                                 const uint8_t* pinf, const Fp* ninv) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, n = t * Rn;
+  if (g >= 3 * n) return;
+  const uint32_t e = g / n;
+  uint32_t j, u, r, src, pb, dst;
+  if (!rs_lane(g % n, t, R, Rn, nl, rst, j, u, r) || !rs_level(l, e, src, pb, dst) || pinf[g % n]) return;
+  const G2A p = load_g2a(S[(size_t)r * k + sel[(size_t)r * t + j]]);
+  Fp2 px[4], py[4];
+  rs_points(p, px, py);
+  G2A a{px[0], py[0], false};
+  if (src) rc_ld(T4 + ((size_t)j * 8 + src) * RC_Q * Rn + u, Rn, a.x, a.y);
+  else if (e == 0) rc_st(T4 + (size_t)j * 8 * RC_Q * Rn + u, Rn, px[0], py[0]);  // T0 = P0 (level 0, once)
+  const G2A s = g2_aff_sum(a, G2A{px[pb], py[pb], false}, 1, ninv[g]);
+  rc_st(T4 + ((size_t)j * 8 + dst) * RC_Q * Rn + u, Rn, s.x, s.y);
+}
+
+// lane (share group q, divergent round u), grid RS lanes = ngroups * Rn padded to whole waves: the columns of
+// its <= RS_G shares, one doubling per column, then the even-d0 corrections; Aps[q * Rn + u]
+DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rs_sac(uint32_t R, uint32_t Rn, uint32_t t, uint32_t ngroups,
+                                                              const uint32_t* nl, const uint8_t* rst,
+                                                              const RsDigits* dig, const uint4* T4,
+                                                              const uint8_t* pinf, G2JStore* Aps) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t q = g / Rn, u = g % Rn;
+  const bool live = q < ngroups && nl[u] < R && rst[nl[u]] == DG_ST_OK_;
+  const uint32_t j0 = q * RS_G, j1 = j0 + RS_G < t ? j0 + RS_G : t;
+  __shared__ G2JStore s_acc[64];
+  G2JStore& acc = s_acc[threadIdx.x];
+  acc.x = fp2_zero();
+  acc.y = fp2_zero();
+  acc.z = fp2_zero();
+  if (!live) return;
+  for (int c = 64; c >= 0; --c) {
+    if (c < 64) g2_dbl_lds(acc);
+    for (uint32_t j = j0; j < j1; ++j) {
+      if (pinf[(size_t)j * Rn + u]) continue;
+      const RsDigits& d = dig[(size_t)j * Rn + u];
+      uint32_t e;
+      bool pos;
+      if (c == 64) {
+        e = d.top;
+        pos = true;
+      } else {
+        e = (uint32_t)((d.um[0] >> c) & 1u) | (uint32_t)((d.um[1] >> c) & 1u) << 1 | (uint32_t)((d.um[2] >> c) & 1u) << 2;
+        pos = (d.sgn >> c) & 1u;
+      }
+      Fp2 x, y;
+      rc_ld(T4 + ((size_t)j * 8 + e) * RC_Q * Rn + u, Rn, x, y);
+      g2_madd_lds(acc, x, pos ? y : fp2_neg(y));
+    }
+  }
+  for (uint32_t j = j0; j < j1; ++j) {
+    if (pinf[(size_t)j * Rn + u] || !dig[(size_t)j * Rn + u].even) continue;
+    Fp2 x, y;
+    rc_ld(T4 + (size_t)j * 8 * RC_Q * Rn + u, Rn, x, y);
+    g2_madd_lds(acc, x, fp2_neg(y));
+  }
+  Aps[(size_t)q * Rn + u] = acc;
+}
+#elif defined(__HIP__)
+DG_KERNEL void __launch_bounds__(128) k_rs_tab_den(uint32_t l, uint32_t R, uint32_t Rn, uint32_t k, uint32_t t,
+                                                   const uint32_t* nl, const uint8_t* rst, const uint32_t* sel,
+                                                   const G2AStore* S, const uint4* T4, uint8_t* pinf, Fp* den);
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_rs_tab_add(uint32_t l, uint32_t R, uint32_t Rn, uint32_t k, uint32_t t,
+                                                                 const uint32_t* nl, const uint8_t* rst,
+                                                                 const uint32_t* sel, const G2AStore* S, uint4* T4,
+                                                                 const uint8_t* pinf, const Fp* ninv);
+DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rs_sac(uint32_t R, uint32_t Rn, uint32_t t, uint32_t ngroups,
+                                                              const uint32_t* nl, const uint8_t* rst,
+                                                              const RsDigits* dig, const uint4* T4,
+                                                              const uint8_t* pinf, G2JStore* Aps);
 #endif
 
 }  // namespace dg

@@ -298,3 +298,55 @@ extern "C" int hc_wnaf_check(uint64_t d) {
   }
   return v == (unsigned __int128)d ? 1 : 0;
 }
+
+// Recover's divergent-round form (recover.h, k_rs_*) on the host: the sign-aligned tables by the device's three
+// affine levels (exact inverses), the shared column loop over groups of RS_G shares, the even-d0 corrections and
+// the sum of the group partial sums, against sum_j g2_mul_u256_psi(S_j, lambda_j).  1 if equal.
+extern "C" int hc_recover_sac_check(const uint8_t* sigs96, const uint32_t* idx, uint32_t t) {
+  std::vector<G2A> P(t);
+  std::vector<RsDigits> dig(t);
+  std::vector<G2A> T((size_t)t * 8);
+  G2J want = jac_infinity<Fp2>();
+  for (uint32_t j = 0; j < t; ++j) {
+    if (!g2_decompress(P[j], sigs96 + 96 * j, false)) return -1;
+    const Fr lam = lagrange_at_zero(idx, t, j);
+    want = jac_add(want, g2_mul_u256_psi(P[j], lam.l));
+    uint64_t d[4];
+    rc_psi_digits(lam, d);
+    dig[j] = rs_recode(d);
+    if (P[j].inf) continue;
+    Fp2 px[4], py[4];
+    rs_points(P[j], px, py);
+    T[(size_t)j * 8] = G2A{px[0], py[0], false};
+    for (uint32_t l = 0; l < 3; ++l)
+      for (uint32_t e = 0; e < 3; ++e) {
+        uint32_t src, pb, dst;
+        if (!rs_level(l, e, src, pb, dst)) continue;
+        const G2A a = T[(size_t)j * 8 + src], b{px[pb], py[pb], false};
+        if (fp2_eq(a.x, b.x)) return 0;  // no exceptional pair for P != O
+        T[(size_t)j * 8 + dst] = g2_aff_sum(a, b, 1, fp_inv(g2_aff_den(a, b, 1)));
+      }
+  }
+  G2J sum = jac_infinity<Fp2>();
+  for (uint32_t j0 = 0; j0 < t; j0 += RS_G) {
+    const uint32_t j1 = j0 + RS_G < t ? j0 + RS_G : t;
+    G2JStore acc{fp2_zero(), fp2_zero(), fp2_zero()};
+    for (int c = 64; c >= 0; --c) {
+      if (c < 64) g2_dbl_lds(acc);
+      for (uint32_t j = j0; j < j1; ++j) {
+        if (P[j].inf) continue;
+        const RsDigits& d = dig[j];
+        const uint32_t e = c == 64 ? d.top
+                                   : (uint32_t)((d.um[0] >> c) & 1u) | (uint32_t)((d.um[1] >> c) & 1u) << 1 |
+                                         (uint32_t)((d.um[2] >> c) & 1u) << 2;
+        const bool pos = c == 64 || ((d.sgn >> c) & 1u);
+        const G2A& x = T[(size_t)j * 8 + e];
+        g2_madd_lds(acc, x.x, pos ? x.y : fp2_neg(x.y));
+      }
+    }
+    for (uint32_t j = j0; j < j1; ++j)
+      if (!P[j].inf && dig[j].even) g2_madd_lds(acc, T[(size_t)j * 8].x, fp2_neg(T[(size_t)j * 8].y));
+    sum = jac_add(sum, G2J{acc.x, acc.y, acc.z});
+  }
+  return jac_eq(sum, want) ? 1 : 0;
+}

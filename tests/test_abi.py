@@ -88,11 +88,11 @@ def test_host_arithmetic_under_asan_ubsan():
 
 def test_prewarmed_kernels_hold_the_largest_private_segment():
     """dg_init dispatches k_verify_items and k_verify_groups (the larger first) on the per-item stream, and
-    k_recover_terms on every workspace stream, so each queue's scratch reaches its final size before any batch
+    k_sign on every workspace stream, so each queue's scratch reaches its final size before any batch
     runs (a larger private segment needed later regrows the queue's scratch mid-pipeline: stalls, or
     HSA_STATUS_ERROR_OUT_OF_RESOURCES).  From the gfx950 code-object metadata of the built objects: the per-item
-    kernels hold the largest private segment of all, and k_recover_terms the largest of every other kernel (the
-    ones that run on the workspace streams)."""
+    kernels hold the largest private segment of all, and k_sign the largest of every other kernel (the ones that
+    run on the workspace streams)."""
     import tempfile
 
     from tools import resource_usage as RU
@@ -106,4 +106,4 @@ def test_prewarmed_kernels_hold_the_largest_private_segment():
     first = max(ks[k] for k in per_item)
     assert first == max(ks.values()), sorted(ks.items(), key=lambda x: -x[1])[:4]
     rest = {k: v for k, v in ks.items() if k not in per_item}
-    assert ks["k_recover_terms"] == max(rest.values()), sorted(rest.items(), key=lambda x: -x[1])[:4]
+    assert ks["k_sign"] == max(rest.values()), sorted(rest.items(), key=lambda x: -x[1])[:4]

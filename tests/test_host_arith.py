@@ -220,3 +220,17 @@ def test_recover_msm_host_build(hc, t, seed):
     idx = list(range(t)) if seed < 0 else sorted(rng.sample(range(300), t))
     arr = (ctypes.c_uint32 * t)(*idx)
     assert hc.hc_recover_msm_check(b"".join(sigs), arr, t) == 1
+
+
+@pytest.mark.parametrize("t,seed", [(1, 0), (3, 1), (9, 2), (17, 3), (33, -1)])
+def test_recover_sac_host_build(hc, t, seed):
+    """recover.h's divergent-round form on the host (sign-aligned tables in three affine levels, one doubling per
+    column shared by groups of 8 shares, even-digit corrections, group sums) equals sum_j lambda_j S_j; one share
+    is the identity when t > 3."""
+    rounds = load("chain_t3n5.json")["rounds"]
+    rng = random.Random(seed + 200)
+    sigs = [hx(rounds[rng.randrange(len(rounds))]["sig"]) for _ in range(t)]
+    if t > 3:
+        sigs[1] = bytes([0xc0]) + bytes(95)
+    idx = list(range(t)) if seed < 0 else sorted(rng.sample(range(256), t))
+    assert hc.hc_recover_sac_check(b"".join(sigs), (ctypes.c_uint32 * t)(*idx), t) == 1

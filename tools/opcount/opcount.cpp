@@ -307,3 +307,59 @@ extern "C" void oc_recover_msm(const uint8_t* sigs96, const uint32_t* idx, uint3
   (void)rc_combine(A[0], A[1], A[2], A[3]);
   take(out + 6);
 }
+
+// Recover's divergent-round form (recover.h k_rs_*) for one round of t shares: out[0..2] the tables (three affine
+// levels, 7 additions per share with the batch inversion's 3 products per value, the psi images), out[3..5] the
+// column loops of the ceil(t / RS_G) lanes and their even-digit corrections (k_rs_sac), out[6..8] the group sums.
+extern "C" void oc_recover_sac(const uint8_t* sigs96, const uint32_t* idx, uint32_t t, uint64_t* out) {
+  std::vector<G2A> P(t), T((size_t)t * 8);
+  std::vector<RsDigits> dig(t);
+  for (uint32_t j = 0; j < t; ++j) {
+    g2_decompress(P[j], sigs96 + 96 * j, false);
+    uint64_t d[4];
+    rc_psi_digits(lagrange_at_zero(idx, t, j), d);
+    dig[j] = rs_recode(d);
+  }
+  reset();
+  for (uint32_t j = 0; j < t; ++j) {
+    for (uint32_t l = 0; l < 3; ++l)
+      for (uint32_t e = 0; e < 3; ++e) {
+        uint32_t src, pb, dst;
+        if (!rs_level(l, e, src, pb, dst)) continue;
+        Fp2 px[4], py[4];
+        rs_points(P[j], px, py);  // each den and add lane recomputes the psi images
+        rs_points(P[j], px, py);
+        const G2A a = src ? T[(size_t)j * 8 + src] : G2A{px[0], py[0], false}, b{px[pb], py[pb], false};
+        const Fp n = g2_aff_den(a, b, 1);
+        g_fp_mul_count += 3;
+        T[(size_t)j * 8 + dst] = g2_aff_sum(a, b, 1, n);
+      }
+    T[(size_t)j * 8] = P[j];
+  }
+  take(out);
+  reset();
+  std::vector<G2J> part;
+  for (uint32_t j0 = 0; j0 < t; j0 += RS_G) {
+    const uint32_t j1 = j0 + RS_G < t ? j0 + RS_G : t;
+    G2JStore acc{fp2_zero(), fp2_zero(), fp2_zero()};
+    for (int c = 64; c >= 0; --c) {
+      if (c < 64) g2_dbl_lds(acc);
+      for (uint32_t j = j0; j < j1; ++j) {
+        const RsDigits& d = dig[j];
+        const uint32_t e = c == 64 ? d.top
+                                   : (uint32_t)((d.um[0] >> c) & 1u) | (uint32_t)((d.um[1] >> c) & 1u) << 1 |
+                                         (uint32_t)((d.um[2] >> c) & 1u) << 2;
+        const G2A& x = T[(size_t)j * 8 + e];
+        g2_madd_lds(acc, x.x, (c == 64 || ((d.sgn >> c) & 1u)) ? x.y : fp2_neg(x.y));
+      }
+    }
+    for (uint32_t j = j0; j < j1; ++j)
+      if (dig[j].even) g2_madd_lds(acc, T[(size_t)j * 8].x, fp2_neg(T[(size_t)j * 8].y));
+    part.push_back(G2J{acc.x, acc.y, acc.z});
+  }
+  take(out + 3);
+  reset();
+  G2J s = part[0];
+  for (size_t q = 1; q < part.size(); ++q) s = jac_add(s, part[q]);
+  take(out + 6);
+}

@@ -94,6 +94,13 @@ def main():
         for q, kname in ((0, "k_rc_tables"), (1, "k_rc_straus"), (2, "k_rc_combine")):
             o[0], o[1], o[2] = rc[3 * q], rc[3 * q + 1], rc[3 * q + 2]
             add(kname + name)
+    # the divergent-round form at n = 256, t = 129 (C5: rounds with corrupted shares select scattered index sets)
+    sig129 = b"".join(bytes.fromhex(rounds[q % len(rounds)]["sig"]) for q in range(129))
+    rs = (ctypes.c_uint64 * 9)()
+    L.oc_recover_sac(sig129, (ctypes.c_uint32 * 129)(*sorted(rng.sample(range(256), 129))), 129, rs)
+    for q, kname in ((0, "k_rs_tables"), (1, "k_rs_sac"), (2, "k_rs_combine")):
+        o[0], o[1], o[2] = rs[3 * q], rs[3 * q + 1], rs[3 * q + 2]
+        add(kname)
     out = {"mac_per_mul": MAC_MUL, "mac_per_sqr": MAC_SQR, "mac_per_inv": MAC_INV, "vmad_per_mul": VMAD_MUL,
            "vmad_per_sqr": VMAD_SQR, "basis": "BASELINE.md: 300 multiply-adds per Montgomery product M",
            "sample": "tests/golden/chain_t3n5.json (64 rounds)", "per_unit": {}}
