@@ -16,8 +16,8 @@ import bench
 # a stub per-kernel timing table {name: (avg us, launches)} shaped like the real one
 KT = {"k_exp_pm3d4": (1260.0, 12), "k_h2c_p1a": (230.0, 2), "k_h2c_p3": (420.0, 2), "k_dec_p1": (410.0, 2),
       "k_pair_miller_coop": (4300.0, 2), "k_final_coop": (2400.0, 2), "k_msm_aff_add": (210.0, 6)}
-KT_REC = {"k_recover_terms_u": (150000.0, 1), "k_kmsm_chunks": (65000.0, 1), "k_exp_pm3d4": (6600.0, 6)}
-KT_ADV = {"k_verify_groups": (90000.0, 9), "k_recover_terms": (155000.0, 1)}
+KT_REC = {"k_rc_straus": (150000.0, 1), "k_kmsm_chunks": (65000.0, 1), "k_exp_pm3d4": (6600.0, 6)}
+KT_ADV = {"k_verify_groups": (90000.0, 9), "k_rs_sac": (85000.0, 1)}
 
 
 def _free_port():
@@ -37,7 +37,7 @@ def _worker(rank, world, port, peaks, tables_out, q):
         dt = bench.max_over_ranks(0.30 + 0.01 * rank, world)
         roof = bench.headline_roofline(KT, KT, 125000, peak, 1000000, 30, world, dt)
         rec = {"metric": "Recover/s", "value": 300000.0, "unit": "recovers/s", "n_gpus": world,
-               "roofline": bench.roofline_of(KT_REC, {"k_recover_terms_u": 50000 * 33}, peak, None, "c3"),
+               "roofline": bench.roofline_of(KT_REC, {"k_rc_straus": 50000}, peak, None, "c3"),
                "kernel_avg_us": {k: v[0] for k, v in KT_REC.items()}, "note": "x" * 500}
         adv = {"metric": "adversarial", "value": 7600.0, "unit": "recovers/s",
                "roofline": bench.roofline_of(KT_ADV, {"k_verify_groups": {"k_verify_groups[1]": 100,
@@ -96,9 +96,9 @@ def test_bench_report_world2(tmp_path, peak1):
     assert "kernel_avg_us" not in d["recover"] and "note" not in d["recover"]
     assert d["cpu_baseline"]["cores"] >= 1 and d["recover"]["cpu_baseline"]["value"] == 30.0
     side = json.load(open(out))
-    assert side["recover"]["kernel_avg_us"]["k_recover_terms_u"] == 150000.0
+    assert side["recover"]["kernel_avg_us"]["k_rc_straus"] == 150000.0
 
 
 def test_roofline_without_peak_reports_achieved():
-    r = bench.roofline_of(KT_REC, {"k_recover_terms_u": 50000 * 33}, None, None, "c3")
+    r = bench.roofline_of(KT_REC, {"k_rc_straus": 50000}, None, None, "c3")
     assert r["achieved"] > 0 and r["frac"] is None and r["issue_frac"] is None
