@@ -658,6 +658,8 @@ def main():
                          "latency-bound tail of one batch overlaps the head of the next)")
     ap.add_argument("--tables-out", default=os.path.join(ROOT, "gpurun_out", "bench_tables.json"),
                     help="side file for the per-kernel timing tables and the peak probe details (rank 0)")
+    ap.add_argument("--no-peak-detail", action="store_true",
+                    help="measure only the roofline denominator, not the other probe forms (profiling runs)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no per-kernel HIP events after the timed region (no roofline)")
     ap.add_argument("--recover-rounds", type=int, default=100000, help="C3 rounds (all GPUs); 0 disables")
@@ -808,7 +810,7 @@ def main():
     dt = max_over_ranks(dt, world)
     # every rank measures the v_mad_u64_u32 peak of its own GPU: the Recover lines below price their kernels
     # against it on every rank
-    peak = measure_peak(shard, local, detail=(rank == 0))
+    peak = measure_peak(shard, local, detail=(rank == 0 and not args.no_peak_detail))
     roof = headline_roofline(kt, kt_iso, bounds[0][1] - bounds[0][0], peak, G, args.steps, world, dt)
     share = {k: round(v[0] * v[1] / (dt * 1e6), 4) for k, v in kt.items()}
     del d_sts, d_sig, d_ps

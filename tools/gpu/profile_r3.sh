@@ -9,7 +9,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r3prof
 mkdir -p $O
 export TMPDIR=/tmp
-NOHEAD="--no-cpu-baseline --no-c1 --sync-rounds 0 --tables-out $O/tables.json"
+NOHEAD="--no-cpu-baseline --no-c1 --sync-rounds 0 --no-peak-detail --tables-out $O/tables.json"
 HEAD="$NOHEAD --recover-rounds 0 --c5-rounds 0"
 C3="$NOHEAD --steps 1 --warmup 1 --recover-rounds 100000 --c5-rounds 0"
 C5="$NOHEAD --steps 1 --warmup 1 --recover-rounds 0 --c5-rounds 10000"
@@ -42,5 +42,8 @@ for cfg in head c3 c5; do
   pmc SQ_MEM "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_INSTS_SALU" $cfg $A
   pmc GRBM "GRBM_GUI_ACTIVE GRBM_COUNT" $cfg $A
 done
+# the per-dispatch CSVs exceed what a call can bring back: summarise on the box, keep the summaries only
+python3 $R/tools/traffic.py $O $O/pmc_summary.csv $O/traffic.json > $O/traffic.log 2>&1 || { echo "summary failed"; tail -5 $O/traffic.log; exit 1; }
+rm -rf $O/pmc_*/
 fi
 find $O -name "*.csv" | sort

@@ -4,7 +4,7 @@ roofline objects) and a per-kernel counter summary CSV.  Tooling only.
     python tools/traffic.py gpurun_out/r2prof profiles/r2_pmc_summary.csv
 
 The profile directory holds one rocprofv3 output directory per counter pass, named pmc_<config>_<counter>
-(tools/gpu/profile_r2.sh): config "head" = bench.py --sync --steps 1 (the headline batches), "c3" = the
+(tools/gpu/profile_r2.sh, profile_r3.sh): config "head" = bench.py --sync --steps 1 (the headline batches), "c3" = the
 Recover run at BASELINE configs[2], "c5" = the adversarial Recover run at configs[4].  Values are averaged
 over every dispatch of a kernel in the run, the same launch mix as bench.py's per-launch kernel averages.
 
@@ -44,9 +44,9 @@ def load(prof):
     return {cfg: {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in ks.items()} for cfg, ks in acc.items()}
 
 
-def main(prof, out_csv):
+def main(prof, out_csv, out_json=None):
     m = load(prof)
-    out = {"source": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate runs per counter (tools/gpu/profile_r2.sh); "
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate runs per counter (tools/gpu/profile_r2.sh, profile_r3.sh); "
                      "bytes = 2 * FETCH_SIZE + WRITE_SIZE (gfx950); head = bench.py --sync --steps 1, c3 = Recover "
                      "configs[2], c5 = adversarial Recover configs[4]", "configs": {}}
     for cfg, ks in sorted(m.items()):
@@ -62,7 +62,7 @@ def main(prof, out_csv):
                     sec[k]["note"] = ("FETCH/WRITE_SIZE imply %.0f TB/s over the launch, beyond the memory "
                                       "system: counter not usable for this (long, scratch-heavy) kernel" % (b / t / 1e12))
         out["configs"][cfg] = sec
-    json.dump(out, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
+    json.dump(out, open(out_json or os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
     cols = sorted({c for ks in m.values() for cs in ks.values() for c in cs if not c.startswith("_")})
     with open(out_csv, "w", newline="") as f:
         w = csv.writer(f)
@@ -74,4 +74,4 @@ def main(prof, out_csv):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
