@@ -224,8 +224,28 @@ def cpu_recover(commits, t, n, msgs, parts, threads, seconds=8.0, label=""):
                       % (R, label, threads, dt)}, (rs, ss, R)
 
 
+class RoundSource:
+    """Rounds 1..total with their prev_sig and signature for the Recover lines: the linked chain file when one
+    holds them, else GPU-signed rounds whose prev_sig is pseudo-random (gpu_signed_rounds: the same per-round
+    work; only the syncFrom line needs the links and is skipped then)."""
+
+    def __init__(self, tbls, total):
+        chain = load_chain(total)
+        self.linked = chain is not None
+        if self.linked:
+            self.sigs = chain
+        else:
+            self.prevs, self.sigs = gpu_signed_rounds(tbls, 1, total, S.master_secret())
+
+    def prev(self, r):
+        """prev_sig of round r (1-based)"""
+        if self.linked:
+            return bytes(self.sigs[r - 2]) if r >= 2 else S.GENESIS_SEED
+        return bytes(self.prevs[r - 1])
+
+
 # --------------------------------------------------------------------------------------- Recover lines
-def make_group_rounds(tbls, chain_sigs, first, R, t, n):
+def make_group_rounds(tbls, src, first, R, t, n):
     """Partials sigma_{i,r} = x_i H(m_r) of an (n, t) group for chain rounds first..first+R-1, signed on the
     GPU (untimed).  Returns (pub, commits, shares, msgs (R, 32), parts (R, n, 98))."""
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "groups.json")))["t%d" % t]
@@ -234,7 +254,7 @@ def make_group_rounds(tbls, chain_sigs, first, R, t, n):
     coeffs = S.poly_coeffs(t)
     shares = [S.share_value(coeffs, i) for i in range(n)]
     rounds = np.arange(first, first + R, dtype=np.uint64)
-    prev = [bytes(chain_sigs[r - 2]) if r >= 2 else S.GENESIS_SEED for r in rounds.tolist()]
+    prev = [src.prev(r) for r in rounds.tolist()]
     msgs = tbls.beacon_messages(rounds - 1, rounds, prev)
     parts = np.empty((R, n, 98), np.uint8)
     step = max(1, 2000000 // n)
@@ -282,9 +302,9 @@ def timed_ranks(fn, world):
     return res, dt
 
 
-def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps=2):
-    """BASELINE configs[2]: VerifyPartial on every share + Lagrange Recover for an (n, t) group over
-    R_total rounds of the chain, each rank its contiguous range through dg_recover_dev with the messages and
+def recover_bench(L, tbls, shard, src, R_total, t, n, world, rank, peak, steps=2):
+    """BASELINE configs[2]: kyber's tbls.Recover for an (n, t) group -- VerifyPartial of the partials
+    in input order up to the t-th valid one, Lagrange interpolation -- over R_total rounds of the chain, each rank its contiguous range through dg_recover_dev with the messages and
     98 B partials already resident in HBM (the headline `value`, like the verify headline), then the RCCL
     all-gather of the recovered signatures, round statuses and share statuses.  `host_api_value` is the same
     work through the host-buffer dg_recover (the partials cross PCIe inside the call); round-1 numbers were
@@ -295,7 +315,7 @@ def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps
     t0 = time.perf_counter()
     import torch
 
-    pub, commits, shares, msgs, parts = make_group_rounds(tbls, chain, a + 1, R, t, n)
+    pub, commits, shares, msgs, parts = make_group_rounds(tbls, src, a + 1, R, t, n)
     gen_s = time.perf_counter() - t0
     dev = torch.device("cuda", torch.cuda.current_device())
     d_msgs = torch.from_numpy(np.ascontiguousarray(msgs)).to(dev)
@@ -306,7 +326,7 @@ def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps
         (sigs, rs, ss), dt = timed_ranks(lambda: tbls.recover_batch_dev(pub, d_msgs, d_parts, t, n, seed=6 + s), world)
         dts.append(dt)
     (gs, grs, gss), gdt = timed_ranks(lambda: gather_recover(sigs, rs, ss, world, R_total), world)
-    assert not grs.any() and np.array_equal(gs, chain[:R_total]), "recovered signatures differ from the chain"
+    assert not grs.any() and np.array_equal(gs, src.sigs[:R_total]), "recovered signatures differ from the chain"
     assert (gss[:, :t] == 0).all() and (gss[:, t:] == 255).all(), "share statuses"
     dt = min(dts)
     # the host-buffer entry point (dg_recover): the 98 B partials cross PCIe inside the call
@@ -318,13 +338,15 @@ def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps
     kt = L.timings()
     L.check(L.lib().dg_set_timing(0))
     # k_rc_straus: one unit = one round (its four psi-component lanes), priced at the C3 index set 0..32
-    units = {"k_decode_items": R * n, "k_rc_straus": R, "k_h2c_uncleared": R,
-             "k_exp_pm3d4": 4 * R + 2 * R * n, "k_dec_p1": R * n, "k_dec_p2": R * n, "k_dec_p3": R * n}
+    # (every round valid: the batch covers each round's first t partials, the window; the rest are not decoded)
+    units = {"k_decode_items": R * t, "k_rc_straus": R, "k_h2c_uncleared": R,
+             "k_exp_pm3d4": 4 * R + 2 * R * t, "k_dec_p1": R * t, "k_dec_p2": R * t, "k_dec_p3": R * t}
     roof = roofline_of(kt, units, peak, {"timing": "HIP events on the launch stream, one dg_recover call"}, "c3")
-    out = {"metric": "Recover/s at n=%d t=%d (all %d shares VerifyPartial'd, first t valid interpolated)" % (n, t, n),
+    out = {"metric": "Recover/s at n=%d t=%d (kyber tbls.Recover: partials VerifyPartial'd in input order up to the "
+                     "t-th valid, Lagrange-interpolated)" % (n, t),
            "value": R_total / (dt + gdt), "unit": "recovers/s", "n_gpus": world, "rounds": R_total,
            "rounds_per_gpu": R, "partials_per_round": n, "s_per_step": dt, "allgather_s": gdt,
-           "partials_verified_per_s": R_total * n / (dt + gdt), "partials_generated_s": gen_s,
+           "partials_examined_per_s": int((gss != 255).sum()) / (dt + gdt), "partials_generated_s": gen_s,
            "host_api_s_per_step": host_dt, "host_api_value": R_total / (host_dt + gdt),
            "roofline": roof, "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
            "note": "inputs resident in HBM (dg_recover_dev), outputs all-gathered (RCCL) and equal to the chain's "
@@ -333,7 +355,7 @@ def recover_bench(L, tbls, shard, chain, R_total, t, n, world, rank, peak, steps
     return out, (commits, msgs, parts)
 
 
-def adversarial_bench(L, tbls, shard, chain, R_total, world, rank, peak, t=129, n=256, frac=0.10, n_short=3):
+def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=256, frac=0.10, n_short=3):
     """BASELINE configs[4]: n = 256, t = 129, ~10% of the (round, share) cells corrupted with the six
     cycling modes of tools/corrupt.py, plus `n_short` rounds with more than n - t corrupted shares (-> "not
     enough shares"); each rank its contiguous range of R_total rounds through dg_recover_dev (inputs resident
@@ -353,7 +375,7 @@ def adversarial_bench(L, tbls, shard, chain, R_total, world, rank, peak, t=129, 
     a, b = shard.round_range(R_total, world, rank)
     R = b - a
     rounds = np.arange(a + 1, b + 2, dtype=np.uint64)  # one extra round for the "other_round" mode
-    prev = [bytes(chain[r - 2]) if r >= 2 else S.GENESIS_SEED for r in rounds.tolist()]
+    prev = [src.prev(r) for r in rounds.tolist()]
     msgs_all = tbls.beacon_messages(rounds - 1, rounds, prev)
     msgs = msgs_all[:R]
     t0 = time.perf_counter()
@@ -387,7 +409,7 @@ def adversarial_bench(L, tbls, shard, chain, R_total, world, rank, peak, t=129, 
     assert np.array_equal(hs, sigs) and np.array_equal(hrs, rs) and np.array_equal(hss, ss), "host / device differ"
     ok_r = np.array([r not in short for r in range(R)], dtype=bool)
     assert np.array_equal(rs != 0, ~ok_r) and (rs[~ok_r] == 5).all(), "round statuses"
-    assert np.array_equal(sigs[ok_r], chain[a:b][ok_r]), "recovered signatures differ from the chain"
+    assert np.array_equal(sigs[ok_r], src.sigs[a:b][ok_r]), "recovered signatures differ from the chain"
     examined = ss != 255
     assert (ss[examined & bad] != 0).all() and (ss[examined & ~bad] == 0).all(), "share statuses"
     (gs, grs, gss), gdt = timed_ranks(lambda: gather_recover(d_sigs, d_rs, d_ss, world, R_total), world)
@@ -667,7 +689,13 @@ def main():
     ap.add_argument("--sync-rounds", type=int, default=100000, help="0 disables the syncFrom catch-up line")
     ap.add_argument("--no-c1", action="store_true", help="no C1 / live-latency lines")
     ap.add_argument("--status-bufs", type=int, default=4, help="steps whose verdicts may be in flight")
+    ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("BENCH_HW_QUEUES", "8")),
+                    help="HIP hardware queues per process (GPU_MAX_HW_QUEUES, set before HIP starts; 0 keeps the "
+                         "environment's): the library's 4 workspace streams, its per-item stream and the caller's "
+                         "streams each want their own queue (DESIGN.md §5.3)")
     args = ap.parse_args()
+    if args.hw_queues > 0:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)  # inherited by the ranks started below
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # start the N ranks (one process per GPU) before anything in this process touches the GPU
@@ -817,16 +845,18 @@ def main():
     torch.cuda.empty_cache()
 
     # Recover lines (sharded like the headline; chain rounds 1..R)
-    rec_chain = load_chain(max(args.recover_rounds, args.c5_rounds + 1, args.sync_rounds, 1000))
     rec = adv = syn = c1 = lat = None
     rec_in = adv_in = None
-    if args.recover_rounds and rec_chain is not None:
-        rec, rec_in = recover_bench(L, tbls, shard, rec_chain, args.recover_rounds, 33, 64, world, rank, peak)
-    if args.c5_rounds and rec_chain is not None:
-        adv, adv_in = adversarial_bench(L, tbls, shard, rec_chain, args.c5_rounds, world, rank, peak)
+    src = None
+    if args.recover_rounds or args.c5_rounds or args.sync_rounds:
+        src = RoundSource(tbls, max(args.recover_rounds, args.c5_rounds + 1, args.sync_rounds, 1000))
+    if args.recover_rounds:
+        rec, rec_in = recover_bench(L, tbls, shard, src, args.recover_rounds, 33, 64, world, rank, peak)
+    if args.c5_rounds:
+        adv, adv_in = adversarial_bench(L, tbls, shard, src, args.c5_rounds, world, rank, peak)
     if rank == 0:
-        if args.sync_rounds and rec_chain is not None:
-            syn = sync_bench(rec_chain, args.sync_rounds)
+        if args.sync_rounds and src.linked:
+            syn = sync_bench(src.sigs, args.sync_rounds)
         if not args.no_c1:
             c1 = c1_gpu(L, tbls)
             if rec_in is not None:
@@ -857,6 +887,7 @@ def main():
                                     "one shared group key (BASELINE configs[%d])"
                                     % (G, world, -(-G // world), args.batch, 1 if G <= 100000 else 3)),
                        "global_rounds": G, "rounds_per_gpu": n, "batches_per_gpu": nb,
+                       "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "parallelism": "rounds sharded dp%d" % world},
             "batch_fallbacks": fallbacks}
     tables = {"kernel_time_share": share, "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},

@@ -70,6 +70,9 @@ struct Ctx {
   // queues stay at the ~5.7 KB of k_sign (with 8 hardware queues, every queue holding 14.5 KB failed
   // with HSA_STATUS_ERROR_OUT_OF_RESOURCES).  Only failed or isolating batches reach it.
   hipStream_t fb_stream = nullptr;
+  // DG_SHARED_FB=1 (A/B only): the per-item kernels on the batch's own stream, every workspace queue prewarmed with
+  // their private segment (the round-2 arrangement)
+  bool shared_fb = getenv("DG_SHARED_FB") != nullptr;
   int cur = 0, next = 0;
   bool timing = false;
   std::vector<Timing> timings;
@@ -138,7 +141,8 @@ enum Slot {
   S_MSM_P1, S_MSM_W, S_MSM_OUT, S_KMSM_CNT, S_KMSM_TOT, S_KMSM_LIST, S_KMSM_CHUNKS, S_KMSM_B, S_KMSM_P1,
   S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_BINV, S_NV, S_NVINV,
   S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_BINV_PRE, S_BINV_ROOTS, S_RC_UNI, S_RC_REF, S_RC_LIST, S_RS_DIG,
-  S_RC_NAF, S_RC_EV, S_RC_TAB, S_RC_D, S_RC_PINF, S_RC_DEN, S_RC_A, S_COUNT
+  S_RC_NAF, S_RC_EV, S_RC_TAB, S_RC_D, S_RC_PINF, S_RC_DEN, S_RC_A, S_PW, S_SLOTW, S_SFULL, S_STFULL, S_INC, S_PB, S_SLOTB,
+  S_SEED2, S_SB, S_STB, S_ISOB, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -302,16 +306,23 @@ struct Batch {
   uint32_t msg_len;
   const uint8_t* key_bytes;   // host: the key encoding(s) (48 B pk, or t x 48 B commits)
   size_t key_len;
-  uint32_t prefix_t = 0;  // Recover: after a failed batch, check items only up to each round's t-th valid one
+  bool item_pass = true;  // false (Recover's window): stop after the batch equation, verdicts in BatchOut
+};
+// what a batch without its per-item pass leaves for the caller (device pointers, valid in stream order)
+struct BatchOut {
+  const uint64_t* seed = nullptr;  // the bound coefficient seed
+  const uint32_t* flag = nullptr;  // flag[0]: the batch equation held
+  const uint8_t* iso = nullptr;    // N: items the equation did not cover (isolated)
+  uint32_t batched_sub = 0;        // 1: the G2 subgroup checks were batched (decode skipped them)
 };
 
 // The batch's coefficient seed (kernels.h k_digest_*): seed' = SHA-256(SHA-256(BE64 seed || key bytes) || D),
 // D = a SHA-256 tree over every (message, signature record) of the batch, left on the device.
-int bind_seed(const Batch& b, uint64_t seed, hipStream_t st, uint64_t** d_seed) {
+int bind_seed(const Batch& b, uint64_t seed, hipStream_t st, uint64_t** d_seed, Slot seed_slot = S_SEED) {
   const uint32_t N = b.R * b.k;
   static const bool no_bind = getenv("DG_NO_BIND") != nullptr;  // A/B diagnostics of the binding's cost only
   if (no_bind) {
-    RET(wsT(S_SEED, 16, d_seed));
+    RET(wsT(seed_slot, 16, d_seed));
     return launch("k_store_seed", k_store_seed, 1, 64, st, seed, *d_seed);
   }
   Sha256 h;
@@ -327,7 +338,7 @@ int bind_seed(const Batch& b, uint64_t seed, hipStream_t st, uint64_t** d_seed) 
   uint8_t *d0, *d1;
   RET(wsT(S_DIG0, (size_t)32 * N, &d0));
   RET(wsT(S_DIG1, (size_t)32 * ((N + 63) / 64) + 64, &d1));
-  RET(wsT(S_SEED, 16, d_seed));
+  RET(wsT(seed_slot, 16, d_seed));
   RET(launch("k_digest_items", k_digest_items, N, 128, st, N, b.k, b.msgs, b.msg_len, b.sigs, b.stride, d0));
   uint32_t n = N;
   while (n > 1) {
@@ -466,7 +477,30 @@ int msm_run_keyed(const Batch& b, const uint64_t* seed, const uint8_t* iso, bool
   return 0;
 }
 
-int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
+// sigma decode of n items (96 B at sigs + stride * i + offset) into S / status; the (round, slot) cell claim of
+// kernels.h (nslots = 0: no cell, every decoded item isolated); `sub`: the G2 subgroup check per item
+int decode_items(uint32_t N, uint32_t k, uint32_t nslots, const uint8_t* sigs, uint32_t stride, uint32_t offset,
+                 const uint32_t* item_slot, const uint8_t* key_status, G2AStore* S, uint8_t* status, uint32_t* cell,
+                 uint8_t* iso, uint32_t sub, hipStream_t st) {
+  if (g_ctx.phased) {
+    // phases.h: flags / x, the two roots through k_exp_pm3d4, then y, sign and the cell claim
+    DecState* ds;
+    Fp *ein, *eout;
+    RET(wsT(S_DECST, N, &ds));
+    RET(wsT(S_DEIN, N, &ein));
+    RET(wsT(S_DEOUT, N, &eout));
+    RET(launch("k_dec_p1", k_dec_p1, N, 128, st, N, sigs, stride, offset, item_slot, key_status, ds, ein, status));
+    RET(launch("k_exp_pm3d4", k_exp_pm3d4, N, 128, st, N, (const Fp*)ein, eout));
+    RET(launch("k_dec_p2", k_dec_p2, N, 128, st, N, ds, ein, (const Fp*)eout, status));
+    RET(launch("k_exp_pm3d4", k_exp_pm3d4, N, 128, st, N, (const Fp*)ein, eout));
+    return launch("k_dec_p3", k_dec_p3, N, 128, st, N, k, nslots, item_slot, (const DecState*)ds, (const Fp*)ein,
+                  (const Fp*)eout, S, status, cell, iso, sub);
+  }
+  return launch("k_decode_items", k_decode_items, N, 128, st, N, k, nslots, sigs, stride, offset, item_slot, key_status, S,
+                status, cell, iso, sub);
+}
+
+int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out = nullptr) {
   const uint32_t N = b.R * b.k;
   uint64_t* d_seed;
   RET(bind_seed(b, seed_in, st, &d_seed));
@@ -494,24 +528,8 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
   // flag[2]: the batch's failure flag beside the equation -- the batched subgroup check's window sums
   // (k_pair_miller_coop) and the affine MSM levels' input check (msm.h aff_input_ok) raise it
   HIPCHK(hipMemsetAsync(flag + 2, 0, 4, st));
-  if (g_ctx.phased) {
-    // phases.h: flags / x, the two roots through k_exp_pm3d4, then y, sign and the cell claim
-    DecState* ds;
-    Fp *ein, *eout;
-    RET(wsT(S_DECST, N, &ds));
-    RET(wsT(S_DEIN, N, &ein));
-    RET(wsT(S_DEOUT, N, &eout));
-    RET(launch("k_dec_p1", k_dec_p1, N, 128, st, N, b.sigs, b.stride, b.offset, b.item_slot, b.key_status, ds, ein,
-               b.status));
-    RET(launch("k_exp_pm3d4", k_exp_pm3d4, N, 128, st, N, (const Fp*)ein, eout));
-    RET(launch("k_dec_p2", k_dec_p2, N, 128, st, N, ds, ein, (const Fp*)eout, b.status));
-    RET(launch("k_exp_pm3d4", k_exp_pm3d4, N, 128, st, N, (const Fp*)ein, eout));
-    RET(launch("k_dec_p3", k_dec_p3, N, 128, st, N, b.k, b.nslots, b.item_slot, (const DecState*)ds, (const Fp*)ein,
-               (const Fp*)eout, b.S, b.status, cell, iso, 1u - batched_sub));
-  } else {
-    RET(launch("k_decode_items", k_decode_items, N, 128, st, N, b.k, b.nslots, b.sigs, b.stride, b.offset,
-               b.item_slot, b.key_status, b.S, b.status, cell, iso, 1u - batched_sub));
-  }
+  RET(decode_items(N, b.k, b.nslots, b.sigs, b.stride, b.offset, b.item_slot, b.key_status, b.S, b.status, cell, iso,
+                   1u - batched_sub, st));
   if (b.nslots == 1)
     RET(launch("k_scale_items", k_scale_items, N, 128, st, N, b.nslots, seed, b.item_slot, (const G2AStore*)b.S,
                (const uint8_t*)b.status, (const uint8_t*)iso, U));
@@ -561,6 +579,13 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
   // is one stream-ordered sequence of launches.
   HIPCHK(hipMemsetAsync(flag + 1, 0, 4, st));
   RET(launch("k_any", k_any, N, 256, st, N, (const uint8_t*)iso, flag + 1));
+  if (!b.item_pass) {
+    out->seed = seed;
+    out->flag = flag;
+    out->iso = iso;
+    out->batched_sub = batched_sub;
+    return 0;
+  }
   G2AStore* H;
   RET(wsT(S_H, b.R, &H));
   RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, (const uint32_t*)flag, b.Q, H));
@@ -568,37 +593,10 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st) {
   Set& set = cur_set();
   const hipStream_t batch_st = st;
   HIPCHK(hipEventRecord(set.to_fb, batch_st));
-  st = g_ctx.fb_stream;
+  st = g_ctx.shared_fb ? batch_st : g_ctx.fb_stream;
   HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
-  if (b.prefix_t == 0) {
-    RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
-               (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status, batched_sub));
-  } else {
-    // Recover: per-item checks over the examined prefix only, in passes that grow it by each round's deficit;
-    // the last pass takes every unverified item before the t-th valid one, so the statuses Recover reads
-    // are exact.  A passed batch marks nothing (only isolated items can be pending).
-    // Up to GRP fresh items of a round are checked together (kernels.h verify_group); the members of a failed
-    // group, and everything in the last pass, are checked alone.  DG_GROUP=1 checks every item alone.
-    uint8_t* fin;
-    uint32_t* glist;
-    RET(wsT(S_FIN, N, &fin));
-    RET(wsT(S_LIST, 4 * ((size_t)N + 1), &glist));
-    RET(launch("k_prefix_init", k_prefix_init, N, 256, st, N, (const uint32_t*)flag, (const uint8_t*)iso,
-               (const uint8_t*)b.status, fin));
-    // An empty pass costs two launches of returning lanes; the speculative margins (k_prefix_groups) keep
-    // the non-empty ones to ~3 at 10% corruption (a pass model over the C5 pattern: 1.75 s of per-item
-    // checks alone -> ~1.05 s).
-    const uint32_t grp = group_size();
-    constexpr int kPasses = 8;
-    for (int pass = 0; pass <= kPasses; ++pass) {
-      HIPCHK(hipMemsetAsync(glist, 0, 4, st));
-      const uint32_t margin = grp < 2 ? 0u : (pass == 0 ? 6u : 2u);
-      RET(launch("k_prefix_groups", k_prefix_groups, b.R, 128, st, b.R, b.k, b.prefix_t, pass == kPasses ? 1u : 0u,
-                 grp, margin, (const uint8_t*)b.status, (const uint8_t*)fin, glist));
-      RET(launch("k_verify_groups", k_verify_groups, N, 64, st, b.k, (const uint32_t*)glist, seed, b.keys,
-                 b.item_slot, (const G2AStore*)H, (const G2AStore*)b.S, b.status, fin, batched_sub, g_ctx.gcount));
-    }
-  }
+  RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
+             (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status, batched_sub));
   HIPCHK(hipEventRecord(set.from_fb, st));
   st = batch_st;
   HIPCHK(hipStreamWaitEvent(st, set.from_fb, 0));
@@ -799,70 +797,201 @@ int poly_keys(const uint8_t* commits48, uint32_t t, const std::vector<uint32_t>&
   return 0;
 }
 
-// VerifyPartial over R rounds x k partials: keys X_i = PubPoly.Eval(i) for every distinct index
-int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const uint8_t* msgs, uint32_t msg_len,
-                        uint32_t k, const uint8_t* partials98, uint64_t seed, hipStream_t st, uint8_t** d_status,
-                        uint8_t** d_partials, G2AStore** d_S, uint32_t prefix_t = 0, bool on_device = false) {
+// Key slots of a VerifyPartial / Recover batch over R rounds x k partials (d_p: device records).  An index enters the
+// batch equation as its own key set only if it occurs in at least 1/8 of the rounds' first w partials (the batch's
+// items), and at most kMaxSlots of them (most frequent first): each set costs an MSM bucket array, a column of the
+// (round, key) cell map and possibly a correction pairing, so a signer that sends a fresh index every round must
+// not get one per index.  Items of the other indices, and every index seen only beyond the window, are checked on
+// their own (their verdicts stay exact).  Counts and first positions come from the device (k_index_scan: 2 x 256 KB
+// back to the host instead of a host pass over the partials); the slot table goes back up (256 KB).  keys: X_i =
+// PubPoly.Eval(i) for every distinct index of the R x k items; item_slot: every item's slot.
+int plan_slots(const uint8_t* commits48, uint32_t t, uint32_t R, uint32_t k, uint32_t w, const uint8_t* d_p,
+               hipStream_t st, G1AStore** keys, uint8_t** kst, uint32_t** d_itemslot, uint32_t* nslots_out) {
   const size_t N = (size_t)R * k;
-  uint8_t *d_m, *d_p, *kst;
-  if (on_device) {  // msgs and partials98 are device pointers (dg_recover_dev)
-    d_m = const_cast<uint8_t*>(msgs);
-    d_p = const_cast<uint8_t*>(partials98);
-  } else {
-    RET(upload(S_MSGS, msgs, (size_t)R * msg_len, &d_m, st));
-    RET(upload(S_IN1, partials98, N * 98, &d_p, st));
-  }
-  // Key slots.  An index enters the batch equation as its own key set only if it occurs in at least 1/8 of
-  // the rounds, and at most kMaxSlots of them (most frequent first): each set costs an MSM bucket array, a
-  // column of the (round, key) cell map and possibly a correction pairing, so a signer that sends a fresh
-  // index every round must not get one per index.  Items of the other indices are checked on their own
-  // (their verdicts stay exact).  Counts and first positions come from the device (k_index_scan: 2 x 256 KB
-  // back to the host instead of a host pass over the partials); the slot table goes back up (256 KB).
   uint32_t *d_cnt, *d_first;
   RET(wsT(S_IDXCNT, 65536, &d_cnt));
   RET(wsT(S_IDXFIRST, 65536, &d_first));
   HIPCHK(hipMemsetAsync(d_cnt, 0, 65536 * 4, st));
   HIPCHK(hipMemsetAsync(d_first, 0xff, 65536 * 4, st));
-  RET(launch("k_index_scan", k_index_scan, (uint32_t)N, 256, st, (uint32_t)N, (const uint8_t*)d_p, d_cnt, d_first));
+  RET(launch("k_index_scan", k_index_scan, (uint32_t)N, 256, st, (uint32_t)N, k, w, d_p, d_cnt, d_first));
   std::vector<uint32_t> count(65536), first(65536);
   HIPCHK(hipMemcpyAsync(count.data(), d_cnt, 65536 * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(first.data(), d_first, 65536 * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   std::vector<uint32_t> distinct;
   for (uint32_t idx = 0; idx < 65536; ++idx)
-    if (count[idx]) distinct.push_back(idx);
+    if (first[idx] != ~0u) distinct.push_back(idx);
   std::stable_sort(distinct.begin(), distinct.end(), [&](uint32_t a, uint32_t b) { return count[a] > count[b]; });
   constexpr uint32_t kMaxSlots = 1024;
   uint32_t nslots = 0;
-  while (nslots < distinct.size() && nslots < kMaxSlots && (nslots == 0 || (size_t)count[distinct[nslots]] * 8 >= R))
+  while (nslots < distinct.size() && nslots < kMaxSlots && count[distinct[nslots]] > 0 &&
+         (nslots == 0 || (size_t)count[distinct[nslots]] * 8 >= R))
     ++nslots;
+  if (nslots == 0) nslots = 1;  // (no item in the window: one empty key set)
   // slots in first-occurrence order within each class (batched, alone), so the usual batch keeps the
   // input's index order
-  std::vector<uint32_t> slot_idx(distinct.begin(), distinct.begin() + nslots);
-  std::vector<uint32_t> alone(distinct.begin() + nslots, distinct.end());
+  std::vector<uint32_t> slot_idx(distinct.begin(), distinct.begin() + std::min<size_t>(nslots, distinct.size()));
+  std::vector<uint32_t> alone(distinct.begin() + slot_idx.size(), distinct.end());
   auto by_first = [&](uint32_t a, uint32_t b) { return first[a] < first[b]; };
   std::sort(slot_idx.begin(), slot_idx.end(), by_first);
   std::sort(alone.begin(), alone.end(), by_first);
   slot_idx.insert(slot_idx.end(), alone.begin(), alone.end());
   std::vector<int32_t> slot_of(65536, -1);
   for (size_t q = 0; q < slot_idx.size(); ++q) slot_of[slot_idx[q]] = (int32_t)q;
-  G1AStore* keys;
-  uint32_t* d_itemslot;
   int32_t* d_slotof;
-  RET(poly_keys(commits48, t, slot_idx, st, &keys, &kst));
+  RET(poly_keys(commits48, t, slot_idx, st, keys, kst));
   RET(upload(S_SLOTOF, slot_of.data(), 65536, &d_slotof, st));
-  RET(wsT(S_ITEMSLOT, N, &d_itemslot));
-  RET(launch("k_item_slots", k_item_slots, (uint32_t)N, 256, st, (uint32_t)N, (const uint8_t*)d_p,
-             (const int32_t*)d_slotof, d_itemslot));
-  G2JStore* Q;
-  RET(hash_rounds(R, d_m, msg_len, st, &Q));
-  RET(wsT(S_S, N, d_S));
-  RET(wsT(S_STATUS, N, d_status));
-  Batch b{R, k, nslots, Q, keys, kst, d_itemslot, d_p, 98, 2, *d_S, *d_status, d_m, msg_len, commits48, (size_t)t * 48};
-  b.prefix_t = prefix_t;
-  RET(batch_verify(b, seed, st));
-  *d_partials = d_p;
+  RET(wsT(S_ITEMSLOT, N, d_itemslot));
+  RET(launch("k_item_slots", k_item_slots, (uint32_t)N, 256, st, (uint32_t)N, d_p, (const int32_t*)d_slotof,
+             *d_itemslot));
+  *nslots_out = nslots;
   return 0;
+}
+
+// VerifyPartial over R rounds x k partials: keys X_i = PubPoly.Eval(i) for every distinct index
+int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const uint8_t* msgs, uint32_t msg_len,
+                        uint32_t k, const uint8_t* partials98, uint64_t seed, hipStream_t st, uint8_t** d_status) {
+  const size_t N = (size_t)R * k;
+  uint8_t *d_m, *d_p, *kst;
+  RET(upload(S_MSGS, msgs, (size_t)R * msg_len, &d_m, st));
+  RET(upload(S_IN1, partials98, N * 98, &d_p, st));
+  G1AStore* keys;
+  uint32_t *d_itemslot, nslots;
+  RET(plan_slots(commits48, t, R, k, k, d_p, st, &keys, &kst, &d_itemslot, &nslots));
+  G2JStore* Q;
+  G2AStore* S;
+  RET(hash_rounds(R, d_m, msg_len, st, &Q));
+  RET(wsT(S_S, N, &S));
+  RET(wsT(S_STATUS, N, d_status));
+  Batch b{R, k, nslots, Q, keys, kst, d_itemslot, d_p, 98, 2, S, *d_status, d_m, msg_len, commits48, (size_t)t * 48};
+  return batch_verify(b, seed, st);
+}
+
+// Recover's per-item pass over the examined prefix (on the per-item stream, ordered after and before the batch's
+// stream).  Recover (kyber tbls.Recover) checks the partials of a round in input order and stops at the t-th valid
+// one, so only the items up to that point need a verdict: about t / (1 - corrupted fraction) of the k.  Passes grow
+// the prefix by each round's deficit; the last takes every unverified item before the t-th valid one, so the
+// statuses Recover reads are exact.  Up to GRP fresh items of a round are checked together (kernels.h
+// verify_group); the members of a failed group, and everything in the last pass, are checked alone.  DG_GROUP=1
+// checks every item alone.  fin: FIN_DONE for the final verdicts, FIN_PENDING for the rest.
+int prefix_pass(uint32_t R, uint32_t k, uint32_t t, const uint64_t* seed, const G1AStore* keys, const uint32_t* item_slot,
+                const G2AStore* H, const G2AStore* S, uint8_t* status, uint8_t* fin, uint32_t subgroup, hipStream_t batch_st) {
+  const size_t N = (size_t)R * k;
+  Set& set = cur_set();
+  HIPCHK(hipEventRecord(set.to_fb, batch_st));
+  const hipStream_t st = g_ctx.shared_fb ? batch_st : g_ctx.fb_stream;
+  HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
+  uint32_t* glist;
+  RET(wsT(S_LIST, 4 * (N + 1), &glist));
+  // An empty pass costs two launches of returning lanes; the speculative margins (k_prefix_groups) keep the
+  // non-empty ones to ~3 at 10% corruption (a pass model over the C5 pattern: 1.75 s of per-item checks alone ->
+  // ~1.05 s).
+  const uint32_t grp = group_size();
+  constexpr int kPasses = 8;
+  for (int pass = 0; pass <= kPasses; ++pass) {
+    HIPCHK(hipMemsetAsync(glist, 0, 4, st));
+    const uint32_t margin = grp < 2 ? 0u : (pass == 0 ? 6u : 2u);
+    RET(launch("k_prefix_groups", k_prefix_groups, R, 128, st, R, k, t, pass == kPasses ? 1u : 0u, grp, margin,
+               (const uint8_t*)status, (const uint8_t*)fin, glist));
+    RET(launch("k_verify_groups", k_verify_groups, (uint32_t)N, 64, st, k, (const uint32_t*)glist, seed, keys, item_slot,
+               H, S, status, fin, subgroup, g_ctx.gcount));
+  }
+  HIPCHK(hipEventRecord(set.from_fb, st));
+  HIPCHK(hipStreamWaitEvent(batch_st, set.from_fb, 0));
+  return 0;
+}
+
+// Recover's VerifyPartial verdicts, examined prefix first.  The batch equation covers the first w = min(t, k)
+// partials of every round (gathered into an R x w table).  When it holds and every window item decoded -- every
+// round of a valid chain -- each round's first t partials are valid, which is all kyber's Recover examines
+// (beacon/beacon.go:488): the other k - w are never decoded.  Otherwise the items beyond the window are decoded
+// (beside the window's into the R x k tables) and the per-item pass decides every verdict of the examined prefix,
+// with coefficients bound to all R x k items.  Outputs: the R x k statuses and decoded sigmas (items beyond the
+// window of a complete round are left unset: Recover never reads them).
+int recover_windowed(const uint8_t* commits48, uint32_t t, uint32_t R, const uint8_t* d_m, uint32_t msg_len, uint32_t k,
+                     const uint8_t* d_p, uint64_t seed, hipStream_t st, uint8_t** d_status, G2AStore** d_S) {
+  const uint32_t w = t < k ? t : k;
+  const size_t N = (size_t)R * k, Nw = (size_t)R * w;
+  if (N * 49 > 0x7fffffffull) return fail(DG_E_ARG, "Recover batch too large (rounds x k >= 2^31 / 49)");
+  uint8_t* kst;
+  G1AStore* keys;
+  uint32_t *d_itemslot, nslots;
+  RET(plan_slots(commits48, t, R, k, w, d_p, st, &keys, &kst, &d_itemslot, &nslots));
+  const uint8_t* d_pw = d_p;
+  const uint32_t* d_slotw = d_itemslot;
+  if (w < k) {
+    uint16_t* pw;
+    uint32_t* sw;
+    RET(wsT(S_PW, Nw * 49, &pw));
+    RET(wsT(S_SLOTW, Nw, &sw));
+    RET(launch("k_rows", k_rows<uint16_t>, (uint32_t)(Nw * 49), 256, st, R, w, 49u, k, 0u, w, 0u, (const uint16_t*)d_p, pw));
+    RET(launch("k_rows", k_rows<uint32_t>, (uint32_t)Nw, 256, st, R, w, 1u, k, 0u, w, 0u, (const uint32_t*)d_itemslot, sw));
+    d_pw = (const uint8_t*)pw;
+    d_slotw = sw;
+  }
+  G2JStore* Q;
+  G2AStore* Sw;
+  uint8_t* stw;
+  RET(hash_rounds(R, d_m, msg_len, st, &Q));
+  RET(wsT(S_S, Nw, &Sw));
+  RET(wsT(S_STATUS, Nw, &stw));
+  Batch bw{R, w, nslots, Q, keys, kst, d_slotw, d_pw, 98, 2, Sw, stw, d_m, msg_len, commits48, (size_t)t * 48};
+  bw.item_pass = false;
+  BatchOut bo;
+  RET(batch_verify(bw, seed, st, &bo));
+  // the window's verdicts into the R x k tables
+  G2AStore* S;
+  uint8_t *status, *fin;
+  uint32_t* inc;
+  RET(wsT(S_SFULL, N, &S));
+  RET(wsT(S_STFULL, N, &status));
+  RET(wsT(S_FIN, N, &fin));
+  RET(wsT(S_INC, 4, &inc));
+  HIPCHK(hipMemsetAsync(inc, 0, 16, st));
+  constexpr uint32_t kQ = sizeof(G2AStore) / 16;
+  static_assert(sizeof(G2AStore) % 16 == 0, "G2AStore rows move as uint4");
+  RET(launch("k_rows", k_rows<uint4>, (uint32_t)(Nw * kQ), 256, st, R, w, kQ, w, 0u, k, 0u, (const uint4*)Sw, (uint4*)S));
+  RET(launch("k_window_fin", k_window_fin, (uint32_t)Nw, 256, st, R, k, 0u, w, bo.flag, bo.iso, (const uint8_t*)stw,
+             status, fin, inc));
+  uint32_t inc_h = 0;
+  HIPCHK(hipMemcpyAsync(&inc_h, inc, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  *d_status = status;
+  *d_S = S;
+  if (inc_h == 0) return 0;
+  // Slow path: decode the items beyond the window (their verdicts are pending until checked)
+  const uint64_t* pseed = bo.seed;
+  if (w < k) {
+    const uint32_t kb = k - w;
+    const size_t Nb = (size_t)R * kb;
+    uint16_t* pb;
+    uint32_t* sb;
+    G2AStore* Sb;
+    uint8_t *stb, *isob;
+    RET(wsT(S_PB, Nb * 49, &pb));
+    RET(wsT(S_SLOTB, Nb, &sb));
+    RET(launch("k_rows", k_rows<uint16_t>, (uint32_t)(Nb * 49), 256, st, R, kb, 49u, k, w, kb, 0u, (const uint16_t*)d_p, pb));
+    RET(launch("k_rows", k_rows<uint32_t>, (uint32_t)Nb, 256, st, R, kb, 1u, k, w, kb, 0u, (const uint32_t*)d_itemslot, sb));
+    RET(wsT(S_SB, Nb, &Sb));
+    RET(wsT(S_STB, Nb, &stb));
+    RET(wsT(S_ISOB, Nb, &isob));
+    RET(decode_items((uint32_t)Nb, kb, 0u, (const uint8_t*)pb, 98, 2, sb, kst, Sb, stb, inc + 2, isob,
+                     1u - bo.batched_sub, st));
+    RET(launch("k_rows", k_rows<uint4>, (uint32_t)(Nb * kQ), 256, st, R, kb, kQ, kb, 0u, k, w, (const uint4*)Sb, (uint4*)S));
+    RET(launch("k_window_fin", k_window_fin, (uint32_t)Nb, 256, st, R, k, w, kb, (const uint32_t*)nullptr,
+               (const uint8_t*)isob, (const uint8_t*)stb, status, fin, inc + 1));
+    // the group tests' coefficients bound to every item they may check
+    uint64_t* s2;
+    Batch bf{R, k, nslots, Q, keys, kst, d_itemslot, d_p, 98, 2, S, status, d_m, msg_len, commits48, (size_t)t * 48};
+    RET(bind_seed(bf, seed ^ 0x77696e646f77ull, st, &s2, S_SEED2));
+    pseed = s2;
+  }
+  G2AStore* H;
+  RET(wsT(S_H, R, &H));
+  HIPCHK(hipMemsetAsync(inc + 2, 0, 8, st));  // k_clear_rounds: flag {0, 0} = clear every round
+  RET(launch("k_clear_rounds", k_clear_rounds, R, 128, st, R, (const uint32_t*)(inc + 2), (const G2JStore*)Q, H));
+  RET(prefix_pass(R, k, t, pseed, keys, d_itemslot, H, S, status, fin, bo.batched_sub, st));
+  return launch("k_count_fallback", k_count_fallback, 1, 64, st, bo.flag, g_ctx.fallbacks);
 }
 
 // Recover's divergent rounds (recover.h k_rs_*): the rounds nl[0..Rn) of the blocks whose rounds selected different
@@ -1032,26 +1161,37 @@ int dg_init(int device) {
   HIPCHK(hipFuncGetAttributes(&fa_items, reinterpret_cast<const void*>(k_verify_items)));
   HIPCHK(hipFuncGetAttributes(&fa_groups, reinterpret_cast<const void*>(k_verify_groups)));
   const bool items_first = fa_items.localSizeBytes > fa_groups.localSizeBytes;
-  for (int pass = 0; pass < 2; ++pass) {
-    if ((pass == 0) == items_first) {
-      hipLaunchKernelGGL(k_verify_items, dim3(1), dim3(64), 0, g_ctx.fb_stream, 0u, 1u, (const uint32_t*)nullptr,
-                         (const G1AStore*)nullptr, (const uint32_t*)nullptr, (const G2AStore*)nullptr,
-                         (const G2AStore*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, 0u);
-    } else {
-      // glist[0] = 0 (the zeroed fallback counter): no groups
-      hipLaunchKernelGGL(k_verify_groups, dim3(1), dim3(64), 0, g_ctx.fb_stream, 1u, (const uint32_t*)g_ctx.fallbacks,
-                         (const uint64_t*)nullptr, (const G1AStore*)nullptr, (const uint32_t*)nullptr,
-                         (const G2AStore*)nullptr, (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr,
-                         0u, g_ctx.gcount);
+  auto prewarm_items = [&](hipStream_t q) {
+    for (int pass = 0; pass < 2; ++pass) {
+      if ((pass == 0) == items_first) {
+        hipLaunchKernelGGL(k_verify_items, dim3(1), dim3(64), 0, q, 0u, 1u, (const uint32_t*)nullptr,
+                           (const G1AStore*)nullptr, (const uint32_t*)nullptr, (const G2AStore*)nullptr,
+                           (const G2AStore*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, 0u);
+      } else {
+        // glist[0] = 0 (the zeroed fallback counter): no groups
+        hipLaunchKernelGGL(k_verify_groups, dim3(1), dim3(64), 0, q, 1u, (const uint32_t*)g_ctx.fallbacks,
+                           (const uint64_t*)nullptr, (const G1AStore*)nullptr, (const uint32_t*)nullptr,
+                           (const G2AStore*)nullptr, (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr,
+                           0u, g_ctx.gcount);
+      }
     }
-  }
-  HIPCHK(hipGetLastError());
-  for (Set& x : g_ctx.sets) {
-    // n = 0: every lane returns
-    hipLaunchKernelGGL(k_sign, dim3(1), dim3(128), 0, x.stream, 0u, (const uint8_t*)nullptr, (const uint16_t*)nullptr,
-                       (const uint8_t*)nullptr, 0u, (const uint8_t*)nullptr, 0u, (uint8_t*)nullptr);
+  };
+  // only the active sets' streams are dispatched to (a stream takes a hardware queue at its first dispatch), the
+  // per-item stream after them: with more streams than hardware queues (GPU_MAX_HW_QUEUES, default 4) streams
+  // share queues, and a cross-stream wait queued on a shared queue holds every stream behind it
+  for (int i = 0; i < active_sets(); ++i) {
+    Set& x = g_ctx.sets[i];
+    if (g_ctx.shared_fb) {
+      prewarm_items(x.stream);
+    } else {
+      // n = 0: every lane returns
+      hipLaunchKernelGGL(k_sign, dim3(1), dim3(128), 0, x.stream, 0u, (const uint8_t*)nullptr, (const uint16_t*)nullptr,
+                         (const uint8_t*)nullptr, 0u, (const uint8_t*)nullptr, 0u, (uint8_t*)nullptr);
+    }
     HIPCHK(hipGetLastError());
   }
+  if (!g_ctx.shared_fb) prewarm_items(g_ctx.fb_stream);
+  HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   g_ctx.device = device;
   g_ctx.ready = true;
@@ -1466,10 +1606,9 @@ int dg_verify_partials(const uint8_t* commits48, uint32_t t, size_t rounds, cons
   RET(check_args_n(rounds * (size_t)k));
   hipStream_t st;
   RET(acquire_set(&st));
-  uint8_t *d_st, *d_p;
-  G2AStore* d_S;
+  uint8_t* d_st;
   RET(verify_partials_dev(commits48, t, (uint32_t)rounds, msgs, (uint32_t)msg_len, k, partials98, fresh_seed(seed), st,
-                          &d_st, &d_p, &d_S));
+                          &d_st));
   HIPCHK(hipMemcpyAsync(status, d_st, rounds * k, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if (g_ctx.timing) collect_timings();
@@ -1489,10 +1628,11 @@ int dg_recover(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t ro
   hipStream_t st;
   RET(acquire_set(&st));
   const uint32_t R = (uint32_t)rounds;
-  uint8_t *d_st, *d_p;
+  uint8_t *d_st, *d_m, *d_p;
   G2AStore* d_S;
-  RET(verify_partials_dev(commits48, t, R, msgs, (uint32_t)msg_len, k, partials98, fresh_seed(seed), st, &d_st, &d_p,
-                          &d_S, t));
+  RET(upload(S_MSGS, msgs, (size_t)R * msg_len, &d_m, st));
+  RET(upload(S_IN1, partials98, (size_t)R * k * 98, &d_p, st));
+  RET(recover_windowed(commits48, t, R, d_m, (uint32_t)msg_len, k, d_p, fresh_seed(seed), st, &d_st, &d_S));
   return recover_tail(R, k, t, d_p, d_st, d_S, out_sig96, round_status, share_status, st);
 }
 
@@ -1510,11 +1650,10 @@ int dg_recover_dev(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_
   hipStream_t st;
   RET(acquire_set(&st));
   const uint32_t R = (uint32_t)rounds;
-  uint8_t *d_st, *d_p;
+  uint8_t* d_st;
   G2AStore* d_S;
-  RET(verify_partials_dev(commits48, t, R, d_msgs, (uint32_t)msg_len, k, d_partials98, fresh_seed(seed), st, &d_st,
-                          &d_p, &d_S, t, true));
-  return recover_tail(R, k, t, d_p, d_st, d_S, d_out_sig96, d_round_status, d_share_status, st);
+  RET(recover_windowed(commits48, t, R, d_msgs, (uint32_t)msg_len, k, d_partials98, fresh_seed(seed), st, &d_st, &d_S));
+  return recover_tail(R, k, t, d_partials98, d_st, d_S, d_out_sig96, d_round_status, d_share_status, st);
 }
 
 int dg_recover_verified(uint32_t t, uint32_t nshares, size_t rounds, uint32_t k, const uint8_t* partials98,

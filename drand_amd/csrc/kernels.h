@@ -631,15 +631,38 @@ DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_groups(uint32_t k
                                                     uint8_t* fin, uint32_t subgroup, unsigned long long* cnt);
 #endif
 #if DG_TU_LIB
-// ---- Recover's per-item pass over the examined prefix only.  Recover (kyber tbls.Recover) checks the
-// partials of a round in input order and stops at the t-th valid one, so after a failed batch only the
-// items up to that point need their own pairing check: about t / (1 - corrupted fraction) of the k.
-// fin[i] = the verdict of item i is final (decode failure, or a passed batch and not isolated).
-DG_KERNEL void __launch_bounds__(256) k_prefix_init(uint32_t n, const uint32_t* flag, const uint8_t* isolate,
-                                                   const uint8_t* status, uint8_t* fin) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  fin[i] = (status[i] != DG_ST_OK_ || (flag[0] && !isolate[i])) ? 1 : 0;
+// ---- Recover's window (drand_gpu.hip recover_windowed).  kyber's tbls.Recover verifies the partials of a
+// round in input order and stops at the t-th valid one (beacon/beacon.go:488), so the batch equation first
+// covers only the first w = t partials of every round; the rest are decoded and checked only for the rounds
+// whose window did not yield t valid shares.  Rows of a round-major table move between the R x k layout of
+// the input and the R x w layout of a window: dst[(r kout + jout + j) ne + e] = src[(r kin + jin + j) ne + e].
+template <typename T>
+__global__ void __launch_bounds__(256) k_rows(uint32_t R, uint32_t w, uint32_t ne, uint32_t kin, uint32_t jin,
+                                            uint32_t kout, uint32_t jout, const T* src, T* dst) {
+  const size_t n = (size_t)R * w * ne;
+  const size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n) return;
+  const size_t item = x / ne;
+  const uint32_t e = (uint32_t)(x - item * ne), r = (uint32_t)(item / w), j = (uint32_t)(item - (size_t)r * w);
+  dst[((size_t)r * kout + jout + j) * ne + e] = src[((size_t)r * kin + jin + j) * ne + e];
+}
+// statuses of window items (r, j0 + j), j < w, into the R x k table, and whether each verdict is final: a decode
+// failure, or (window batch: flag != null) a passed batch equation and not isolated.  inc |= 1: an item is
+// pending (it needs its own check); inc |= 2: a window item is not valid while shares lie beyond the window
+// (kyber would go on to the next partial).
+DG_KERNEL void __launch_bounds__(256) k_window_fin(uint32_t R, uint32_t k, uint32_t j0, uint32_t w, const uint32_t* flag,
+                                                  const uint8_t* iso, const uint8_t* st_w, uint8_t* status,
+                                                  uint8_t* fin, uint32_t* inc) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * w) return;
+  const uint32_t r = i / w, f = r * k + j0 + (i - r * w);
+  const uint8_t st = st_w[i];
+  const bool done = st != DG_ST_OK_ || (flag && flag[0] && !iso[i]);
+  status[f] = st;
+  fin[f] = done ? FIN_DONE : FIN_PENDING;
+  uint32_t m = done ? 0u : 1u;
+  if (flag && st != DG_ST_OK_ && w < k) m |= 2u;
+  if (m) atomicOr(inc, m);
 }
 // per round: scanning in input order, the unverified items up to the point where the round would reach
 // t + margin valid shares if every fresh unverified item were valid and every member of a failed group (bad
@@ -688,12 +711,13 @@ DG_KERNEL void __launch_bounds__(128) k_prefix_groups(uint32_t R, uint32_t k, ui
 // Key-slot statistics of a VerifyPartial / Recover batch (drand_gpu.hip verify_partials_dev): per share
 // index its number of partials and its first position; then each item's slot from the host's slot table.
 #if DG_TU_LIB
-DG_KERNEL void __launch_bounds__(256) k_index_scan(uint32_t n, const uint8_t* partials98, uint32_t* count,
-                                                  uint32_t* first) {
+// (count: only the items of each round's first w of k, the window of a Recover batch; first: every item)
+DG_KERNEL void __launch_bounds__(256) k_index_scan(uint32_t n, uint32_t k, uint32_t w, const uint8_t* partials98,
+                                                  uint32_t* count, uint32_t* first) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t idx = (uint32_t)partials98[98ull * i] << 8 | partials98[98ull * i + 1];
-  atomicAdd(&count[idx], 1u);
+  if (i % k < w) atomicAdd(&count[idx], 1u);
   if (i < first[idx]) atomicMin(&first[idx], i);
 }
 DG_KERNEL void __launch_bounds__(256) k_item_slots(uint32_t n, const uint8_t* partials98, const int32_t* slot_of,
