@@ -64,7 +64,7 @@ struct Ctx {
   int device = -1;
   bool ready = false;
   Set sets[kSets];
-  // The per-item pairing kernels (k_verify_items, k_verify_groups: ~14.5 KB of private segment per lane) run on
+  // The per-item pairing kernels (k_verify_items, k_verify_groups: two-lane teams, team.h) run on
   // this one stream, whatever set the batch uses: a hardware queue reserves scratch for the largest private
   // segment dispatched on it, so only this stream's queue holds that reservation and the workspace sets'
   // queues stay at the ~5.7 KB of k_sign (with 8 hardware queues, every queue holding 14.5 KB failed
@@ -196,7 +196,7 @@ hipEvent_t get_event() {
 template <typename... Args>
 int launch(const char* name, void (*k)(Args...), uint32_t n_threads, uint32_t block, hipStream_t st, Args... args) {
   if (n_threads == 0) return 0;
-  uint32_t grid = (n_threads + block - 1) / block;
+  const uint32_t grid = (uint32_t)(((uint64_t)n_threads + block - 1) / block);
   Ctx& c = g_ctx;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c.timing) {
@@ -595,7 +595,7 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
   HIPCHK(hipEventRecord(set.to_fb, batch_st));
   st = g_ctx.shared_fb ? batch_st : g_ctx.fb_stream;
   HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
-  RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
+  RET(launch("k_verify_items", k_verify_items, 2 * N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
              (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status, batched_sub));
   HIPCHK(hipEventRecord(set.from_fb, st));
   st = batch_st;
@@ -893,7 +893,7 @@ int prefix_pass(uint32_t R, uint32_t k, uint32_t t, const uint64_t* seed, const 
     const uint32_t margin = grp < 2 ? 0u : (pass == 0 ? 6u : 2u);
     RET(launch("k_prefix_groups", k_prefix_groups, R, 128, st, R, k, t, pass == kPasses ? 1u : 0u, grp, margin,
                (const uint8_t*)status, (const uint8_t*)fin, glist));
-    RET(launch("k_verify_groups", k_verify_groups, (uint32_t)N, 64, st, k, (const uint32_t*)glist, seed, keys, item_slot,
+    RET(launch("k_verify_groups", k_verify_groups, (uint32_t)(2 * N), 64, st, k, (const uint32_t*)glist, seed, keys, item_slot,
                H, S, status, fin, subgroup, g_ctx.gcount));
   }
   HIPCHK(hipEventRecord(set.from_fb, st));
