@@ -64,7 +64,7 @@ struct Ctx {
   int device = -1;
   bool ready = false;
   Set sets[kSets];
-  // The per-item pairing kernels (k_verify_items, k_verify_groups: two-lane teams, team.h) run on
+  // The per-item pairing kernels (k_verify_items, k_verify_groups: ~14.5 KB of private segment per lane) run on
   // this one stream, whatever set the batch uses: a hardware queue reserves scratch for the largest private
   // segment dispatched on it, so only this stream's queue holds that reservation and the workspace sets'
   // queues stay at the ~5.7 KB of k_sign (with 8 hardware queues, every queue holding 14.5 KB failed
@@ -142,7 +142,7 @@ enum Slot {
   S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_BINV, S_NV, S_NVINV,
   S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_BINV_PRE, S_BINV_ROOTS, S_RC_UNI, S_RC_REF, S_RC_LIST, S_RS_DIG,
   S_RC_NAF, S_RC_EV, S_RC_TAB, S_RC_D, S_RC_PINF, S_RC_DEN, S_RC_A, S_PW, S_SLOTW, S_SFULL, S_STFULL, S_INC, S_PB, S_SLOTB,
-  S_SEED2, S_SB, S_STB, S_ISOB, S_COUNT
+  S_SEED2, S_SB, S_STB, S_ISOB, S_KMSM_GOFS, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -445,7 +445,6 @@ int msm_run_keyed(const Batch& b, const uint64_t* seed, const uint8_t* iso, bool
   const size_t max_chunks_sz = ((size_t)nwin * N) / KMSM_CHUNK + 1 + nkeys;
   if (max_chunks_sz > 0xffffffffull) return fail(DG_E_ARG, "batch too large for the keyed MSM");
   const uint32_t max_chunks = (uint32_t)max_chunks_sz;
-  RET(wsT(S_KMSM_CHUNKS, max_chunks, &chunks));
   RET(wsT(S_KMSM_B, nkeys, &B));
   RET(wsT(S_KMSM_P1, (size_t)nsets * nwin * MSM_C * 16, &P1));
   RET(wsT(S_KMSM_TMP, (size_t)nsets * nwin * MSM_C * 16, &tmp));
@@ -455,17 +454,49 @@ int msm_run_keyed(const Batch& b, const uint64_t* seed, const uint8_t* iso, bool
   HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * nkeys, st));
   RET(launch("k_kmsm_count", k_kmsm_count, N, 256, st, N, b.k, nsets, nwin, seed, b.item_slot, (const uint8_t*)b.status,
              iso, cnt));
-  RET(launch("k_kscan_local", k_kscan_local, nblocks * 256, 256, st, nkeys, (const uint32_t*)cnt, offset, chunk_off,
-             tot));
-  RET(launch("k_kscan_top", k_kscan_top, 64, 64, st, nblocks, nkeys, tot, chunk_off));
-  RET(launch("k_kscan_add", k_kscan_add, nkeys, 256, st, nkeys, (const uint32_t*)tot, offset, cursor, chunk_off));
+  const size_t E = (size_t)nwin * N;
+  const bool aff = !g_ctx.msm_jac && E + nkeys < 0x7fffffffull;  // affine first levels (DG_MSM_JAC=1: chunk sums)
+  auto scan = [&](uint32_t div, uint32_t* groups) -> int {
+    RET(launch("k_kscan_local", k_kscan_local, nblocks * 256, 256, st, nkeys, div, (const uint32_t*)cnt, offset, groups,
+               tot));
+    RET(launch("k_kscan_top", k_kscan_top, 64, 64, st, nblocks, nkeys, tot, groups));
+    return launch("k_kscan_add", k_kscan_add, nkeys, 256, st, nkeys, (const uint32_t*)tot, offset, cursor, groups);
+  };
+  uint32_t* gofs = nullptr;
+  if (aff) {
+    RET(wsT(S_KMSM_GOFS, (size_t)MSM_AFF_L * (nkeys + 1), &gofs));
+    for (uint32_t l = 0; l < MSM_AFF_L; ++l) RET(scan(2u << l, gofs + (size_t)l * (nkeys + 1)));
+  } else {
+    RET(scan(KMSM_CHUNK, chunk_off));
+  }
   RET(launch("k_kmsm_scatter", k_kmsm_scatter, N, 256, st, N, b.k, nsets, nwin, seed, b.item_slot,
              (const uint8_t*)b.status, iso, cursor, list));
-  RET(launch("k_kmsm_chunks", k_kmsm_chunks, max_chunks, 128, st, max_chunks, nkeys, (const uint32_t*)cnt,
-             (const uint32_t*)offset, (const uint32_t*)chunk_off, (const uint32_t*)list, (const G2AStore*)b.S,
-             chunks));
-  RET(launch("k_kmsm_buckets", k_kmsm_buckets, nkeys, 128, st, nkeys, (const uint32_t*)chunk_off,
-             (const G2JStore*)chunks, B));
+  if (aff) {
+    G2AStore* A;
+    Fp *den, *dinv;
+    const uint32_t maxg0 = (uint32_t)(E / 2) + nkeys;
+    RET(wsT(S_MSM_AFF, E, &A));
+    RET(wsT(S_MSM_DEN, maxg0, &den));
+    RET(wsT(S_MSM_DINV, maxg0, &dinv));
+    for (uint32_t l = 0; l < MSM_AFF_L; ++l) {
+      const uint32_t maxg = (uint32_t)(E >> (l + 1)) + nkeys;
+      const uint32_t* gl = gofs + (size_t)l * (nkeys + 1);
+      RET(launch("k_kmsm_aff_den", k_kmsm_aff_den, maxg, 128, st, l, maxg, nkeys, (const uint32_t*)cnt,
+                 (const uint32_t*)offset, gl, (const uint32_t*)list, (const G2AStore*)b.S, (const G2AStore*)A, den));
+      RET(batch_inv(maxg, den, dinv, st));
+      RET(launch("k_kmsm_aff_add", k_kmsm_aff_add, maxg, 128, st, l, maxg, nkeys, (const uint32_t*)cnt,
+                 (const uint32_t*)offset, gl, (const uint32_t*)list, (const G2AStore*)b.S, A, (const Fp*)dinv));
+    }
+    RET(launch("k_kmsm_buckets_aff", k_kmsm_buckets_aff, nkeys, 128, st, nkeys, (const uint32_t*)cnt,
+               (const uint32_t*)offset, (const G2AStore*)A, B));
+  } else {
+    RET(wsT(S_KMSM_CHUNKS, max_chunks, &chunks));
+    RET(launch("k_kmsm_chunks", k_kmsm_chunks, max_chunks, 128, st, max_chunks, nkeys, (const uint32_t*)cnt,
+               (const uint32_t*)offset, (const uint32_t*)chunk_off, (const uint32_t*)list, (const G2AStore*)b.S,
+               chunks));
+    RET(launch("k_kmsm_buckets", k_kmsm_buckets, nkeys, 128, st, nkeys, (const uint32_t*)chunk_off,
+               (const G2JStore*)chunks, B));
+  }
   RET(launch("k_kmsm_slices", k_kmsm_slices, nsets * nwin * MSM_C * 16, 128, st, nsets, nwin, (const G2JStore*)B, P1));
   RET(reduce_rows(P1, tmp, nsets * nwin * MSM_C, 16, st));  // S[set][w][k] = P1[...]
   RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * nwin * nsets, 128, st, nwin, nsets, (const G2JStore*)P1, W));
@@ -595,7 +626,7 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
   HIPCHK(hipEventRecord(set.to_fb, batch_st));
   st = g_ctx.shared_fb ? batch_st : g_ctx.fb_stream;
   HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
-  RET(launch("k_verify_items", k_verify_items, 2 * N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
+  RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
              (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status, batched_sub));
   HIPCHK(hipEventRecord(set.from_fb, st));
   st = batch_st;
@@ -893,7 +924,7 @@ int prefix_pass(uint32_t R, uint32_t k, uint32_t t, const uint64_t* seed, const 
     const uint32_t margin = grp < 2 ? 0u : (pass == 0 ? 6u : 2u);
     RET(launch("k_prefix_groups", k_prefix_groups, R, 128, st, R, k, t, pass == kPasses ? 1u : 0u, grp, margin,
                (const uint8_t*)status, (const uint8_t*)fin, glist));
-    RET(launch("k_verify_groups", k_verify_groups, (uint32_t)(2 * N), 64, st, k, (const uint32_t*)glist, seed, keys, item_slot,
+    RET(launch("k_verify_groups", k_verify_groups, (uint32_t)N, 64, st, k, (const uint32_t*)glist, seed, keys, item_slot,
                H, S, status, fin, subgroup, g_ctx.gcount));
   }
   HIPCHK(hipEventRecord(set.from_fb, st));

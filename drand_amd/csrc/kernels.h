@@ -6,7 +6,6 @@
 #include "pairing.h"
 #include "fr.h"
 #include "coop.h"
-#include "team.h"
 
 #ifndef DG_HOT_WAVES
 #define DG_HOT_WAVES 2  // min waves per SIMD for the hot kernels: 256 VGPRs each (measured: 2 beats 1 by 6%)
@@ -506,59 +505,47 @@ constexpr uint32_t GRP = 4;
 constexpr uint8_t FIN_PENDING = 0, FIN_DONE = 1, FIN_RECHECK = 2;
 constexpr uint64_t GROUP_TAG = 0x67726f7570746573ull;  // domain of rho_i, apart from alpha_r and beta_s
 #if DG_TU_VERIFY
-// The per-item pairing checks run on two-lane teams (team.h): lane 0 holds the pair (x, H_r), lane 1 the pair
-// (-g1, s) of the check e(x, H_r) e(-g1, s) == 1, and each lane half of every GT value.  Threads 2j, 2j+1 are
-// one check; a team leaves or branches only as a whole around the team.h calls (their DPP moves read the partner
-// lane's registers).
-DGI G1A g1_neg_gen() { return G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false}; }
-// c ? a : b
-DGI G1A g1a_pick(bool c, const G1A& a, const G1A& b) { return G1A{fp_sel(c, b.x, a.x), fp_sel(c, b.y, a.y), c ? a.inf : b.inf}; }
-DGI G2A g2a_pick(bool c, const G2A& a, const G2A& b) { return G2A{fp2_pick(c, a.x, b.x), fp2_pick(c, a.y, b.y), c ? a.inf : b.inf}; }
-DGI G2A t2_x(const G2A& a) { return G2A{t2_x(a.x), t2_x(a.y), t2_x((uint32_t)a.inf) != 0u}; }
-DGI G1J t2_x(const G1J& a) { return G1J{t2_x(a.x), t2_x(a.y), t2_x(a.z)}; }
-DGI G2J t2_x(const G2J& a) { return G2J{t2_x(a.x), t2_x(a.y), t2_x(a.z)}; }
-// the team's check of e(x, h) e(-g1, s) == 1 (pairs with an identity dropped, as in kyber's bls.Verify)
-DGI bool t2_verify_eq(const G1A& x, const G2A& hq, const G2A& s, uint32_t h) {
-  const G1A P = g1a_pick(h, g1_neg_gen(), x);
-  const G2A Q = g2a_pick(h, s, hq);
-  const bool present = h ? !s.inf : (!x.inf && !hq.inf);
-  return t2_pair_check(P, Q, present, h);
+// the Miller loop out of line, so its state and the final exponentiation's do not share one stack frame
+// (the per-item kernels' private segment must stay under the queue's scratch limit: ~14 KB per lane)
+DGN Fp12 miller_loop2(const G1A* P, const G2A* Q, int np) { return miller_loop<2>(P, Q, np); }
+// e(x, h) * e(-g1, s) == 1 (the identity's pairings dropped): kyber's bls.Verify equation
+DGN bool pair_check(const G1A& x, const G2A& h, const G2A& s) {
+  G1A P[2];
+  G2A Qa[2];
+  int np = 0;
+  if (!x.inf && !h.inf) {
+    P[np] = x;
+    Qa[np] = h;
+    ++np;
+  }
+  if (!s.inf) {
+    P[np] = G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false};
+    Qa[np] = s;
+    ++np;
+  }
+  return np == 0 ? true : fp12_is_one(final_exp_cubed(miller_loop2(P, Qa, np)));
 }
-// individual bls.Verify of item i: e(X_slot, H_{i/k}) == e(g1, S_i); with `subgroup` the decode skipped the
-// per-item G2 subgroup check (batched on the MSM windows), so it is done here (both lanes: the verdict is the
-// team's): a sigma outside G2 is a decode error, as in g2_decompress
 DGN void verify_item(size_t i, uint32_t k, const G1AStore* keys, const uint32_t* item_slot, const G2AStore* H,
-                     const G2AStore* S, uint8_t* status, uint32_t subgroup, uint32_t h) {
+                     const G2AStore* S, uint8_t* status, uint32_t subgroup) {
   const G2A s = load_g2a(S[i]);
   if (subgroup && !s.inf && !g2_in_subgroup_aff(s.x, s.y)) {
-    if (h == 0) status[i] = DG_ST_SIG_DECODE_;
+    status[i] = DG_ST_SIG_DECODE_;
     return;
   }
-  const bool good = t2_verify_eq(load_g1a(keys[item_slot ? item_slot[i] : 0u]), load_g2a(H[i / k]), s, h);
-  if (h == 0) status[i] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
+  const bool good = pair_check(load_g1a(keys[item_slot ? item_slot[i] : 0u]), load_g2a(H[i / k]), s);
+  status[i] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
 }
 
-// Group tests of Recover's examined prefix: up to GRP members of one round checked together,
-// e(sum rho_i X_i, H_r) == e(g1, sum rho_i S_i).  Lane h takes members h and h + 2: their subgroup checks and
-// its half of both random linear combinations (two-point sign-aligned column sums); the halves cross once.  A
-// single (n == 1) is member 0 on lane 0.
-DGN void verify_group(const uint32_t* mem, uint32_t n, uint32_t k, uint64_t seed, const G1AStore* keys,
-                      const uint32_t* item_slot, const G2AStore* H, const G2AStore* S, uint8_t* status,
-                      uint8_t* fin, uint32_t subgroup, uint32_t h) {
+// the members' weighted sums a = sum rho_i X_i, b = sum rho_i S_i; members failing the subgroup check are
+// decided here (decode error) and left out.  Returns the live members (their item indices in live[]).
+DGN uint32_t group_combine(const uint32_t* mem, uint32_t n, uint64_t seed, const G1AStore* keys,
+                           const uint32_t* item_slot, const G2AStore* S, uint8_t* status, uint8_t* fin,
+                           uint32_t subgroup, G1A& a, G2A& b, uint32_t* live) {
   G1J xp[GRP];
   G2J sp[GRP];
   uint64_t rho[GRP];
-  uint32_t live = 0, mine[2] = {~0u, ~0u};
-  G1A xa{fp_zero(), fp_zero(), true};
-  G2A sa{fp2_zero(), fp2_zero(), true};
-  for (uint32_t q = 0; q < GRP; ++q) {
-    xp[q] = jac_infinity<Fp>();
-    sp[q] = jac_infinity<Fp2>();
-    rho[q] = 0;
-  }
-  for (uint32_t q = 0; q < 2; ++q) {
-    const uint32_t m = h + 2 * q;
-    if (m >= n) continue;
+  uint32_t nl = 0;
+  for (uint32_t m = 0; m < n; ++m) {
     const uint32_t i = mem[m];
     const G2A s = load_g2a(S[i]);
     // (a recheck was subgroup-checked by its group)
@@ -567,69 +554,71 @@ DGN void verify_group(const uint32_t* mem, uint32_t n, uint32_t k, uint64_t seed
       fin[i] = FIN_DONE;
       continue;
     }
-    const G1A x = load_g1a(keys[item_slot ? item_slot[i] : 0u]);
-    mine[q] = i;
-    live |= 1u << q;
-    xa = x;
-    sa = s;
-    xp[q] = jac_from_aff(x);
-    sp[q] = jac_from_aff(s);
-    rho[q] = rlc_coeff(seed ^ GROUP_TAG, i);
+    if (n == 1) {  // a share's own check: its key and signature as they are
+      a = load_g1a(keys[item_slot ? item_slot[i] : 0u]);
+      b = s;
+      live[0] = i;
+      return 1;
+    }
+    xp[nl] = jac_from_aff(load_g1a(keys[item_slot ? item_slot[i] : 0u]));
+    sp[nl] = jac_from_aff(s);
+    rho[nl] = rlc_coeff(seed ^ GROUP_TAG, i);
+    live[nl++] = i;
   }
-  const uint32_t team_live = live | t2_x(live) << 2;
-  if (team_live == 0) return;
+  for (uint32_t m = nl; m < GRP; ++m) {
+    xp[m] = jac_infinity<Fp>();
+    sp[m] = jac_infinity<Fp2>();
+    rho[m] = 0;
+  }
+  if (nl) {
+    a = g1_to_aff(jac_msm4_sac(xp, rho));
+    b = g2_to_aff(jac_msm4_sac(sp, rho));
+  }
+  return nl;
+}
+DGN void verify_group(const uint32_t* mem, uint32_t n, uint32_t k, uint64_t seed, const G1AStore* keys,
+                      const uint32_t* item_slot, const G2AStore* H, const G2AStore* S, uint8_t* status,
+                      uint8_t* fin, uint32_t subgroup) {
   G1A a;
   G2A b;
-  if (n == 1) {  // a share's own check: its key and signature as they are (on lane 0)
-    a = xa;
-    b = t2_x(sa);  // lane 1 takes lane 0's signature
-    b = g2a_pick(h, b, sa);
-  } else {
-    const G1J ah = jac_msm4_sac(xp, rho);
-    const G2J bh = jac_msm4_sac(sp, rho);
-    a = g1_to_aff(jac_add(ah, t2_x(ah)));
-    b = g2_to_aff(jac_add(bh, t2_x(bh)));
+  uint32_t live[GRP];
+  const uint32_t nl = group_combine(mem, n, seed, keys, item_slot, S, status, fin, subgroup, a, b, live);
+  if (nl == 0) return;
+  // one call site of the pairing check for singles and groups alike: a wave holding both runs it once
+  const bool good = pair_check(a, load_g2a(H[mem[0] / k]), b);
+  if (n == 1) {
+    status[live[0]] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
+    fin[live[0]] = FIN_DONE;
+    return;
   }
-  // lane 0 needs a (its pair is (a, H_r)), lane 1 needs b (its pair is (-g1, b))
-  const bool good = t2_verify_eq(a, load_g2a(H[mem[0] / k]), b, h);
-  for (uint32_t q = 0; q < 2; ++q) {
-    if (!(live >> q & 1u)) continue;
-    const uint32_t i = mine[q];
-    if (n == 1) {
-      status[i] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
-      fin[i] = FIN_DONE;
-    } else {
-      if (good) status[i] = DG_ST_OK_;
-      fin[i] = good ? FIN_DONE : FIN_RECHECK;
-    }
+  for (uint32_t m = 0; m < nl; ++m) {
+    if (good) status[live[m]] = DG_ST_OK_;
+    fin[live[m]] = good ? FIN_DONE : FIN_RECHECK;
   }
 }
-// every decoded item after a failed batch (flag[0] == 0), only the isolated ones after a passed batch;
-// threads 2i, 2i + 1: item i
+// every decoded item after a failed batch (flag[0] == 0), only the isolated ones after a passed batch
 DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
                                                     const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
                                                     const uint8_t* isolate, uint8_t* status, uint32_t subgroup) {
-  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i = tid >> 1, h = tid & 1u;
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (status[i] != DG_ST_OK_) return;
   if (flag[0] && !isolate[i]) return;
-  verify_item(i, k, keys, item_slot, H, S, status, subgroup, h);
+  verify_item(i, k, keys, item_slot, H, S, status, subgroup);
 }
 
-// threads 2g, 2g + 1 with g < glist[0]: group g (one member: the item's own check)
+// lane g < glist[0]: group g (one member: the item's own check)
 DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_groups(uint32_t k, const uint32_t* glist, const uint64_t* seedp,
                                                     const G1AStore* keys, const uint32_t* item_slot,
                                                     const G2AStore* H, const G2AStore* S, uint8_t* status,
                                                     uint8_t* fin, uint32_t subgroup, unsigned long long* cnt) {
-  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t g = tid >> 1, h = tid & 1u;
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= glist[0]) return;
   const uint32_t* mem = glist + 4 + 4 * (size_t)g;
   uint32_t n = 0;
   while (n < GRP && mem[n] != ~0u) ++n;
-  if (h == 0) atomicAdd(&cnt[n - 1], 1ull);
-  verify_group(mem, n, k, *seedp, keys, item_slot, H, S, status, fin, subgroup, h);
+  atomicAdd(&cnt[n - 1], 1ull);
+  verify_group(mem, n, k, *seedp, keys, item_slot, H, S, status, fin, subgroup);
 }
 #elif DG_TU_LIB
 // (defined in kernels_verify.hip)

@@ -517,7 +517,9 @@ DG_KERNEL void __launch_bounds__(256) k_kmsm_count(uint32_t N, uint32_t k, uint3
 
 // block b of KSCAN_B keys: exclusive scans of count and of ceil(count / KMSM_CHUNK) within the block,
 // block totals into tot[b], tot[nblocks + b]
-DG_KERNEL void __launch_bounds__(256) k_kscan_local(uint32_t nkeys, const uint32_t* count, uint32_t* offset,
+// (div: the chunk length of chunk_off -- KMSM_CHUNK for the Jacobian chunk sums, 2^(l+1) for the groups of affine
+// level l)
+DG_KERNEL void __launch_bounds__(256) k_kscan_local(uint32_t nkeys, uint32_t div, const uint32_t* count, uint32_t* offset,
                                                     uint32_t* chunk_off, uint32_t* tot) {
   __shared__ uint32_t s_c[256], s_k[256];
   const uint32_t t = threadIdx.x, base = blockIdx.x * KSCAN_B + t * 4;
@@ -527,7 +529,7 @@ DG_KERNEL void __launch_bounds__(256) k_kscan_local(uint32_t nkeys, const uint32
     c[j] = sc;
     kk[j] = sk;
     sc += v;
-    sk += (v + KMSM_CHUNK - 1) / KMSM_CHUNK;
+    sk += (v + div - 1) / div;
   }
   s_c[t] = sc;
   s_k[t] = sk;
@@ -641,7 +643,76 @@ DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_buckets(uint32_t nkey
   for (uint32_t c = chunk_off[b]; c < chunk_off[b + 1]; ++c) g2_add_lds(acc, load_g2j(chunks[c]));
   B[b] = acc;
 }
+// ---- Keyed MSM with affine first levels (msm_run_keyed): the entries of every (window, digit, set) bucket -- the
+// decoded signatures, affine -- summed pairwise in MSM_AFF_L levels of affine additions with one batch inversion per
+// level, as the single-key levels above (k_msm_aff_*), over the keyed list; then one lane per bucket adds its
+// chunk sums A[offset[b] + c 2^L] with mixed additions.  About 15 Fp products per addition instead of the 29 of
+// a mixed Jacobian addition in the chunk sums.  gofs: the level's group offsets per bucket (k_kscan_* with
+// div = 2^(l+1)).
+DG_KERNEL void __launch_bounds__(128) k_kmsm_aff_den(uint32_t l, uint32_t maxg, uint32_t nkeys, const uint32_t* count,
+                                                     const uint32_t* offset, const uint32_t* gofs, const uint32_t* list,
+                                                     const G2AStore* S, const G2AStore* A, Fp* den) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= maxg) return;
+  Fp n = fp_one();
+  uint32_t i, end;
+  if (g < gofs[nkeys] && aff_group(nkeys, count, offset, gofs, l, g, i, end)) {
+    const uint32_t j = i + (1u << l);
+    const G2AStore &a = l == 0 ? S[list[i]] : A[i], &b = l == 0 ? S[list[j]] : A[j];
+    if (!a.inf && !b.inf) {
+      if (!fp2_eq(a.x, b.x))
+        n = fp2_norm(fp2_sub(b.x, a.x));
+      else if (fp2_eq(a.y, b.y))
+        n = fp2_norm(fp2_dbl(a.y));
+    }
+  }
+  den[g] = n;
+}
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_kmsm_aff_add(uint32_t l, uint32_t maxg, uint32_t nkeys,
+                                                                  const uint32_t* count, const uint32_t* offset,
+                                                                  const uint32_t* gofs, const uint32_t* list,
+                                                                  const G2AStore* S, G2AStore* A, const Fp* ninv) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= maxg || g >= gofs[nkeys]) return;
+  uint32_t i, end;
+  const bool pair = aff_group(nkeys, count, offset, gofs, l, g, i, end);
+  if (!pair && l > 0) return;  // the lone entry already sits at i
+  const G2A p = aff_srcA(l == 0 ? S[list[i]] : A[i]);
+  if (!pair) {
+    store_g2a(A[i], p);
+    return;
+  }
+  const G2A q = aff_srcA(l == 0 ? S[list[i + 1]] : A[i + (1u << l)]);
+  store_g2a(A[i], g2_aff_sum(p, q, g2_aff_kind(p, q), ninv[g]));
+}
+// lane = bucket key: the sum of its affine chunk sums (identity when empty), the running sum in LDS
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_buckets_aff(uint32_t nkeys, const uint32_t* count,
+                                                                       const uint32_t* offset, const G2AStore* A,
+                                                                       G2JStore* B) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nkeys) return;
+  __shared__ G2JStore s_acc[128];
+  G2JStore& acc = s_acc[threadIdx.x];
+  store_g2j(acc, jac_infinity<Fp2>());
+  const uint32_t nch = (count[b] + (1u << MSM_AFF_L) - 1) >> MSM_AFF_L;
+  const G2AStore* Ab = A + offset[b];
+  for (uint32_t c = 0; c < nch; ++c) {
+    const G2AStore& a = Ab[c << MSM_AFF_L];
+    if (!a.inf) g2_madd_lds(acc, a.x, a.y);
+  }
+  B[b] = acc;
+}
 #elif defined(__HIP__)
+DG_KERNEL void __launch_bounds__(128) k_kmsm_aff_den(uint32_t l, uint32_t maxg, uint32_t nkeys, const uint32_t* count,
+                                                     const uint32_t* offset, const uint32_t* gofs, const uint32_t* list,
+                                                     const G2AStore* S, const G2AStore* A, Fp* den);
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_kmsm_aff_add(uint32_t l, uint32_t maxg, uint32_t nkeys,
+                                                                  const uint32_t* count, const uint32_t* offset,
+                                                                  const uint32_t* gofs, const uint32_t* list,
+                                                                  const G2AStore* S, G2AStore* A, const Fp* ninv);
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_buckets_aff(uint32_t nkeys, const uint32_t* count,
+                                                                       const uint32_t* offset, const G2AStore* A,
+                                                                       G2JStore* B);
 DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_buckets(uint32_t nkeys, const uint32_t* chunk_off,
                                                                    const G2JStore* chunks, G2JStore* B);
 DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_chunks(uint32_t max_chunks, uint32_t nkeys,

@@ -351,127 +351,3 @@ extern "C" int hc_recover_sac_check(const uint8_t* sigs96, const uint32_t* idx, 
   return jac_eq(sum, want) ? 1 : 0;
 }
 
-// ---- Two-lane teams (team.h) on the host: lanes 0 and 1 of a team as two threads, every t2_x a barrier exchange.
-#include <atomic>
-#include <thread>
-namespace {
-std::atomic<uint32_t> t2_val[2];
-std::atomic<int> t2_cnt{0}, t2_gen{0};
-thread_local int t2_lane = 0;
-void t2_barrier() {
-  const int g = t2_gen.load();
-  if (t2_cnt.fetch_add(1) == 1) {
-    t2_cnt.store(0);
-    t2_gen.fetch_add(1);
-  } else {
-    while (t2_gen.load() == g) std::this_thread::yield();
-  }
-}
-uint32_t t2_host_xchg(uint32_t v) {
-  t2_val[t2_lane].store(v);
-  t2_barrier();
-  const uint32_t r = t2_val[1 - t2_lane].load();
-  t2_barrier();
-  return r;
-}
-// fn(h) on both lanes
-template <class Fn>
-void t2_run(Fn fn) {
-  std::thread other([&] {
-    t2_lane = 1;
-    g_t2_xchg = t2_host_xchg;
-    fn(1u);
-    g_t2_xchg = nullptr;
-  });
-  t2_lane = 0;
-  g_t2_xchg = t2_host_xchg;
-  fn(0u);
-  g_t2_xchg = nullptr;
-  other.join();
-}
-uint64_t t2_rng = 1;
-Fp rnd_fp() {
-  Fp a;
-  for (int i = 0; i < 12; ++i) {
-    t2_rng = t2_rng * 6364136223846793005ull + 1442695040888963407ull;
-    a.l[i] = (uint32_t)(t2_rng >> 32);
-  }
-  a.l[11] &= 0x0fffffffu;  // < 2^380 < p
-  return fp_to_mont(a);
-}
-Fp2 rnd_fp2() { return Fp2{rnd_fp(), rnd_fp()}; }
-Fp6 rnd_fp6() { return Fp6{rnd_fp2(), rnd_fp2(), rnd_fp2()}; }
-Fp12 rnd_fp12() { return Fp12{rnd_fp6(), rnd_fp6()}; }
-bool fp6_same(const Fp6& a, const Fp6& b) {
-  return fp2_eq(a.c0, b.c0) && fp2_eq(a.c1, b.c1) && fp2_eq(a.c2, b.c2);
-}
-bool fp12_same(const Fp12& r, const Fp6 (&h)[2]) { return fp6_same(r.c0, h[0]) && fp6_same(r.c1, h[1]); }
-}  // namespace
-
-// bit k set: team block k differs from the one-lane Fp12 routine on random inputs (0 = all agree)
-extern "C" uint32_t hc_t2_selftest(uint64_t seed) {
-  t2_rng = seed | 1;
-  const Fp12 a = rnd_fp12(), b = rnd_fp12();
-  const Fp2 c0 = rnd_fp2(), c1 = rnd_fp2(), c4 = rnd_fp2();
-  // an element of the cyclotomic subgroup: a^((p^6 - 1)(p^2 + 1))
-  const Fp12 e1 = fp12_mul(fp12_conj(a), fp12_inv(a));
-  const Fp12 cy = fp12_mul(fp12_frob(fp12_frob(e1)), e1);
-  uint32_t bad = 0;
-  Fp6 o[2];
-  auto half = [](const Fp12& x, uint32_t h) { return h ? x.c1 : x.c0; };
-  t2_run([&](uint32_t h) { o[h] = t2_sqr(half(a, h), h); });
-  bad |= fp12_same(fp12_sqr(a), o) ? 0u : 1u << 0;
-  t2_run([&](uint32_t h) { o[h] = t2_mul(half(a, h), half(b, h), h); });
-  bad |= fp12_same(fp12_mul(a, b), o) ? 0u : 1u << 1;
-  t2_run([&](uint32_t h) { o[h] = t2_mul_line(half(a, h), c0, c1, c4, h); });
-  bad |= fp12_same(fp12_mul_014(a, c0, c1, c4), o) ? 0u : 1u << 2;
-  t2_run([&](uint32_t h) { o[h] = t2_frob(half(a, h), h); });
-  bad |= fp12_same(fp12_frob(a), o) ? 0u : 1u << 3;
-  t2_run([&](uint32_t h) { o[h] = t2_inv(half(a, h), h); });
-  bad |= fp12_same(fp12_inv(a), o) ? 0u : 1u << 4;
-  t2_run([&](uint32_t h) { o[h] = t2_conj(half(a, h), h); });
-  bad |= fp12_same(fp12_conj(a), o) ? 0u : 1u << 5;
-  t2_run([&](uint32_t h) { o[h] = t2_cyc_sqr(half(cy, h), h); });
-  bad |= fp12_same(fp12_cyc_sqr(cy), o) ? 0u : 1u << 6;
-  bad |= fp12_same(fp12_sqr(cy), o) ? 0u : 1u << 7;
-  t2_run([&](uint32_t h) { o[h] = t2_exp_z(half(cy, h), h); });
-  bad |= fp12_same(cyc_exp_z(cy), o) ? 0u : 1u << 8;
-  bool one[2];
-  t2_run([&](uint32_t h) { one[h] = t2_final_exp_is_one(half(a, h), h); });
-  const bool want = fp12_is_one(final_exp_cubed(a));
-  bad |= (one[0] == want && one[1] == want) ? 0u : 1u << 9;
-  return bad;
-}
-// the team's bls.Verify of (pk, msg, sig): lane 0 the pair (pk, H(msg)), lane 1 (-g1, sig); 0 valid, 1 invalid,
-// 2 / 4 decode errors (as hc_verify); 8: the two lanes disagree
-extern "C" int hc_t2_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t n, const uint8_t* sig96) {
-  G1A pk;
-  if (!g1_decompress(pk, pk48, true)) return 4;
-  G2A s;
-  if (!g2_decompress(s, sig96, true)) return 2;
-  const G2A hq = g2_to_aff(hash_to_g2(msg, n, DSTN, 43));
-  const G1A ng{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false};
-  bool ok[2];
-  t2_run([&](uint32_t h) {
-    const G1A P = h ? ng : pk;
-    const G2A Q = h ? s : hq;
-    const bool present = h ? !s.inf : (!pk.inf && !hq.inf);
-    ok[h] = t2_pair_check(P, Q, present, h);
-  });
-  if (ok[0] != ok[1]) return 8;
-  return ok[0] ? 0 : 1;
-}
-// the team's Miller loop against miller_loop<2> (both pairs present): 1 if equal
-extern "C" int hc_t2_miller_check(const uint8_t* pk48, const uint8_t* msg, uint32_t n, const uint8_t* sig96) {
-  G1A pk;
-  G2A s;
-  if (!g1_decompress(pk, pk48, true) || !g2_decompress(s, sig96, true)) return -1;
-  const G2A hq = g2_to_aff(hash_to_g2(msg, n, DSTN, 43));
-  const G1A ng{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false};
-  G1A P[2] = {pk, ng};
-  G2A Q[2] = {hq, s};
-  const Fp12 want = miller_loop<2>(P, Q, 2);
-  Fp6 o[2];
-  t2_run([&](uint32_t h) { o[h] = t2_miller(P[h], Q[h], true, h); });
-  return fp12_same(want, o) ? 1 : 0;
-}

@@ -235,26 +235,3 @@ def test_recover_sac_host_build(hc, t, seed):
     idx = list(range(t)) if seed < 0 else sorted(rng.sample(range(256), t))
     assert hc.hc_recover_sac_check(b"".join(sigs), (ctypes.c_uint32 * t)(*idx), t) == 1
 
-
-def test_team_blocks_host_build(hc):
-    """Two-lane team arithmetic (team.h; the per-item pairing kernels), run on the host as two threads whose DPP
-    moves become barrier exchanges: every GT block equals the one-lane Fp12 routine of field.h / pairing.h on
-    random inputs (squaring, product, line product, Frobenius, inverse, conjugate, cyclotomic squaring,
-    exponentiation by z, final exponentiation == 1)."""
-    hc.hc_t2_selftest.restype = ctypes.c_uint32
-    for seed in (1, 2, 3):
-        assert hc.hc_t2_selftest(ctypes.c_uint64(seed)) == 0, seed
-
-
-def test_team_verify_host_build(hc):
-    """The team's Miller loop equals miller_loop<2> and its bls.Verify verdicts equal the one-lane check's on the
-    golden chain (valid and swapped signatures)."""
-    ch = load("chain_t3n5.json")
-    pk = hx(ch["pk"])
-    r0 = ch["rounds"][0]
-    assert hc.hc_t2_miller_check(pk, hx(r0["msg"]), 32, hx(r0["sig"])) == 1
-    for i, r in enumerate(ch["rounds"][:2]):
-        msg, sig = hx(r["msg"]), hx(ch["rounds"][(i + (i % 2)) % 64]["sig"])
-        want = hc.hc_verify(pk, msg, len(msg), sig)
-        assert want == (0 if i % 2 == 0 else 1)
-        assert hc.hc_t2_verify(pk, msg, len(msg), sig) == want
