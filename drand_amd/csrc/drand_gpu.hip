@@ -142,7 +142,7 @@ enum Slot {
   S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_BINV, S_NV, S_NVINV,
   S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_BINV_PRE, S_BINV_ROOTS, S_RC_UNI, S_RC_REF, S_RC_LIST, S_RS_DIG,
   S_RC_NAF, S_RC_EV, S_RC_TAB, S_RC_D, S_RC_PINF, S_RC_DEN, S_RC_A, S_PW, S_SLOTW, S_SFULL, S_STFULL, S_INC, S_PB, S_SLOTB,
-  S_SEED2, S_SB, S_STB, S_ISOB, S_KMSM_GOFS, S_COUNT
+  S_SEED2, S_SB, S_STB, S_ISOB, S_KMSM_GOFS, S_KMSM_BP, S_KMSM_BT2, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -487,8 +487,13 @@ int msm_run_keyed(const Batch& b, const uint64_t* seed, const uint8_t* iso, bool
       RET(launch("k_kmsm_aff_add", k_kmsm_aff_add, maxg, 128, st, l, maxg, nkeys, (const uint32_t*)cnt,
                  (const uint32_t*)offset, gl, (const uint32_t*)list, (const G2AStore*)b.S, A, (const Fp*)dinv));
     }
-    RET(launch("k_kmsm_buckets_aff", k_kmsm_buckets_aff, nkeys, 128, st, nkeys, (const uint32_t*)cnt,
-               (const uint32_t*)offset, (const G2AStore*)A, B));
+    G2JStore *BP, *BT2;
+    RET(wsT(S_KMSM_BP, (size_t)nkeys * KMSM_BSPLIT, &BP));
+    RET(wsT(S_KMSM_BT2, (size_t)nkeys * KMSM_BSPLIT, &BT2));
+    RET(launch("k_kmsm_buckets_aff", k_kmsm_buckets_aff, nkeys * KMSM_BSPLIT, 128, st, nkeys, (const uint32_t*)cnt,
+               (const uint32_t*)offset, (const G2AStore*)A, BP));
+    RET(reduce_rows(BP, BT2, nkeys, KMSM_BSPLIT, st));  // BP[b] = bucket b
+    B = BP;
   } else {
     RET(wsT(S_KMSM_CHUNKS, max_chunks, &chunks));
     RET(launch("k_kmsm_chunks", k_kmsm_chunks, max_chunks, 128, st, max_chunks, nkeys, (const uint32_t*)cnt,

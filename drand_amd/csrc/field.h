@@ -525,6 +525,17 @@ DGI Fp2 fp2_sub(const Fp2& a, const Fp2& b) { return Fp2{fp_sub(a.c0, b.c0), fp_
 DGI Fp2 fp2_dbl(const Fp2& a) { return Fp2{fp_dbl(a.c0), fp_dbl(a.c1)}; }
 DGI Fp2 fp2_neg(const Fp2& a) { return Fp2{fp_neg(a.c0), fp_neg(a.c1)}; }
 DGI Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
+// DG_FP2_CALL=1 (the per-item pairing TU): fp2_mul / fp2_sqr are one out-of-line call each (fp2_mul_r below,
+// operands and result in VGPRs, the Karatsuba products inlined in the callee) instead of three / two Fp-level calls
+#ifndef DG_FP2_CALL
+#define DG_FP2_CALL 0
+#endif
+#if DG_FP2_CALL && defined(__HIP_DEVICE_COMPILE__) && DG_FP_CALL == 1
+__device__ __noinline__ Fp2 fp2_mul_r(DG_P12(a), DG_P12(b), DG_P12(c), DG_P12(d));
+__device__ __noinline__ Fp2 fp2_sqr_r(DG_P12(a), DG_P12(b));
+DGI Fp2 fp2_mul(const Fp2& a, const Fp2& b) { return fp2_mul_r(DG_A12(a.c0), DG_A12(a.c1), DG_A12(b.c0), DG_A12(b.c1)); }
+DGI Fp2 fp2_sqr(const Fp2& a) { return fp2_sqr_r(DG_A12(a.c0), DG_A12(a.c1)); }
+#else
 DGH Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
   Fp t0 = fp_mul(a.c0, b.c0);
   Fp t1 = fp_mul(a.c1, b.c1);
@@ -535,6 +546,7 @@ DGH Fp2 fp2_sqr(const Fp2& a) {
   Fp m = fp_mul(a.c0, a.c1);
   return Fp2{fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(m)};
 }
+#endif
 // Fp2 products as one out-of-line call each, operands and result in VGPRs (48 / 24 scalar arguments, the
 // three or two Fp products inlined in the callee).  A caller of the Fp-level calls must keep its whole live set
 // in the ~108 callee-saved VGPRs across every one of them (or spill it to scratch); across one Fp2-level call

@@ -51,6 +51,10 @@ constexpr uint32_t MSM_CHUNK = 8;   // points per first-level lane
 #endif
 constexpr uint32_t KMSM_CHUNK = DG_KMSM_CHUNK;
 constexpr uint32_t MSM_BSPLIT = 32;  // lanes per bucket at the second level
+#ifndef DG_KMSM_BSPLIT
+#define DG_KMSM_BSPLIT 4
+#endif
+constexpr uint32_t KMSM_BSPLIT = DG_KMSM_BSPLIT;  // lanes per keyed bucket over its affine chunk sums
 constexpr uint32_t MSM_SLICE_LANES = 64;  // lanes per (side, window, bit slice) in k_msm_slices
 
 #if defined(__HIP__) && DG_TU_LIB
@@ -685,22 +689,25 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_kmsm_aff_add(uint32_t l, u
   const G2A q = aff_srcA(l == 0 ? S[list[i + 1]] : A[i + (1u << l)]);
   store_g2a(A[i], g2_aff_sum(p, q, g2_aff_kind(p, q), ninv[g]));
 }
-// lane = bucket key: the sum of its affine chunk sums (identity when empty), the running sum in LDS
+// lane (bucket key b, q < KMSM_BSPLIT): chunk sums q, q + KMSM_BSPLIT, ... of bucket b with mixed additions, the
+// running sum in LDS, into BP[b * KMSM_BSPLIT + q] (then row-summed): ~400 points per bucket at C3 leave ~50 chunk
+// sums, which one lane per bucket added in a long dependent chain
 DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_buckets_aff(uint32_t nkeys, const uint32_t* count,
                                                                        const uint32_t* offset, const G2AStore* A,
-                                                                       G2JStore* B) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nkeys) return;
+                                                                       G2JStore* BP) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nkeys * KMSM_BSPLIT) return;
+  const uint32_t b = g / KMSM_BSPLIT, q = g % KMSM_BSPLIT;
   __shared__ G2JStore s_acc[128];
   G2JStore& acc = s_acc[threadIdx.x];
   store_g2j(acc, jac_infinity<Fp2>());
   const uint32_t nch = (count[b] + (1u << MSM_AFF_L) - 1) >> MSM_AFF_L;
   const G2AStore* Ab = A + offset[b];
-  for (uint32_t c = 0; c < nch; ++c) {
+  for (uint32_t c = q; c < nch; c += KMSM_BSPLIT) {
     const G2AStore& a = Ab[c << MSM_AFF_L];
     if (!a.inf) g2_madd_lds(acc, a.x, a.y);
   }
-  B[b] = acc;
+  BP[g] = acc;
 }
 #elif defined(__HIP__)
 DG_KERNEL void __launch_bounds__(128) k_kmsm_aff_den(uint32_t l, uint32_t maxg, uint32_t nkeys, const uint32_t* count,
@@ -712,7 +719,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_kmsm_aff_add(uint32_t l, u
                                                                   const G2AStore* S, G2AStore* A, const Fp* ninv);
 DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_buckets_aff(uint32_t nkeys, const uint32_t* count,
                                                                        const uint32_t* offset, const G2AStore* A,
-                                                                       G2JStore* B);
+                                                                       G2JStore* BP);
 DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_buckets(uint32_t nkeys, const uint32_t* chunk_off,
                                                                    const G2JStore* chunks, G2JStore* B);
 DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_kmsm_chunks(uint32_t max_chunks, uint32_t nkeys,

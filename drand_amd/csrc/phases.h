@@ -245,17 +245,85 @@ DGI bool dec_p3(const DecState& ds, const Fp& c, const Fp& t, bool subgroup, G2A
 }
 
 #if defined(__HIP__)
+// x^((p-3)/4) with the width-3 table (x, x^3, x^5, x^7) in LDS (DG_EXP_LDS=1, an A/B of k_exp_pm3d4): without the
+// table in registers the kernel fits 3 waves per SIMD (168 VGPRs) instead of 2, the four entries packed (12 limbs,
+// 48 B) lane-major in LDS, 192 B per lane, 147 KB per CU at 3 waves per SIMD; 378 squarings and 108 products
+// instead of 376 and 85
+#ifndef DG_EXP_LDS
+#define DG_EXP_LDS 0
+#endif
+// DG_EXP_LDS=2: the width-2 table (x, x^3; 96 B per lane) at 4 waves per SIMD, 378 squarings and 142 products
+#if DG_EXP_LDS == 2
+#define DG_EXP_NTAB 2
+#define DG_EXP_SCHED(f) EXP_PM3D4_W2_##f
+#else
+#define DG_EXP_NTAB 4
+#define DG_EXP_SCHED(f) EXP_PM3D4_##f
+#endif
+#if DG_EXP_LDS
+DGI void fp_pow_pm3d4_lds(const Fp& x, Fp& out, uint32_t* tab, uint32_t stride) {
+  // tab[(e * 12 + l) * stride]: limb l of entry e of this lane (stride = threads per block)
+  uint32_t t[14], x2[14], acc[14], nxt[14], m[14];
+  fp28_unpack(x.l, t);
+  fp28_sos_sqr_d(t, x2);
+  auto put = [&](int e, const uint32_t (&d)[14]) {
+    uint32_t w[12];
+    fp28_pack(d, w);
+#pragma unroll
+    for (int l = 0; l < 12; ++l) tab[(e * 12 + l) * stride] = w[l];
+  };
+  auto get = [&](int e, uint32_t (&d)[14]) {
+    uint32_t w[12];
+#pragma unroll
+    for (int l = 0; l < 12; ++l) w[l] = tab[(e * 12 + l) * stride];
+    fp28_unpack(w, d);
+  };
+  put(0, t);
+#pragma unroll 1
+  for (int e = 1; e < DG_EXP_NTAB; ++e) {
+    fp28_sos_mul_d(t, x2, nxt);
+#pragma unroll
+    for (int d = 0; d < 14; ++d) t[d] = nxt[d];
+    put(e, t);
+  }
+  get(DG_EXP_SCHED(FIRST), acc);
+  for (int s = 0; s < DG_EXP_SCHED(NSTEPS); ++s) {
+    const int k = DG_EXP_SCHED(STEPS)[s][0];
+    const int idx = DG_EXP_SCHED(STEPS)[s][1];
+    for (int j = 0; j < k; ++j) {
+      fp28_sos_sqr_d(acc, nxt);
+#pragma unroll
+      for (int d = 0; d < 14; ++d) acc[d] = nxt[d];
+    }
+    if (idx >= 0) {
+      get(idx, m);
+      fp28_sos_mul_d(acc, m, nxt);
+#pragma unroll
+      for (int d = 0; d < 14; ++d) acc[d] = nxt[d];
+    }
+  }
+  Fp r;
+  fp28_pack(acc, r.l);
+  out = fp_reduce_once(r);
+}
+#endif
 #ifndef DG_PHASE_WAVES
 #define DG_PHASE_WAVES 2  // min waves per SIMD of p1a, p3, dec_p3 (1 wave: above 256 VGPRs; 2: p3 554 -> 422 us)
 #endif
 #ifndef DG_EXP_WAVES
-#define DG_EXP_WAVES 2
+#define DG_EXP_WAVES (DG_EXP_LDS == 2 ? 4 : (DG_EXP_LDS ? 3 : 2))
 #endif
 #if DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128, DG_EXP_WAVES) k_exp_pm3d4(uint32_t n, const Fp* in, Fp* out) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+#if DG_EXP_LDS
+  __shared__ uint32_t s_tab[DG_EXP_NTAB * 12 * 128];
+  if (i >= n) return;
+  fp_pow_pm3d4_lds(in[i], out[i], s_tab + threadIdx.x, 128u);
+#else
   if (i >= n) return;
   out[i] = fp_pow_pm3d4_sos(in[i]);
+#endif
 }
 
 DG_KERNEL void __launch_bounds__(128, DG_PHASE_WAVES) k_h2c_p1a(uint32_t R, const uint8_t* msgs, uint32_t msg_len, const uint8_t* dst,
