@@ -688,10 +688,11 @@ def main():
     ap.add_argument("--c5-rounds", type=int, default=10000, help="C5 rounds (all GPUs); 0 disables")
     ap.add_argument("--sync-rounds", type=int, default=100000, help="0 disables the syncFrom catch-up line")
     ap.add_argument("--no-c1", action="store_true", help="no C1 / live-latency lines")
-    ap.add_argument("--status-bufs", type=int, default=4, help="steps whose verdicts may be in flight")
-    ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("BENCH_HW_QUEUES", "8")),
+    ap.add_argument("--status-bufs", type=int, default=int(os.environ.get("DG_SETS", "10")),
+                    help="steps whose verdicts may be in flight (at least the library's workspace sets, DG_SETS = 10)")
+    ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("BENCH_HW_QUEUES", "16")),
                     help="HIP hardware queues per process (GPU_MAX_HW_QUEUES, set before HIP starts; 0 keeps the "
-                         "environment's): the library's 4 workspace streams, its per-item stream and the caller's "
+                         "environment's): the library's 10 workspace streams, its per-item stream and the caller's "
                          "streams each want their own queue (DESIGN.md §5.3)")
     args = ap.parse_args()
     if args.hw_queues > 0:
@@ -751,7 +752,7 @@ def main():
     d_ps = torch.from_numpy(psb).to(dev)
     d_off = torch.from_numpy(off.astype(np.int32)).to(dev)
     d_sig = torch.from_numpy(np.ascontiguousarray(sigs)).to(dev)
-    # status buffers rotate over the steps in flight (the library itself keeps at most DG_SETS = 4 batches
+    # status buffers rotate over the steps in flight (the library itself keeps at most DG_SETS = 10 batches
     # in flight); a buffer is reused once the all-gather that read it has finished
     nbuf = args.status_bufs
     d_sts = [torch.full((n,), 99, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
@@ -793,7 +794,7 @@ def main():
 
     # prime every workspace set once (its grow-only buffers are allocated on first use), then the W warmup
     # steps: no allocation or first-dispatch cost falls inside the timed region
-    for w in range(max(1, 4 // nb + 1)):
+    for w in range(max(1, int(os.environ.get("DG_SETS", "10")) // nb + 1)):
         step(500 + w)
     drain()
     for w in range(args.warmup):

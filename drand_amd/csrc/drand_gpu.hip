@@ -32,13 +32,13 @@ struct Timing {
 // through the asynchronous entry point rotate over kSets sets, so the latency-bound tail of one batch
 // (Miller loops, final exponentiation: a few workgroups) overlaps the throughput-bound head of the next.
 #ifndef DG_MAX_SETS
-#define DG_MAX_SETS 8
+#define DG_MAX_SETS 12
 #endif
-constexpr int kSets = DG_MAX_SETS;  // capacity; DG_SETS (environment, default 4) sets are used
+constexpr int kSets = DG_MAX_SETS;  // capacity; DG_SETS (environment, default 10) sets are used
 int active_sets() {
   static const int n = [] {
     const char* e = getenv("DG_SETS");
-    int v = e ? atoi(e) : 4;
+    int v = e ? atoi(e) : 10;
     return v < 1 ? 1 : (v > kSets ? kSets : v);
   }();
   return n;
@@ -176,6 +176,21 @@ int acquire_set(hipStream_t* st) {
     s.busy = false;
   }
   c.cur = i;
+  *st = s.stream;
+  return 0;
+}
+
+// The multi-key blocking entry points (VerifyPartial, Recover) always take set 0 (waiting for a batch still using
+// it): their grow-only buffers are the largest (~20 GB at 100k rounds x 64 partials: the keyed MSM's affine entry
+// array), and rotating them over every set would hold one such copy per set.
+int acquire_set0(hipStream_t* st) {
+  Ctx& c = g_ctx;
+  Set& s = c.sets[0];
+  if (s.busy) {
+    HIPCHK(hipEventSynchronize(s.done));
+    s.busy = false;
+  }
+  c.cur = 0;
   *st = s.stream;
   return 0;
 }
@@ -622,15 +637,16 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
     out->batched_sub = batched_sub;
     return 0;
   }
+  // the per-item pass on the per-item stream (g_ctx.fb_stream), ordered after and before this set's stream; the
+  // per-round H_r = h_eff(Q_r) there too (k_clear_rounds: ~5 KB of private segment, kept off the set streams)
   G2AStore* H;
   RET(wsT(S_H, b.R, &H));
-  RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, (const uint32_t*)flag, b.Q, H));
-  // the per-item pass on the per-item stream (g_ctx.fb_stream), ordered after and before this set's stream
   Set& set = cur_set();
   const hipStream_t batch_st = st;
   HIPCHK(hipEventRecord(set.to_fb, batch_st));
   st = g_ctx.shared_fb ? batch_st : g_ctx.fb_stream;
   HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
+  RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, (const uint32_t*)flag, b.Q, H));
   RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
              (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status, batched_sub));
   HIPCHK(hipEventRecord(set.from_fb, st));
@@ -911,12 +927,17 @@ int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const 
 // verify_group); the members of a failed group, and everything in the last pass, are checked alone.  DG_GROUP=1
 // checks every item alone.  fin: FIN_DONE for the final verdicts, FIN_PENDING for the rest.
 int prefix_pass(uint32_t R, uint32_t k, uint32_t t, const uint64_t* seed, const G1AStore* keys, const uint32_t* item_slot,
-                const G2AStore* H, const G2AStore* S, uint8_t* status, uint8_t* fin, uint32_t subgroup, hipStream_t batch_st) {
+                const G2JStore* Q, const uint32_t* zero2, const G2AStore* S, uint8_t* status, uint8_t* fin,
+                uint32_t subgroup, hipStream_t batch_st) {
   const size_t N = (size_t)R * k;
   Set& set = cur_set();
   HIPCHK(hipEventRecord(set.to_fb, batch_st));
   const hipStream_t st = g_ctx.shared_fb ? batch_st : g_ctx.fb_stream;
   HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
+  // H_r = h_eff(Q_r) for every round (zero2: the flag pair {0, 0})
+  G2AStore* H;
+  RET(wsT(S_H, R, &H));
+  RET(launch("k_clear_rounds", k_clear_rounds, R, 128, st, R, zero2, Q, H));
   uint32_t* glist;
   RET(wsT(S_LIST, 4 * (N + 1), &glist));
   // An empty pass costs two launches of returning lanes; the speculative margins (k_prefix_groups) keep the
@@ -930,7 +951,7 @@ int prefix_pass(uint32_t R, uint32_t k, uint32_t t, const uint64_t* seed, const 
     RET(launch("k_prefix_groups", k_prefix_groups, R, 128, st, R, k, t, pass == kPasses ? 1u : 0u, grp, margin,
                (const uint8_t*)status, (const uint8_t*)fin, glist));
     RET(launch("k_verify_groups", k_verify_groups, (uint32_t)N, 64, st, k, (const uint32_t*)glist, seed, keys, item_slot,
-               H, S, status, fin, subgroup, g_ctx.gcount));
+               (const G2AStore*)H, S, status, fin, subgroup, g_ctx.gcount));
   }
   HIPCHK(hipEventRecord(set.from_fb, st));
   HIPCHK(hipStreamWaitEvent(batch_st, set.from_fb, 0));
@@ -1022,11 +1043,9 @@ int recover_windowed(const uint8_t* commits48, uint32_t t, uint32_t R, const uin
     RET(bind_seed(bf, seed ^ 0x77696e646f77ull, st, &s2, S_SEED2));
     pseed = s2;
   }
-  G2AStore* H;
-  RET(wsT(S_H, R, &H));
   HIPCHK(hipMemsetAsync(inc + 2, 0, 8, st));  // k_clear_rounds: flag {0, 0} = clear every round
-  RET(launch("k_clear_rounds", k_clear_rounds, R, 128, st, R, (const uint32_t*)(inc + 2), (const G2JStore*)Q, H));
-  RET(prefix_pass(R, k, t, pseed, keys, d_itemslot, H, S, status, fin, bo.batched_sub, st));
+  RET(prefix_pass(R, k, t, pseed, keys, d_itemslot, (const G2JStore*)Q, (const uint32_t*)(inc + 2), S, status, fin,
+                  bo.batched_sub, st));
   return launch("k_count_fallback", k_count_fallback, 1, 64, st, bo.flag, g_ctx.fallbacks);
 }
 
@@ -1190,9 +1209,11 @@ int dg_init(int device) {
   // lane), stalled every queue for ~0.5 s (rocprofv3 trace).  Dispatch the largest-scratch kernels once here,
   // with zero items (every lane returns at once), so the growth happens now -- the largest first: a dispatch
   // that needs a larger private segment than the queue's current one, right behind it, failed with
-  // HSA_STATUS_ERROR_OUT_OF_RESOURCES on the box.  The per-item kernels go to the per-item stream only; every
-  // workspace stream gets k_sign, the largest private segment of the kernels that run there
-  // (tests/test_abi.py checks both orderings against the code-object metadata).
+  // HSA_STATUS_ERROR_OUT_OF_RESOURCES on the box.  Each queue reserves its scratch for every wave the device can
+  // hold, so the kernels with the large private segments (the per-item pairing checks, k_clear_rounds, k_sign,
+  // k_hash_to_g2) all run on the per-item stream, and the workspace streams are prewarmed with the largest of the
+  // rest, k_rc_combine (~4 KB; tests/test_abi.py checks both orderings against the code-object metadata):
+  // with 12 workspace streams on 32 queues at k_sign's 5.7 KB, dg_init failed with that error.
   hipFuncAttributes fa_items{}, fa_groups{};
   HIPCHK(hipFuncGetAttributes(&fa_items, reinterpret_cast<const void*>(k_verify_items)));
   HIPCHK(hipFuncGetAttributes(&fa_groups, reinterpret_cast<const void*>(k_verify_groups)));
@@ -1221,8 +1242,8 @@ int dg_init(int device) {
       prewarm_items(x.stream);
     } else {
       // n = 0: every lane returns
-      hipLaunchKernelGGL(k_sign, dim3(1), dim3(128), 0, x.stream, 0u, (const uint8_t*)nullptr, (const uint16_t*)nullptr,
-                         (const uint8_t*)nullptr, 0u, (const uint8_t*)nullptr, 0u, (uint8_t*)nullptr);
+      hipLaunchKernelGGL(k_rc_combine, dim3(1), dim3(128), 0, x.stream, 0u, 0u, (const uint32_t*)nullptr,
+                         (const uint8_t*)nullptr, (const G2JStore*)nullptr, (G2JStore*)nullptr);
     }
     HIPCHK(hipGetLastError());
   }
@@ -1337,6 +1358,7 @@ int dg_hash_to_g2(size_t n, const uint8_t* msgs, size_t msg_len, const uint8_t* 
   if (!msgs || !dst || !out96 || dst_len > 255 || n > 0xffffffffu) return fail(DG_E_ARG, "bad arguments");
   hipStream_t st;
   RET(acquire_set(&st));
+  st = g_ctx.fb_stream;  // (its private segment: the per-item stream's queue holds the large scratch reservations)
   const uint8_t *d_msgs, *d_dst;
   RET(upload(S_MSGS, msgs, n * msg_len, (uint8_t**)&d_msgs, st));
   RET(upload(S_DST, dst, dst_len, (uint8_t**)&d_dst, st));
@@ -1359,6 +1381,7 @@ int dg_sign(size_t n, const uint8_t* scalars32, const uint16_t* index, const uin
   RET(check_args_n(n));
   hipStream_t st;
   RET(acquire_set(&st));
+  st = g_ctx.fb_stream;  // (its private segment: the per-item stream's queue holds the large scratch reservations)
   uint8_t *d_sc, *d_m, *d_dst, *d_out;
   uint16_t* d_idx = nullptr;
   RET(upload(S_IN0, scalars32, n * 32, &d_sc, st));
@@ -1641,7 +1664,7 @@ int dg_verify_partials(const uint8_t* commits48, uint32_t t, size_t rounds, cons
   if (!commits48 || t == 0 || !msgs || !partials98 || !status) return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(rounds * (size_t)k));
   hipStream_t st;
-  RET(acquire_set(&st));
+  RET(acquire_set0(&st));
   uint8_t* d_st;
   RET(verify_partials_dev(commits48, t, (uint32_t)rounds, msgs, (uint32_t)msg_len, k, partials98, fresh_seed(seed), st,
                           &d_st));
@@ -1662,7 +1685,7 @@ int dg_recover(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_t ro
     return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(rounds * (size_t)(k > t ? k : t)));
   hipStream_t st;
-  RET(acquire_set(&st));
+  RET(acquire_set0(&st));
   const uint32_t R = (uint32_t)rounds;
   uint8_t *d_st, *d_m, *d_p;
   G2AStore* d_S;
@@ -1684,7 +1707,7 @@ int dg_recover_dev(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_
     return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(rounds * (size_t)(k > t ? k : t)));
   hipStream_t st;
-  RET(acquire_set(&st));
+  RET(acquire_set0(&st));
   const uint32_t R = (uint32_t)rounds;
   uint8_t* d_st;
   G2AStore* d_S;
@@ -1703,7 +1726,7 @@ int dg_recover_verified(uint32_t t, uint32_t nshares, size_t rounds, uint32_t k,
     return fail(DG_E_ARG, "bad arguments");
   RET(check_args_n(rounds * (size_t)(k > t ? k : t)));
   hipStream_t st;
-  RET(acquire_set(&st));
+  RET(acquire_set0(&st));
   const uint32_t R = (uint32_t)rounds;
   const size_t N = (size_t)R * k;
   uint8_t *d_p, *d_vst, *d_st;

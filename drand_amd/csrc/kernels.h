@@ -173,19 +173,6 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_h2c_uncleared(uint32_t n, 
                                                       G2JStore* outQ);
 #endif
 
-// sigma decode + subgroup check (A10)
-#if DG_TU_LIB
-DG_KERNEL void __launch_bounds__(128) k_decode_sigs(uint32_t n, const uint8_t* sigs, uint32_t stride, uint32_t offset,
-                                                    G2AStore* outS, uint8_t* status) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  G2A a;
-  bool ok = g2_decompress(a, sigs + (size_t)stride * i + offset, true);
-  if (!ok) a = G2A{fp2_zero(), fp2_zero(), true};
-  store_g2a(outS[i], a);
-  status[i] = ok ? DG_ST_OK_ : DG_ST_SIG_DECODE_;
-}
-#endif
 
 // G1 decode (keys, commits), with subgroup check
 #if DG_TU_LIB

@@ -88,11 +88,12 @@ def test_host_arithmetic_under_asan_ubsan():
 
 def test_prewarmed_kernels_hold_the_largest_private_segment():
     """dg_init dispatches k_verify_items and k_verify_groups (the larger first) on the per-item stream, and
-    k_sign on every workspace stream, so each queue's scratch reaches its final size before any batch
+    k_rc_combine on every workspace stream, so each queue's scratch reaches its final size before any batch
     runs (a larger private segment needed later regrows the queue's scratch mid-pipeline: stalls, or
     HSA_STATUS_ERROR_OUT_OF_RESOURCES).  From the gfx950 code-object metadata of the built objects: the per-item
-    kernels hold the largest private segment of all, and k_sign the largest of every other kernel (the ones that
-    run on the workspace streams)."""
+    kernels hold the largest private segment of all; the other large-scratch kernels run on the per-item stream too
+    (k_clear_rounds, k_sign, k_hash_to_g2), and k_rc_combine holds the largest of every kernel that runs on the
+    workspace streams."""
     import tempfile
 
     from tools import resource_usage as RU
@@ -105,5 +106,6 @@ def test_prewarmed_kernels_hold_the_largest_private_segment():
     per_item = ("k_verify_groups", "k_verify_items")
     first = max(ks[k] for k in per_item)
     assert first == max(ks.values()), sorted(ks.items(), key=lambda x: -x[1])[:4]
-    rest = {k: v for k, v in ks.items() if k not in per_item}
-    assert ks["k_sign"] == max(rest.values()), sorted(rest.items(), key=lambda x: -x[1])[:4]
+    per_item_stream = per_item + ("k_clear_rounds", "k_sign", "k_hash_to_g2")
+    rest = {k: v for k, v in ks.items() if k not in per_item_stream}
+    assert ks["k_rc_combine"] == max(rest.values()), sorted(rest.items(), key=lambda x: -x[1])[:4]
