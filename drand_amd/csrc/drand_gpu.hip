@@ -209,7 +209,24 @@ hipEvent_t get_event() {
 
 // launch helper with optional per-kernel event timing
 template <typename... Args>
+int launch_shm(const char* name, void (*k)(Args...), uint32_t n_threads, uint32_t block, uint32_t shm, hipStream_t st,
+               Args... args);
+template <typename... Args>
 int launch(const char* name, void (*k)(Args...), uint32_t n_threads, uint32_t block, hipStream_t st, Args... args) {
+  return launch_shm(name, k, n_threads, block, 0u, st, args...);
+}
+// DG_VERIFY_LDS=<bytes> (A/B only): dynamic LDS per workgroup of the per-item pairing kernels, which caps their
+// workgroups (one wave each) per CU and so the scratch they keep in flight
+uint32_t verify_lds() {
+  static const uint32_t v = [] {
+    const char* e = getenv("DG_VERIFY_LDS");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  return v;
+}
+template <typename... Args>
+int launch_shm(const char* name, void (*k)(Args...), uint32_t n_threads, uint32_t block, uint32_t shm, hipStream_t st,
+               Args... args) {
   if (n_threads == 0) return 0;
   const uint32_t grid = (uint32_t)(((uint64_t)n_threads + block - 1) / block);
   Ctx& c = g_ctx;
@@ -219,7 +236,7 @@ int launch(const char* name, void (*k)(Args...), uint32_t n_threads, uint32_t bl
     e1 = get_event();
     (void)hipEventRecord(e0, st);
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, st, args...);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(block), shm, st, args...);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(DG_E_HIP, std::string("launch ") + name + ": " + hipGetErrorString(e));
   if (c.timing) {
@@ -647,7 +664,7 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
   st = g_ctx.shared_fb ? batch_st : g_ctx.fb_stream;
   HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
   RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, (const uint32_t*)flag, b.Q, H));
-  RET(launch("k_verify_items", k_verify_items, N, 64, st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
+  RET(launch_shm("k_verify_items", k_verify_items, N, 64, verify_lds(), st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
              (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status, batched_sub));
   HIPCHK(hipEventRecord(set.from_fb, st));
   st = batch_st;
@@ -950,7 +967,7 @@ int prefix_pass(uint32_t R, uint32_t k, uint32_t t, const uint64_t* seed, const 
     const uint32_t margin = grp < 2 ? 0u : (pass == 0 ? 6u : 2u);
     RET(launch("k_prefix_groups", k_prefix_groups, R, 128, st, R, k, t, pass == kPasses ? 1u : 0u, grp, margin,
                (const uint8_t*)status, (const uint8_t*)fin, glist));
-    RET(launch("k_verify_groups", k_verify_groups, (uint32_t)N, 64, st, k, (const uint32_t*)glist, seed, keys, item_slot,
+    RET(launch_shm("k_verify_groups", k_verify_groups, (uint32_t)N, 64, verify_lds(), st, k, (const uint32_t*)glist, seed, keys, item_slot,
                (const G2AStore*)H, S, status, fin, subgroup, g_ctx.gcount));
   }
   HIPCHK(hipEventRecord(set.from_fb, st));
