@@ -76,6 +76,27 @@ extern thread_local uint64_t g_fp_mul_count, g_fp_sqr_count, g_fp_inv_count;
 #define DG_COUNT_INV() ((void)0)
 #endif
 
+// 32-bit add / subtract with carry.  On the device through clang's carry builtins, which lower to the full-rate
+// v_add_co_u32 / v_addc_co_u32 (v_sub_co / v_subb_co) chains with the carry in VCC; the 64-bit form below was
+// compiled to 64-bit adds (v_lshl_add_u64) and sign shifts, ~8.4k of them in one Fp12 product of the per-item
+// pairing (DG_ADDC_BUILTIN=0 keeps it, A/B).
+#ifndef DG_ADDC_BUILTIN
+#define DG_ADDC_BUILTIN 1
+#endif
+#if DG_ADDC_BUILTIN && defined(__HIP_DEVICE_COMPILE__)
+DGI uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+  unsigned int co;
+  const uint32_t s = __builtin_addc(a, b, cin, &co);
+  *cout = co;
+  return s;
+}
+DGI uint32_t subb32(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+  unsigned int bo;
+  const uint32_t d = __builtin_subc(a, b, bin, &bo);
+  *bout = bo;
+  return d;
+}
+#else
 DGI uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
   uint64_t s = (uint64_t)a + b + cin;
   *cout = (uint32_t)(s >> 32);
@@ -86,6 +107,7 @@ DGI uint32_t subb32(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
   *bout = (uint32_t)(d >> 63);
   return (uint32_t)d;
 }
+#endif
 
 DGI Fp fp_const(const uint32_t (&c)[12]) {
   Fp r;
