@@ -552,6 +552,27 @@ DGI Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
 #ifndef DG_FP2_CALL
 #define DG_FP2_CALL 0
 #endif
+// DG_FP2_LAZY=1: every inlined Fp2 product (host builds, fp2_mul_r, fp2_mul_seq / fp2_mul_in) reduces lazily
+// (fp28.h fp28_fp2_mul_d: three digit products, two Montgomery reductions)
+#ifndef DG_FP2_LAZY
+#define DG_FP2_LAZY 0
+#endif
+DGI Fp2 fp2_mul_lazy(const Fp2& a, const Fp2& b) {
+  uint32_t x0[14], x1[14], y0[14], y1[14], r0[14], r1[14];
+  fp28_unpack(a.c0.l, x0);
+  fp28_unpack(a.c1.l, x1);
+  fp28_unpack(b.c0.l, y0);
+  fp28_unpack(b.c1.l, y1);
+  fp28_fp2_mul_d(x0, x1, y0, y1, r0, r1);
+  const uint32_t neg = 0u - (r0[13] >> 31);  // r0 in (-p, 0): add p (mod 2^384)
+  Fp2 r;
+  fp28_pack(r0, r.c0.l);
+  fp28_pack(r1, r.c1.l);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.c0.l[i] = addc32(r.c0.l[i], P_LIMBS[i] & neg, c, &c);
+  return Fp2{fp_reduce_once(r.c0), fp_reduce_once(r.c1)};
+}
 #if DG_FP2_CALL && defined(__HIP_DEVICE_COMPILE__) && DG_FP_CALL == 1
 __device__ __noinline__ Fp2 fp2_mul_r(DG_P12(a), DG_P12(b), DG_P12(c), DG_P12(d));
 __device__ __noinline__ Fp2 fp2_sqr_r(DG_P12(a), DG_P12(b));
@@ -559,10 +580,14 @@ DGI Fp2 fp2_mul(const Fp2& a, const Fp2& b) { return fp2_mul_r(DG_A12(a.c0), DG_
 DGI Fp2 fp2_sqr(const Fp2& a) { return fp2_sqr_r(DG_A12(a.c0), DG_A12(a.c1)); }
 #else
 DGH Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
+#if DG_FP2_LAZY && !(defined(__HIP_DEVICE_COMPILE__) && DG_FP_CALL == 1)
+  return fp2_mul_lazy(a, b);
+#else
   Fp t0 = fp_mul(a.c0, b.c0);
   Fp t1 = fp_mul(a.c1, b.c1);
   Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
   return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+#endif
 }
 DGH Fp2 fp2_sqr(const Fp2& a) {
   Fp m = fp_mul(a.c0, a.c1);
@@ -576,6 +601,9 @@ DGH Fp2 fp2_sqr(const Fp2& a) {
 #if defined(__HIP_DEVICE_COMPILE__) && DG_FP_CALL == 1
 __device__ __noinline__ Fp2 fp2_mul_r(DG_P12(a), DG_P12(b), DG_P12(c), DG_P12(d)) {
   const Fp x0{{DG_L12(a)}}, x1{{DG_L12(b)}}, y0{{DG_L12(c)}}, y1{{DG_L12(d)}};
+#if DG_FP2_LAZY
+  return fp2_mul_lazy(Fp2{x0, x1}, Fp2{y0, y1});
+#endif
   const Fp t0 = fp28_mul(x0, y0);
   const Fp t1 = fp28_mul(x1, y1);
   const Fp t2 = fp28_mul(fp_add(x0, x1), fp_add(y0, y1));
@@ -611,6 +639,17 @@ DGI Fp fp_mul_seq(Fp a, Fp b) {
   return r;
 }
 DGI Fp2 fp2_mul_seq(const Fp2& a, const Fp2& b) {
+#if DG_FP2_LAZY
+  Fp2 x = a, y = b;
+  DG_PIN_FP(x.c0);
+  DG_PIN_FP(x.c1);
+  DG_PIN_FP(y.c0);
+  DG_PIN_FP(y.c1);
+  Fp2 r = fp2_mul_lazy(x, y);
+  DG_PIN_FP(r.c0);
+  DG_PIN_FP(r.c1);
+  return r;
+#endif
   const Fp t0 = fp_mul_seq(a.c0, b.c0);
   const Fp t1 = fp_mul_seq(a.c1, b.c1);
   const Fp t2 = fp_mul_seq(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
@@ -622,6 +661,9 @@ DGI Fp2 fp2_sqr_seq(const Fp2& a) {
 }
 // and inlined (the products' code at every call site)
 DGI Fp2 fp2_mul_in(const Fp2& a, const Fp2& b) {
+#if DG_FP2_LAZY
+  return fp2_mul_lazy(a, b);
+#endif
   const Fp t0 = fp_mul_inl(a.c0, b.c0);
   const Fp t1 = fp_mul_inl(a.c1, b.c1);
   const Fp t2 = fp_mul_inl(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
@@ -757,7 +799,12 @@ DG12 Fp12 fp12_mul(const Fp12& a, const Fp12& b) {
   Fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
   return Fp12{fp6_add(t0, fp6_mul_v(t1)), c1};
 }
-DG12 Fp12 fp12_sqr(const Fp12& a) {
+#if defined(DG_ML_INLINE) && DG_ML_INLINE
+DGI
+#else
+DG12
+#endif
+Fp12 fp12_sqr(const Fp12& a) {
   // complex squaring: (a0 + a1 w)^2 = (a0^2 + v a1^2) + 2 a0 a1 w
   Fp6 ab = fp6_mul(a.c0, a.c1);
   Fp6 s = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
@@ -777,7 +824,17 @@ DGI void fp4_sqr(const Fp2& a, const Fp2& b, Fp2& c0, Fp2& c1) {
   c0 = fp2_add(fp2_mul_xi(t1), t0);
   c1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(a, b)), t0), t1);
 }
-DG12 Fp12 fp12_cyc_sqr(const Fp12& f) {
+// DG_CYC_INLINE=1: inlined into its only caller, the loop of cyc_exp_z (the accumulator then stays in registers
+// across the 63 squarings instead of crossing the call through the stack)
+#ifndef DG_CYC_INLINE
+#define DG_CYC_INLINE 1
+#endif
+#if DG_CYC_INLINE
+DGI
+#else
+DG12
+#endif
+Fp12 fp12_cyc_sqr(const Fp12& f) {
   Fp2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
   Fp2 t0, t1, t2, t3;
   fp4_sqr(z0, z1, t0, t1);
@@ -794,7 +851,15 @@ DG12 Fp12 fp12_cyc_sqr(const Fp12& f) {
 }
 
 // multiply by the sparse line l = c0 + c1 v + c4 v w (M-type twist; slots 0, 1, 4)
-DG12 Fp12 fp12_mul_014(const Fp12& f, const Fp2& c0, const Fp2& c1, const Fp2& c4) {
+#ifndef DG_ML_INLINE
+#define DG_ML_INLINE 1  // 0: out of line; 1: the line product and the squaring inlined into the Miller loop (A/B)
+#endif
+#if DG_ML_INLINE
+DGI
+#else
+DG12
+#endif
+Fp12 fp12_mul_014(const Fp12& f, const Fp2& c0, const Fp2& c1, const Fp2& c4) {
   Fp6 aa = fp6_mul_01(f.c0, c0, c1);
   Fp6 bb = fp6_mul_1(f.c1, c4);
   Fp6 s = fp6_mul_01(fp6_add(f.c0, f.c1), c0, fp2_add(c1, c4));

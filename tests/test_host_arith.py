@@ -235,3 +235,11 @@ def test_recover_sac_host_build(hc, t, seed):
     idx = list(range(t)) if seed < 0 else sorted(rng.sample(range(256), t))
     assert hc.hc_recover_sac_check(b"".join(sigs), (ctypes.c_uint32 * t)(*idx), t) == 1
 
+
+
+def test_fp2_lazy_product_matches_karatsuba(hc):
+    """DG_FP2_LAZY's product (fp28.h fp28_fp2_mul_d: signed column sums, two reductions, the negative c0 case
+    fixed up by + p) equals the three-reduction Karatsuba product, including all 81 combinations of 0, 1, p - 1."""
+    hc.hc_fp2_mul_lazy_check.restype = ctypes.c_int
+    hc.hc_fp2_mul_lazy_check.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
+    assert hc.hc_fp2_mul_lazy_check(0x9E3779B97F4A7C15, 20000) == 0
