@@ -819,10 +819,21 @@ DG12 Fp12 fp12_inv(const Fp12& a) {
 // Squaring in the cyclotomic subgroup (elements after the easy part of the final exponentiation), Granger-Scott:
 // Fp12 seen as three Fp4 = Fp2[s]/(s^2 - xi) pieces (c0.c0, c1.c1), (c1.c0, c0.c2), (c0.c1, c1.c2); 9 Fp2
 // squarings (18 Fp products) instead of the 36 of fp12_sqr.
+// DG_CYC_SQR: the Fp2 squarings of fp4_sqr as Fp-level calls (0), inlined and serialised (1), inlined (2)
+#ifndef DG_CYC_SQR
+#define DG_CYC_SQR 0
+#endif
+#if DG_CYC_SQR == 1
+#define DG_FP4_SQR2 fp2_sqr_seq
+#elif DG_CYC_SQR == 2
+#define DG_FP4_SQR2 fp2_sqr_in
+#else
+#define DG_FP4_SQR2 fp2_sqr
+#endif
 DGI void fp4_sqr(const Fp2& a, const Fp2& b, Fp2& c0, Fp2& c1) {
-  Fp2 t0 = fp2_sqr(a), t1 = fp2_sqr(b);
+  Fp2 t0 = DG_FP4_SQR2(a), t1 = DG_FP4_SQR2(b);
   c0 = fp2_add(fp2_mul_xi(t1), t0);
-  c1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(a, b)), t0), t1);
+  c1 = fp2_sub(fp2_sub(DG_FP4_SQR2(fp2_add(a, b)), t0), t1);
 }
 // DG_CYC_INLINE=1: inlined into its only caller, the loop of cyc_exp_z (the accumulator then stays in registers
 // across the 63 squarings instead of crossing the call through the stack)

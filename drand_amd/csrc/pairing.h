@@ -12,7 +12,13 @@ struct G2Proj {
   Fp2 x, y, z;
 };
 
-DG12 void line_dbl(G2Proj& T, Fp2& c0, Fp2& c1, Fp2& c4, const Fp& px, const Fp& py) {
+// DG_ML_INLINE=2 also inlines the line evaluations into the Miller loop (A/B)
+#if defined(DG_ML_INLINE) && DG_ML_INLINE >= 2
+DGI
+#else
+DG12
+#endif
+void line_dbl(G2Proj& T, Fp2& c0, Fp2& c1, Fp2& c4, const Fp& px, const Fp& py) {
   Fp2 a = fp2_mul_fp(fp2_mul(T.x, T.y), fp_const(FP_TWO_INV));
   Fp2 b = fp2_sqr(T.y);
   Fp2 c = fp2_sqr(T.z);
@@ -30,7 +36,12 @@ DG12 void line_dbl(G2Proj& T, Fp2& c0, Fp2& c1, Fp2& c4, const Fp& px, const Fp&
   T.z = fp2_mul(b, h);
 }
 
-DG12 void line_add(G2Proj& T, const Fp2& qx, const Fp2& qy, Fp2& c0, Fp2& c1, Fp2& c4, const Fp& px, const Fp& py) {
+#if defined(DG_ML_INLINE) && DG_ML_INLINE >= 2
+DGI
+#else
+DG12
+#endif
+void line_add(G2Proj& T, const Fp2& qx, const Fp2& qy, Fp2& c0, Fp2& c1, Fp2& c4, const Fp& px, const Fp& py) {
   Fp2 theta = fp2_sub(T.y, fp2_mul(qy, T.z));
   Fp2 lambda = fp2_sub(T.x, fp2_mul(qx, T.z));
   Fp2 c = fp2_sqr(theta);
