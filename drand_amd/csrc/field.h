@@ -821,7 +821,7 @@ DG12 Fp12 fp12_inv(const Fp12& a) {
 // squarings (18 Fp products) instead of the 36 of fp12_sqr.
 // DG_CYC_SQR: the Fp2 squarings of fp4_sqr as Fp-level calls (0), inlined and serialised (1), inlined (2)
 #ifndef DG_CYC_SQR
-#define DG_CYC_SQR 0
+#define DG_CYC_SQR 2
 #endif
 #if DG_CYC_SQR == 1
 #define DG_FP4_SQR2 fp2_sqr_seq

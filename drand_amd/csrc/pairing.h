@@ -86,8 +86,83 @@ DGI Fp12 miller_loop(const G1A* P, const G2A* Q, int np) {
   return fp12_conj(f);  // z < 0
 }
 
+// Compressed cyclotomic squaring (Karabina, "Squaring in cyclotomic subgroups", Math. Comp. 2013): an element of
+// the cyclotomic subgroup is determined by four of its six Fp2 coefficients, and squaring maps those four among
+// themselves.  Naming as in fp12_cyc_sqr: g0 = c0.c0, g1 = c1.c1, g2 = c1.c0, g3 = c0.c2, g4 = c0.c1, g5 = c1.c2.
+//   h2 = 2 g2 + 3 xi (2 g4 g5)          h3 = 3 (g4^2 + xi g5^2) - 2 g3
+//   h4 = 3 (g2^2 + xi g3^2) - 2 g4      h5 = 2 g5 + 3 (2 g2 g3)
+// six Fp2 squarings (2 g_i g_j = (g_i + g_j)^2 - g_i^2 - g_j^2) instead of Granger-Scott's nine.  Decompression
+// (g2 != 0): g1 = (xi g5^2 + 3 g4^2 - 2 g3) / (4 g2), g0 = xi (2 g1^2 + g2 g5 - 3 g3 g4) + 1.
+#ifndef DG_CYC_KARABINA
+#define DG_CYC_KARABINA 1
+#endif
+struct CycC {
+  Fp2 g2, g3, g4, g5;
+};
+DGI CycC cyc_sqr_c(const CycC& g) {
+  const Fp2 s2 = DG_FP4_SQR2(g.g2), s3 = DG_FP4_SQR2(g.g3), s4 = DG_FP4_SQR2(g.g4), s5 = DG_FP4_SQR2(g.g5);
+  const Fp2 b23 = fp2_sub(fp2_sub(DG_FP4_SQR2(fp2_add(g.g2, g.g3)), s2), s3);  // 2 g2 g3
+  const Fp2 b45 = fp2_sub(fp2_sub(DG_FP4_SQR2(fp2_add(g.g4, g.g5)), s4), s5);  // 2 g4 g5
+  const Fp2 t45 = fp2_mul_xi(b45);
+  const Fp2 a45 = fp2_add(s4, fp2_mul_xi(s5));
+  const Fp2 a23 = fp2_add(s2, fp2_mul_xi(s3));
+  CycC h;
+  h.g2 = fp2_add(fp2_dbl(g.g2), fp2_add(fp2_dbl(t45), t45));
+  h.g3 = fp2_sub(fp2_add(fp2_dbl(a45), a45), fp2_dbl(g.g3));
+  h.g4 = fp2_sub(fp2_add(fp2_dbl(a23), a23), fp2_dbl(g.g4));
+  h.g5 = fp2_add(fp2_dbl(g.g5), fp2_add(fp2_dbl(b23), b23));
+  return h;
+}
+// the full element from its compressed form, given inv = 1 / (4 g2)
+DGI Fp12 cyc_decompress(const CycC& g, const Fp2& inv) {
+  const Fp2 g44 = fp2_sqr(g.g4);
+  const Fp2 num = fp2_sub(fp2_add(fp2_mul_xi(fp2_sqr(g.g5)), fp2_add(fp2_dbl(g44), g44)), fp2_dbl(g.g3));
+  const Fp2 g1 = fp2_mul(num, inv);
+  const Fp2 g34 = fp2_mul(g.g3, g.g4);
+  const Fp2 t = fp2_sub(fp2_add(fp2_dbl(fp2_sqr(g1)), fp2_mul(g.g2, g.g5)), fp2_add(fp2_dbl(g34), g34));
+  const Fp2 g0 = fp2_add(fp2_mul_xi(t), fp2_one());
+  return Fp12{Fp6{g0, g.g4, g.g3}, Fp6{g.g2, g1, g.g5}};
+}
+
 // a^z for a in the cyclotomic subgroup (z < 0: conjugate of a^|z|), cyclotomic squarings
 DG12 Fp12 cyc_exp_z(const Fp12& a) {
+#if DG_CYC_KARABINA
+  // |z| = 2^63 + 2^62 + 2^60 + 2^57 + 2^48 + 2^16: the six powers a^(2^k) by 63 compressed squarings, their
+  // denominators inverted together (Montgomery's trick, one Fp2 inversion), then five products.  A zero
+  // denominator (g2 = 0 at some power, e.g. a = 1) takes the uncompressed chain below.
+  {
+    constexpr int NB = 6;
+    CycC s[NB];
+    Fp2 pre[NB];
+    CycC c{a.c1.c0, a.c0.c2, a.c0.c1, a.c1.c2};
+    int n = 0;
+    for (int k = 1; k <= 63; ++k) {
+      c = cyc_sqr_c(c);
+      if ((Z_ABS >> k) & 1) s[n++] = c;
+    }
+    bool zero = false;
+    Fp2 run = fp2_one();
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const Fp2 d = fp2_dbl(fp2_dbl(s[i].g2));
+      zero |= fp2_is_zero(d);
+      run = i ? fp2_mul(run, d) : d;
+      pre[i] = run;
+    }
+    if (!zero) {
+      Fp2 inv = fp2_inv(run);  // 1 / (d_0 ... d_5)
+      Fp12 acc = fp12_one();
+#pragma unroll
+      for (int i = NB - 1; i >= 0; --i) {
+        const Fp2 inv_i = i ? fp2_mul(inv, pre[i - 1]) : inv;
+        if (i) inv = fp2_mul(inv, fp2_dbl(fp2_dbl(s[i].g2)));
+        const Fp12 e = cyc_decompress(s[i], inv_i);
+        acc = (i == NB - 1) ? e : fp12_mul(acc, e);
+      }
+      return fp12_conj(acc);
+    }
+  }
+#endif
   Fp12 acc = a;
   for (int b = 62; b >= 0; --b) {
     acc = fp12_cyc_sqr(acc);

@@ -391,3 +391,50 @@ extern "C" int hc_fp2_mul_lazy_check(uint64_t seed, uint32_t n) {
   }
   return bad;
 }
+
+// cyc_exp_z (Karabina compressed squarings, batched decompression) against the Granger-Scott square-and-multiply
+// chain, on n cyclotomic elements f^((p^6 - 1)(p^2 + 1)) of pseudo-random f, plus the element 1 (every
+// denominator zero: the uncompressed fallback).  Returns the number of mismatches.
+extern "C" int hc_cyc_exp_check(uint64_t seed, uint32_t n) {
+  uint64_t s = seed | 1;
+  auto rnd_fp = [&s]() {
+    Fp a;
+    for (int i = 0; i < 12; i += 2) {
+      s ^= s << 13;
+      s ^= s >> 7;
+      s ^= s << 17;
+      a.l[i] = (uint32_t)s;
+      a.l[i + 1] = (uint32_t)(s >> 32);
+    }
+    a.l[11] &= 0x1fffffffu;
+    return fp_reduce_once(fp_reduce_once(fp_reduce_once(a)));
+  };
+  auto gs = [](const Fp12& a) {
+    Fp12 acc = a;
+    for (int b = 62; b >= 0; --b) {
+      acc = fp12_cyc_sqr(acc);
+      if ((Z_ABS >> b) & 1) acc = fp12_mul(acc, a);
+    }
+    return fp12_conj(acc);
+  };
+  int bad = 0;
+  for (uint32_t it = 0; it <= n; ++it) {
+    Fp12 f2 = fp12_one();
+    if (it < n) {
+      Fp12 f;
+      Fp* c[12] = {&f.c0.c0.c0, &f.c0.c0.c1, &f.c0.c1.c0, &f.c0.c1.c1, &f.c0.c2.c0, &f.c0.c2.c1,
+                   &f.c1.c0.c0, &f.c1.c0.c1, &f.c1.c1.c0, &f.c1.c1.c1, &f.c1.c2.c0, &f.c1.c2.c1};
+      for (int i = 0; i < 12; ++i) *c[i] = rnd_fp();
+      const Fp12 f1 = fp12_mul(fp12_conj(f), fp12_inv(f));
+      f2 = fp12_mul(fp12_frob(fp12_frob(f1)), f1);
+    }
+    const Fp12 x = cyc_exp_z(f2), y = gs(f2);
+    const Fp6* u[2] = {&x.c0, &x.c1};
+    const Fp6* v[2] = {&y.c0, &y.c1};
+    bool eq = true;
+    for (int h = 0; h < 2; ++h)
+      eq = eq && fp2_eq(u[h]->c0, v[h]->c0) && fp2_eq(u[h]->c1, v[h]->c1) && fp2_eq(u[h]->c2, v[h]->c2);
+    bad += !eq;
+  }
+  return bad;
+}

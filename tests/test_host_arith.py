@@ -243,3 +243,12 @@ def test_fp2_lazy_product_matches_karatsuba(hc):
     hc.hc_fp2_mul_lazy_check.restype = ctypes.c_int
     hc.hc_fp2_mul_lazy_check.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
     assert hc.hc_fp2_mul_lazy_check(0x9E3779B97F4A7C15, 20000) == 0
+
+
+def test_karabina_exponentiation_matches_granger_scott(hc):
+    """pairing.h cyc_exp_z (compressed squarings, one batched Fp2 inversion for the six decompressions) equals the
+    Granger-Scott square-and-multiply chain on cyclotomic elements, and the all-zero-denominator fallback (a = 1)
+    returns 1."""
+    hc.hc_cyc_exp_check.restype = ctypes.c_int
+    hc.hc_cyc_exp_check.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
+    assert hc.hc_cyc_exp_check(0xD1CE5EED, 24) == 0
