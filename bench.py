@@ -86,20 +86,29 @@ def traffic_of(kernel, config="head"):
     return t["bytes_per_launch"] if t else None
 
 
-def load_chain(total):
-    """sigs (total, 96) of rounds 1..total of the synthetic chain (the smallest chain file that holds them)."""
-    best = None
-    d = os.path.join(ROOT, "data")
-    if os.path.isdir(d):
-        for f in os.listdir(d):
-            if f.startswith("chain_v1_") and f.endswith(".bin"):
-                n = int(f[len("chain_v1_"):-4])
-                if n >= total and (best is None or n < best[0]):
-                    best = (n, os.path.join(d, f))
-    if best is None:
+def load_chain(total, data_dir=None):
+    """sigs (total, 96) of rounds 1..total of the synthetic linked chain: the smallest chain file that holds them,
+    checked against its pinned SHA-256 (tools/synthetic.CHAIN_SHA256).  None when no file covers `total` (or the
+    covering file fails its digest: logged)."""
+    try:
+        n, path = S.find_chain(total, data_dir)
+    except S.ChainFileError as e:
+        log("chain:", e)
         return None
-    mm = np.memmap(best[1], dtype=np.uint8, mode="r", shape=(best[0], 96))
+    mm = np.memmap(path, dtype=np.uint8, mode="r", shape=(n, 96))
     return np.array(mm[:total])
+
+
+def require_chain(total, allow_unlinked, data_dir=None):
+    """The chain rounds a timed line verifies.  Without a pinned chain file that covers them the bench exits
+    non-zero (status 3) unless --allow-unlinked was given: a configs[1]/[3] line must never silently turn into
+    unlinked rounds signed by the library under test."""
+    chain = load_chain(total, data_dir)
+    if chain is None and not allow_unlinked:
+        log("no digest-pinned chain file covers %d rounds: refusing to measure unlinked GPU-signed rounds "
+            "(--allow-unlinked overrides; tools/gen_chain.py %d makes the file)" % (total, total))
+        sys.exit(3)
+    return chain
 
 
 def gpu_signed_rounds(lib_tbls, first, n, x):
@@ -224,13 +233,37 @@ def cpu_recover(commits, t, n, msgs, parts, threads, seconds=8.0, label=""):
                       % (R, label, threads, dt)}, (rs, ss, R)
 
 
+def cpu_verify_partials(commits, msgs, parts, threads, seconds=6.0):
+    """VerifyPartial (beacon/beacon.go:148: PubPoly.Eval of the share's index + bls.Verify) on the host, one CPU-twin
+    call per partial, `threads` at once (ctypes releases the GIL), over a bounded sample of the same partials ->
+    partials/s."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import twin
+
+    R, n = parts.shape[0], parts.shape[1]
+    items = [(r, j) for r in range(R) for j in range(n)]
+    t0 = time.time()
+    twin.verify_partial(commits, bytes(msgs[0]), bytes(parts[0, 0]))
+    per = time.time() - t0
+    m = int(min(len(items), max(threads, seconds * threads / max(per, 1e-6))))
+    t0 = time.time()
+    with ThreadPoolExecutor(threads) as ex:
+        st = list(ex.map(lambda it: twin.verify_partial(commits, bytes(msgs[it[0]]), bytes(parts[it[0], it[1]])),
+                         items[:m]))
+    dt = time.time() - t0
+    assert not any(st), "CPU twin rejected a valid partial"
+    return m / dt, "%d partials (first %d rounds x %d), CPU twin VerifyPartial, %d threads, %.1f s" % (
+        m, -(-m // n), n, threads, dt)
+
+
 class RoundSource:
     """Rounds 1..total with their prev_sig and signature for the Recover lines: the linked chain file when one
     holds them, else GPU-signed rounds whose prev_sig is pseudo-random (gpu_signed_rounds: the same per-round
     work; only the syncFrom line needs the links and is skipped then)."""
 
-    def __init__(self, tbls, total):
-        chain = load_chain(total)
+    def __init__(self, tbls, total, allow_unlinked=False):
+        chain = require_chain(total, allow_unlinked)
         self.linked = chain is not None
         if self.linked:
             self.sigs = chain
@@ -329,6 +362,38 @@ def recover_bench(L, tbls, shard, src, R_total, t, n, world, rank, peak, steps=2
     assert not grs.any() and np.array_equal(gs, src.sigs[:R_total]), "recovered signatures differ from the chain"
     assert (gss[:, :t] == 0).all() and (gss[:, t:] == 255).all(), "share statuses"
     dt = min(dts)
+    # BASELINE configs[2] as written: VerifyPartial of EVERY partial (ProcessBeacon, beacon/beacon.go:148: all n of
+    # every round) + Recover (:488).  Timed as dg_verify_partials_dev over all R x n partials, then (a) kyber's
+    # Recover, which re-verifies the examined prefix (the dg_recover_dev time above), and (b) the Lagrange half
+    # from those verdicts (dg_recover_verified_dev).
+    tbls.verify_partial_batch_dev(pub, d_msgs, d_parts, seed=3)  # warmup (workspace growth at R x n items)
+    vdts = []
+    for s in range(steps):
+        d_vst, vdt = timed_ranks(lambda: tbls.verify_partial_batch_dev(pub, d_msgs, d_parts, seed=30 + s), world)
+        vdts.append(vdt)
+    vdt = min(vdts)
+    assert int(d_vst.max().item()) == 0, "VerifyPartial rejected a valid partial"
+    tbls.recover_verified_batch_dev(d_parts, d_vst, t, n)  # warmup
+    (vs, vrs, vss), rvdt = timed_ranks(lambda: tbls.recover_verified_batch_dev(d_parts, d_vst, t, n), world)
+    assert not int(vrs.max().item()) and torch.equal(vs, sigs), "Recover from the verdicts differs"
+    L.check(L.lib().dg_set_timing(1))
+    tbls.verify_partial_batch_dev(pub, d_msgs, d_parts, seed=8)
+    vkt = L.timings()
+    L.check(L.lib().dg_set_timing(0))
+    vroof = roofline_of(vkt, {"k_exp_pm3d4": 4 * R + 2 * R * n, "k_dec_p1": R * n, "k_dec_p2": R * n,
+                              "k_dec_p3": R * n}, peak, {"timing": "HIP events on the launch stream, one call"}, "c3vp")
+    vp_line = {"metric": "BASELINE configs[2]: VerifyPartial on all %d shares of every round + Lagrange Recover, n=%d "
+                         "t=%d (recovers/s)" % (n, n, t),
+               "value": R_total / (vdt + dt + gdt), "unit": "recovers/s",
+               "value_recover_from_verdicts": R_total / (vdt + rvdt + gdt),
+               "partials_verified_per_s": R_total * n / vdt, "verify_partials_s": vdt, "recover_s": dt,
+               "recover_from_verdicts_s": rvdt, "roofline": vroof,
+               "kernel_avg_us": {k_: round(v[0], 1) for k_, v in vkt.items()},
+               "note": "value: dg_verify_partials_dev over all R x n partials (HBM-resident) + kyber Recover "
+                       "(dg_recover_dev, which re-verifies its examined prefix); value_recover_from_verdicts: the "
+                       "same VerifyPartial pass + dg_recover_verified_dev (Lagrange from the verdicts, no second "
+                       "pairing); every status OK and every signature equal to the chain's"}
+    del d_vst
     # the host-buffer entry point (dg_recover): the 98 B partials cross PCIe inside the call
     (hs, hrs, hss), host_dt = timed_ranks(lambda: tbls.recover_batch(pub, msgs, parts, t, n, seed=7), world)
     assert np.array_equal(hs, gs[a:b]) and np.array_equal(hss, gss[a:b]), "host and device Recover differ"
@@ -352,7 +417,7 @@ def recover_bench(L, tbls, shard, src, R_total, t, n, world, rank, peak, steps=2
            "note": "inputs resident in HBM (dg_recover_dev), outputs all-gathered (RCCL) and equal to the chain's "
                    "signatures; host_api_value: the host-buffer dg_recover, with the PCIe transfer of %d MB of "
                    "partials per GPU inside the call" % (R * n * 98 // 10**6)}
-    return out, (commits, msgs, parts)
+    return out, (commits, msgs, parts), vp_line
 
 
 def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=256, frac=0.10, n_short=3):
@@ -360,7 +425,7 @@ def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=
     cycling modes of tools/corrupt.py, plus `n_short` rounds with more than n - t corrupted shares (-> "not
     enough shares"); each rank its contiguous range of R_total rounds through dg_recover_dev (inputs resident
     in HBM; the batch equation fails, so the examined prefix of every round takes the per-item pass: group
-    tests of up to 4 shares -- a passed group's members are accepted with error probability <= 2^-64 -- and
+    tests of up to 4 shares -- a passed group's members are accepted with error probability <= 2^-63 (odd 64-bit weights) -- and
     single pairing checks for the members of failed groups; DG_GROUP=1 makes every check a single one), then
     the all-gather of the outputs.  Checked without the CPU: recovered signatures equal the chain's, exactly the short rounds
     report NOT_ENOUGH, every examined corrupted share is rejected and every examined clean one accepted
@@ -597,7 +662,20 @@ def headline_roofline(kt, kt_iso, per, peak, G, steps, world, dt):
 
 # keys of a sub-line (recover, adversarial, ...) that go to the side file instead of the printed line
 SIDE_KEYS = ("kernel_avg_us", "kernel_avg_us_isolated", "kernel_time_share", "note", "sample", "partials_generated_s",
-             "setup_s", "checks_by_members", "timing")
+             "setup_s", "checks_by_members", "timing", "allgather_s", "host_api_s_per_step", "rounds_per_gpu",
+             "partials_per_round", "recover_s", "recover_from_verdicts_s")
+
+
+# sub-lines print a short metric name (the full description is in the side file), and only these roofline and
+# cpu_baseline fields: the whole line must stay under 4 KB
+SHORT_METRIC = {"recover": "configs[2] kyber Recover/s, n=64 t=33 (examined prefix verified)",
+                "c2_verify_all": "configs[2] VerifyPartial(all 64) + Recover, recovers/s",
+                "adversarial": "configs[4] adversarial Recover/s, n=256 t=129, 10% corrupted",
+                "c1": "configs[0] n=5 t=3: 5 Signs + Recover + VerifyRecovered, rounds/s",
+                "live_latency": "live round n=64 t=33, ms per call",
+                "sync": "syncFrom catch-up rounds/s"}
+SUB_ROOF = ("kernel", "achieved", "peak", "unit", "frac", "traffic", "issue_frac", "kernel_avg_us")
+SUB_CPU = ("value", "unit", "cores", "kind", "all_host_cpus_linear_est", "statuses_match_gpu")
 
 
 def report(rank, world, head, roof, cpu, lines, tables, tables_out):
@@ -620,12 +698,15 @@ def report(rank, world, head, roof, cpu, lines, tables, tables_out):
             continue
         line = dict(line)
         side[name] = {k: line.pop(k) for k in SIDE_KEYS if k in line}
+        if name in SHORT_METRIC and "metric" in line:  # the long description goes to the side file
+            side[name]["metric"] = line["metric"]
+            line["metric"] = SHORT_METRIC[name]
         if isinstance(line.get("roofline"), dict):
             side[name]["roofline"] = line["roofline"]
-            line["roofline"] = compact_roofline(line["roofline"])
+            line["roofline"] = {k: v for k, v in compact_roofline(line["roofline"]).items() if k in SUB_ROOF}
         if isinstance(line.get("cpu_baseline"), dict):
             side[name]["cpu_baseline"] = line["cpu_baseline"]
-            line["cpu_baseline"] = {k: v for k, v in line["cpu_baseline"].items() if k != "sample"}
+            line["cpu_baseline"] = {k: v for k, v in line["cpu_baseline"].items() if k in SUB_CPU}
         out[name] = line
     if isinstance(cpu, dict) and "sample" in cpu:
         side["cpu_baseline"] = cpu
@@ -675,6 +756,9 @@ def main():
                     help="rounds per step over all GPUs (default 100k at N = 1, the 1M chain at N > 1)")
     ap.add_argument("--batch", type=int, default=100000, help="max rounds per device batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--allow-unlinked", action="store_true",
+                    help="without a digest-pinned chain file, measure GPU-signed unlinked rounds (labelled so in "
+                         "`data`) instead of exiting with status 3")
     ap.add_argument("--sync", dest="use_sync", action="store_true",
                     help="blocking dg_verify_beacons_dev per batch (default: dg_verify_beacons_dev_async, so the "
                          "latency-bound tail of one batch overlaps the head of the next)")
@@ -711,6 +795,9 @@ def main():
     if world != args.gpus:
         log("world size %d != --gpus %d" % (world, args.gpus))
         sys.exit(2)
+    # the chain before anything touches the GPU: no pinned file covering G rounds -> exit 3 (require_chain)
+    G = args.global_rounds or (100000 if world == 1 else 1000000)
+    chain = require_chain(G, args.allow_unlinked)
 
     import torch
     import torch.distributed as dist
@@ -724,12 +811,10 @@ def main():
     from drand_amd import tbls, shard
 
     lib = L.lib(local)
-    G = args.global_rounds or (100000 if world == 1 else 1000000)
     x = S.master_secret()
     pk = S.GROUP_PK  # x * g1, the chain's group key (public fixture constant)
     a, b = shard.round_range(G, world, rank)
     n = b - a
-    chain = load_chain(G)
     if chain is not None:
         sigs = chain[a:b]
         prev = chain[a - 1:b - 1] if a > 0 else np.concatenate([np.zeros((1, 96), np.uint8), chain[:b - 1]])
@@ -846,13 +931,14 @@ def main():
     torch.cuda.empty_cache()
 
     # Recover lines (sharded like the headline; chain rounds 1..R)
-    rec = adv = syn = c1 = lat = None
+    rec = adv = syn = c1 = lat = c2 = None
     rec_in = adv_in = None
     src = None
     if args.recover_rounds or args.c5_rounds or args.sync_rounds:
-        src = RoundSource(tbls, max(args.recover_rounds, args.c5_rounds + 1, args.sync_rounds, 1000))
+        src = RoundSource(tbls, max(args.recover_rounds, args.c5_rounds + 1, args.sync_rounds, 1000),
+                          args.allow_unlinked)
     if args.recover_rounds:
-        rec, rec_in = recover_bench(L, tbls, shard, src, args.recover_rounds, 33, 64, world, rank, peak)
+        rec, rec_in, c2 = recover_bench(L, tbls, shard, src, args.recover_rounds, 33, 64, world, rank, peak)
     if args.c5_rounds:
         adv, adv_in = adversarial_bench(L, tbls, shard, src, args.c5_rounds, world, rank, peak)
     if rank == 0:
@@ -874,6 +960,12 @@ def main():
         if rec_in is not None:
             cb, _ = cpu_recover(rec_in[0], 33, 64, rec_in[1], rec_in[2], th, label="C3 n=64 t=33")
             rec["cpu_baseline"] = cpu_label(cb, th, machine, quota)
+            if c2 is not None:
+                # configs[2] on the host: every partial VerifyPartial'd, then kyber's Recover
+                vps, vsample = cpu_verify_partials(rec_in[0], rec_in[1], rec_in[2], th)
+                c2["cpu_baseline"] = cpu_label({"value": 1.0 / (64 / vps + 1.0 / cb["value"]), "unit": "recovers/s",
+                                                "kind": "port", "partials_verified_per_s": vps,
+                                                "sample": vsample + "; Recover: " + cb["sample"]}, th, machine, quota)
         if adv_in is not None:
             cb, (trs, tss, Rs) = cpu_recover(adv_in[0], 129, 256, adv_in[1], adv_in[2], th, seconds=6.0,
                                              label="C5 n=256 t=129 corrupted")
@@ -894,7 +986,7 @@ def main():
     tables = {"kernel_time_share": share, "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
               "kernel_avg_us_isolated": {k: round(v[0], 1) for k, v in kt_iso.items()}, "peak": peak}
     report(rank, world, head, roof, cpu, {"recover": rec, "adversarial": adv, "c1": c1, "live_latency": lat,
-                                          "sync": syn}, tables, args.tables_out)
+                                          "sync": syn, "c2_verify_all": c2}, tables, args.tables_out)
     if world > 1:
         dist.destroy_process_group()
 

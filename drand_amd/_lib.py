@@ -54,6 +54,8 @@ SIGNATURES = {
     "dg_group_counts": ([_P], _I),
     "dg_set_group_size": ([_U32], _I),
     "dg_recover_dev": ([_P, _U32, _U32, _SZ, _P, _SZ, _U32, _P, _P, _P, _P, _U64], _I),
+    "dg_verify_partials_dev": ([_P, _U32, _SZ, _P, _SZ, _U32, _P, _P, _U64], _I),
+    "dg_recover_verified_dev": ([_U32, _U32, _SZ, _U32, _P, _P, _P, _P, _P], _I),
     "dg_set_timing": ([_I], _I),
     "dg_last_timings": ([_P, _P, _P, _I], _I),
 }

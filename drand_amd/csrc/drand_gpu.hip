@@ -917,13 +917,12 @@ int plan_slots(const uint8_t* commits48, uint32_t t, uint32_t R, uint32_t k, uin
   return 0;
 }
 
-// VerifyPartial over R rounds x k partials: keys X_i = PubPoly.Eval(i) for every distinct index
-int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const uint8_t* msgs, uint32_t msg_len,
-                        uint32_t k, const uint8_t* partials98, uint64_t seed, hipStream_t st, uint8_t** d_status) {
+// VerifyPartial over R rounds x k partials (messages d_m and 98 B records d_p in device memory): keys X_i =
+// PubPoly.Eval(i) for every distinct index; the statuses are left in *d_status (stream order)
+int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const uint8_t* d_m, uint32_t msg_len,
+                        uint32_t k, const uint8_t* d_p, uint64_t seed, hipStream_t st, uint8_t** d_status) {
   const size_t N = (size_t)R * k;
-  uint8_t *d_m, *d_p, *kst;
-  RET(upload(S_MSGS, msgs, (size_t)R * msg_len, &d_m, st));
-  RET(upload(S_IN1, partials98, N * 98, &d_p, st));
+  uint8_t* kst;
   G1AStore* keys;
   uint32_t *d_itemslot, nslots;
   RET(plan_slots(commits48, t, R, k, k, d_p, st, &keys, &kst, &d_itemslot, &nslots));
@@ -1022,6 +1021,9 @@ int recover_windowed(const uint8_t* commits48, uint32_t t, uint32_t R, const uin
   RET(wsT(S_FIN, N, &fin));
   RET(wsT(S_INC, 4, &inc));
   HIPCHK(hipMemsetAsync(inc, 0, 16, st));
+  // items beyond the window start as "not examined" (the fast path never decodes them; the slow path overwrites
+  // them below), so no status of an earlier batch survives in the reused buffer
+  if (w < k) HIPCHK(hipMemsetAsync(status, DG_ST_NOT_EXAMINED_, N, st));
   constexpr uint32_t kQ = sizeof(G2AStore) / 16;
   static_assert(sizeof(G2AStore) % 16 == 0, "G2AStore rows move as uint4");
   RET(launch("k_rows", k_rows<uint4>, (uint32_t)(Nw * kQ), 256, st, R, w, kQ, w, 0u, k, 0u, (const uint4*)Sw, (uint4*)S));
@@ -1682,10 +1684,29 @@ int dg_verify_partials(const uint8_t* commits48, uint32_t t, size_t rounds, cons
   RET(check_args_n(rounds * (size_t)k));
   hipStream_t st;
   RET(acquire_set0(&st));
-  uint8_t* d_st;
-  RET(verify_partials_dev(commits48, t, (uint32_t)rounds, msgs, (uint32_t)msg_len, k, partials98, fresh_seed(seed), st,
-                          &d_st));
+  uint8_t *d_st, *d_m, *d_p;
+  RET(upload(S_MSGS, msgs, rounds * msg_len, &d_m, st));
+  RET(upload(S_IN1, partials98, rounds * k * 98, &d_p, st));
+  RET(verify_partials_dev(commits48, t, (uint32_t)rounds, d_m, (uint32_t)msg_len, k, d_p, fresh_seed(seed), st, &d_st));
   HIPCHK(hipMemcpyAsync(status, d_st, rounds * k, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (g_ctx.timing) collect_timings();
+  return 0;
+}
+
+int dg_verify_partials_dev(const uint8_t* commits48, uint32_t t, size_t rounds, const uint8_t* d_msgs, size_t msg_len,
+                           uint32_t k, const uint8_t* d_partials98, uint8_t* d_status, uint64_t seed) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  if (rounds == 0 || k == 0) return 0;
+  if (!commits48 || t == 0 || !d_msgs || !d_partials98 || !d_status) return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(rounds * (size_t)k));
+  hipStream_t st;
+  RET(acquire_set0(&st));
+  uint8_t* d_st;
+  RET(verify_partials_dev(commits48, t, (uint32_t)rounds, d_msgs, (uint32_t)msg_len, k, d_partials98, fresh_seed(seed),
+                          st, &d_st));
+  HIPCHK(hipMemcpyAsync(d_status, d_st, rounds * k, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipStreamSynchronize(st));
   if (g_ctx.timing) collect_timings();
   return 0;
@@ -1755,6 +1776,29 @@ int dg_recover_verified(uint32_t t, uint32_t nshares, size_t rounds, uint32_t k,
   RET(launch("k_decode_verified", k_decode_verified, (uint32_t)N, 128, st, (uint32_t)N, (const uint8_t*)d_p,
              (const uint8_t*)d_vst, d_S, d_st));
   return recover_tail(R, k, t, d_p, d_st, d_S, out_sig96, round_status, share_status, st);
+}
+
+int dg_recover_verified_dev(uint32_t t, uint32_t nshares, size_t rounds, uint32_t k, const uint8_t* d_partials98,
+                            const uint8_t* d_verified_status, uint8_t* d_out_sig96, uint8_t* d_round_status,
+                            uint8_t* d_share_status) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  (void)nshares;
+  if (rounds == 0) return 0;
+  if (t == 0 || k == 0 || !d_partials98 || !d_verified_status || !d_out_sig96 || !d_round_status || !d_share_status)
+    return fail(DG_E_ARG, "bad arguments");
+  RET(check_args_n(rounds * (size_t)(k > t ? k : t)));
+  hipStream_t st;
+  RET(acquire_set0(&st));
+  const uint32_t R = (uint32_t)rounds;
+  const size_t N = (size_t)R * k;
+  uint8_t* d_st;
+  G2AStore* d_S;
+  RET(wsT(S_STATUS, N, &d_st));
+  RET(wsT(S_S, N, &d_S));
+  RET(launch("k_decode_verified", k_decode_verified, (uint32_t)N, 128, st, (uint32_t)N, d_partials98, d_verified_status,
+             d_S, d_st));
+  return recover_tail(R, k, t, d_partials98, d_st, d_S, d_out_sig96, d_round_status, d_share_status, st);
 }
 
 }  // extern "C"

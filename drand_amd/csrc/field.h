@@ -329,6 +329,20 @@ DGH Fp fp_inv_fermat(const Fp& a) { return fp_pow_sched(a, EXP_PM2_FIRST, EXP_PM
 // limbs (the modinv32 organisation of libsecp256k1, restated for the 381-bit p).  37 batches = 1110
 // divsteps >= the proven bound (49 * 381 + 57) / 17 = 1102 for 381-bit inputs.  ~35k simple integer
 // instructions instead of a 455-multiplication exponentiation; public inputs only (verification).
+//
+// s30_divsteps / s30_update_de / s30_update_fg / s30_normalize adapt libsecp256k1's src/modinv32_impl.h
+// (secp256k1_modinv32_divsteps_30, _update_de_30, _update_fg_30, _normalize_30), which carries this notice:
+//   Copyright (c) 2020 Peter Dettman, Pieter Wuille.  Distributed under the MIT software license:
+//   Permission is hereby granted, free of charge, to any person obtaining a copy of this software and
+//   associated documentation files (the "Software"), to deal in the Software without restriction, including
+//   without limitation the rights to use, copy, modify, merge, publish, distribute, sublicense, and/or sell
+//   copies of the Software, and to permit persons to whom the Software is furnished to do so, subject to the
+//   following conditions: The above copyright notice and this permission notice shall be included in all copies
+//   or substantial portions of the Software.  THE SOFTWARE IS PROVIDED "AS IS", WITHOUT WARRANTY OF ANY KIND,
+//   EXPRESS OR IMPLIED, INCLUDING BUT NOT LIMITED TO THE WARRANTIES OF MERCHANTABILITY, FITNESS FOR A PARTICULAR
+//   PURPOSE AND NONINFRINGEMENT.  IN NO EVENT SHALL THE AUTHORS OR COPYRIGHT HOLDERS BE LIABLE FOR ANY CLAIM,
+//   DAMAGES OR OTHER LIABILITY, WHETHER IN AN ACTION OF CONTRACT, TORT OR OTHERWISE, ARISING FROM, OUT OF OR IN
+//   CONNECTION WITH THE SOFTWARE OR THE USE OR OTHER DEALINGS IN THE SOFTWARE.
 constexpr int S30_N = 13;
 struct S30 {
   int32_t v[S30_N];
@@ -788,6 +802,17 @@ DGI Fp6 fp6_mul_1(const Fp6& a, const Fp2& b1) {
 
 // ------------------------------------------------------------------------------------------- Fp12
 DGI Fp12 fp12_one() { return Fp12{Fp6{fp2_one(), fp2_zero(), fp2_zero()}, fp6_zero()}; }
+// DG_ML_INLINE: 0 keeps the Miller loop's sparse line product out of line; 1 (default) inlines it into the loop body
+// of miller_loop (pairing.h); 2 also the line evaluations.  DG_ML_SQR_INLINE=1 inlines fp12_sqr as well.  Until
+// round 3 fp12_sqr tested DG_ML_INLINE before the default was defined, so every shipped and measured build kept the
+// squaring out of line; defining it inline grows the per-item kernels' private segment 11.4 -> 15.0 KB, so the
+// default stays what was measured (0).
+#ifndef DG_ML_INLINE
+#define DG_ML_INLINE 1
+#endif
+#ifndef DG_ML_SQR_INLINE
+#define DG_ML_SQR_INLINE 0
+#endif
 DGI bool fp12_is_one(const Fp12& a) {
   return fp2_eq(a.c0.c0, fp2_one()) && fp2_is_zero(a.c0.c1) && fp2_is_zero(a.c0.c2) && fp2_is_zero(a.c1.c0) &&
          fp2_is_zero(a.c1.c1) && fp2_is_zero(a.c1.c2);
@@ -799,7 +824,7 @@ DG12 Fp12 fp12_mul(const Fp12& a, const Fp12& b) {
   Fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
   return Fp12{fp6_add(t0, fp6_mul_v(t1)), c1};
 }
-#if defined(DG_ML_INLINE) && DG_ML_INLINE
+#if DG_ML_SQR_INLINE
 DGI
 #else
 DG12
@@ -862,9 +887,6 @@ Fp12 fp12_cyc_sqr(const Fp12& f) {
 }
 
 // multiply by the sparse line l = c0 + c1 v + c4 v w (M-type twist; slots 0, 1, 4)
-#ifndef DG_ML_INLINE
-#define DG_ML_INLINE 1  // 0: out of line; 1: the line product and the squaring inlined into the Miller loop (A/B)
-#endif
 #if DG_ML_INLINE
 DGI
 #else

@@ -485,7 +485,7 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_clear_rounds(uint32_t R, 
 // checked together, e(sum_i rho_i X_i, H_r) == e(g1, sum_i rho_i S_i) with independent 64-bit rho_i from the
 // batch's bound seed.  Every S_i is in G2 (subgroup-checked here as in verify_item) and H_r is in G2, so a
 // member with x_i H_r != S_i makes the sum vanish for at most one rho_i value mod r: a group with a bad
-// member passes with probability <= 2^-64.  A passed group gives every member kyber's nil verdict; the
+// member passes with probability <= 2^-63 (rho_i is odd: 2^63 values).  A passed group gives every member kyber's nil verdict; the
 // members of a failed group are marked for their own check (fin = FIN_RECHECK) in the next pass, which
 // decides every verdict Recover reads.  At f = 10% and GRP = 4 that is ~0.6 pairing checks per item.
 constexpr uint32_t GRP = 4;

@@ -158,6 +158,36 @@ def recover_batch_dev(pub: PubPoly, d_msgs, d_partials, t, n, seed=0):
     return out, rs, ss
 
 
+def verify_partial_batch_dev(pub: PubPoly, d_msgs, d_partials, seed=0):
+    """verify_partial_batch with device-resident inputs and output (dg_verify_partials_dev): d_msgs (R, msg_len),
+    d_partials (R, k, 98) uint8 torch tensors on the current GPU -> statuses (R, k) device tensor."""
+    import torch
+
+    R, k = d_partials.shape[0], d_partials.shape[1]
+    st = torch.empty((R, k), dtype=torch.uint8, device=d_partials.device)
+    c = pub.commits_array()
+    torch.cuda.current_stream(d_partials.device).synchronize()
+    L.check(L.lib().dg_verify_partials_dev(L.ptr(c), c.shape[0], R, L.ptr(d_msgs), d_msgs.shape[1], k,
+                                           L.ptr(d_partials), L.ptr(st), seed))
+    return st
+
+
+def recover_verified_batch_dev(d_partials, d_verified_status, t, n):
+    """recover_verified_batch with device-resident partials (R, k, 98), verdicts (R, k) and outputs
+    (dg_recover_verified_dev) -> device tensors (sigs (R, 96), round_status (R,), share_status (R, k))."""
+    import torch
+
+    R, k = d_partials.shape[0], d_partials.shape[1]
+    dev = d_partials.device
+    out = torch.empty((R, 96), dtype=torch.uint8, device=dev)
+    rs = torch.empty(R, dtype=torch.uint8, device=dev)
+    ss = torch.empty((R, k), dtype=torch.uint8, device=dev)
+    torch.cuda.current_stream(dev).synchronize()
+    L.check(L.lib().dg_recover_verified_dev(t, n, R, k, L.ptr(d_partials), L.ptr(d_verified_status), L.ptr(out),
+                                            L.ptr(rs), L.ptr(ss)))
+    return out, rs, ss
+
+
 def recover_verified_batch(pub: PubPoly, msgs, partials, verified_status, t, n):
     """The live round's Recover (beacon/beacon.go:472-494) with the VerifyPartial verdicts ProcessBeacon
     already holds (beacon/beacon.go:148): partials (R, k, 98), verified_status (R, k) DG_ST_* ->

@@ -207,17 +207,11 @@ func (s *Scheme) VerifyPartialBatch(public *share.PubPoly, msgs [][]byte, partia
 	if err != nil {
 		return nil, err
 	}
-	p := make([]byte, 0, 98*R*k)
-	for r := range msgs {
-		if len(partials[r]) != k {
-			return nil, errors.New("gpu: rounds with different partial counts")
-		}
-		for _, x := range partials[r] {
-			if len(x) != 98 {
-				return nil, errors.New("gpu: partial of the wrong length (verify it on the CPU)")
-			}
-			p = append(p, x...)
-		}
+	// a partial of the wrong length is an error of its own (kyber's VerifyPartial fails to parse it), not of the
+	// batch: its error comes from the CPU scheme and a never-valid placeholder record takes its slot
+	p, short, err := packPartials(partials, k)
+	if err != nil {
+		return nil, err
 	}
 	c, err := commits(public)
 	if err != nil {
@@ -231,12 +225,42 @@ func (s *Scheme) VerifyPartialBatch(public *share.PubPoly, msgs [][]byte, partia
 	for r := range out {
 		out[r] = make([]error, k)
 		for j := 0; j < k; j++ {
-			if v := st[r*k+j]; v != C.DG_ST_OK {
+			if short[r*k+j] {
+				out[r][j] = s.cpu.VerifyPartial(public, msgs[r], partials[r][j])
+				if out[r][j] == nil { // cannot happen for a wrong-length share; never report it valid
+					out[r][j] = errors.New("gpu: partial of the wrong length")
+				}
+			} else if v := st[r*k+j]; v != C.DG_ST_OK {
 				out[r][j] = fmt.Errorf("gpu: invalid partial signature (status %d)", v)
 			}
 		}
 	}
 	return out, nil
+}
+
+// placeholder98 stands in for a partial of the wrong length: index 0 and a sigma whose first byte lacks the
+// compression flag, which the library reports as a decode error (DG_ST_SIG_DECODE) -- never valid, so Recover
+// skips it as kyber's tbls.Recover skips a partial that fails VerifyPartial.
+var placeholder98 = make([]byte, 98)
+
+// packPartials lays out R rounds of k partials as 98 B records; short[i] marks a partial of the wrong length,
+// replaced by placeholder98.
+func packPartials(partials [][][]byte, k int) ([]byte, []bool, error) {
+	p := make([]byte, 0, 98*len(partials)*k)
+	short := make([]bool, len(partials)*k)
+	for r := range partials {
+		if len(partials[r]) != k {
+			return nil, nil, errors.New("gpu: rounds with different partial counts")
+		}
+		for j, x := range partials[r] {
+			if len(x) != 98 {
+				short[r*k+j] = true
+				x = placeholder98
+			}
+			p = append(p, x...)
+		}
+	}
+	return p, short, nil
 }
 
 // RecoverBatch: tbls.Recover per round (first t valid partials in input order, deduplicated by index,
@@ -251,17 +275,10 @@ func (s *Scheme) RecoverBatch(public *share.PubPoly, msgs [][]byte, partials [][
 	if err != nil {
 		return nil, nil, err
 	}
-	p := make([]byte, 0, 98*R*k)
-	for r := range msgs {
-		if len(partials[r]) != k {
-			return nil, nil, errors.New("gpu: rounds with different partial counts")
-		}
-		for _, x := range partials[r] {
-			if len(x) != 98 {
-				return nil, nil, errors.New("gpu: partial of the wrong length (recover it on the CPU)")
-			}
-			p = append(p, x...)
-		}
+	// a wrong-length partial is skipped, as tbls.Recover skips a partial that fails VerifyPartial
+	p, _, err := packPartials(partials, k)
+	if err != nil {
+		return nil, nil, err
 	}
 	c, err := commits(public)
 	if err != nil {

@@ -144,6 +144,17 @@ int dg_recover_dev(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_
                    size_t msg_len, uint32_t k, const uint8_t* d_partials98, uint8_t* d_out_sig96,
                    uint8_t* d_round_status, uint8_t* d_share_status, uint64_t seed);
 
+/* dg_verify_partials with messages, partials and statuses in device memory (commits48 stays a host buffer):
+ * VerifyPartial of every incoming partial as ProcessBeacon does (beacon/beacon.go:148), HBM-resident.  Completes
+ * before return. */
+int dg_verify_partials_dev(const uint8_t* commits48, uint32_t t, size_t rounds, const uint8_t* d_msgs, size_t msg_len,
+                           uint32_t k, const uint8_t* d_partials98, uint8_t* d_status, uint64_t seed);
+/* dg_recover_verified with partials, verdicts and outputs in device memory: the Lagrange half of the live round
+ * (beacon/beacon.go:488) after dg_verify_partials_dev.  Completes before return. */
+int dg_recover_verified_dev(uint32_t t, uint32_t nshares, size_t rounds, uint32_t k, const uint8_t* d_partials98,
+                            const uint8_t* d_verified_status, uint8_t* d_out_sig96, uint8_t* d_round_status,
+                            uint8_t* d_share_status);
+
 /* Asynchronous device-resident VerifyBeacon batch (the streaming form of syncFrom's catch-up,
  * beacon/beacon.go:529-607): enqueues the batch on the next of the library's rotating workspace sets and
  * returns without waiting, so consecutive batches overlap (one batch's Miller loops and final

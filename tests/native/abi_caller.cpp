@@ -44,6 +44,10 @@ EXPECT_TYPE(dg_group_counts, int (*)(uint64_t*));
 EXPECT_TYPE(dg_set_group_size, int (*)(uint32_t));
 EXPECT_TYPE(dg_recover_dev, int (*)(const uint8_t*, uint32_t, uint32_t, size_t, const uint8_t*, size_t, uint32_t,
                                     const uint8_t*, uint8_t*, uint8_t*, uint8_t*, uint64_t));
+EXPECT_TYPE(dg_verify_partials_dev, int (*)(const uint8_t*, uint32_t, size_t, const uint8_t*, size_t, uint32_t,
+                                            const uint8_t*, uint8_t*, uint64_t));
+EXPECT_TYPE(dg_recover_verified_dev, int (*)(uint32_t, uint32_t, size_t, uint32_t, const uint8_t*, const uint8_t*,
+                                             uint8_t*, uint8_t*, uint8_t*));
 EXPECT_TYPE(dg_wait_all, int (*)(void));
 EXPECT_TYPE(dg_set_timing, int (*)(int));
 EXPECT_TYPE(dg_last_timings, int (*)(const char**, double*, int*, int));
@@ -80,6 +84,8 @@ int main() {
   expect("dg_recover", dg_recover(pk, 1, 1, 1, msg, 32, 1, part, out, st, st + 1, 1), DG_E_NODEV);
   expect("dg_recover_dev", dg_recover_dev(pk, 1, 1, 1, msg, 32, 1, part, out, st, st + 1, 1), DG_E_NODEV);
   expect("dg_recover_verified", dg_recover_verified(1, 1, 1, 1, part, st, out, st, st + 1), DG_E_NODEV);
+  expect("dg_verify_partials_dev", dg_verify_partials_dev(pk, 1, 1, msg, 32, 1, part, st, 1), DG_E_NODEV);
+  expect("dg_recover_verified_dev", dg_recover_verified_dev(1, 1, 1, 1, part, st, out, st, st + 1), DG_E_NODEV);
   expect("dg_verify_beacons_dev", dg_verify_beacons_dev(pk, 1, pr, rr, msg, off, sig, st, 1, nullptr), DG_E_NODEV);
   expect("dg_verify_beacons_dev_async",
          dg_verify_beacons_dev_async(pk, 1, pr, rr, msg, off, sig, st, 1, nullptr, nullptr), DG_E_NODEV);

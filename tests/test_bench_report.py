@@ -52,11 +52,29 @@ def _worker(rank, world, port, peaks, tables_out, q):
             rec["cpu_baseline"] = bench.cpu_label({"value": 30.0, "unit": "recovers/s", "sample": "stub"}, th,
                                                   machine, quota)
         head = {"value": 1e6 * 30 / dt, "n_gpus": world, "steps": 30, "warmup": 1, "ms_per_step": dt / 30 * 1e3,
-                "scaling": "strong", "data": "stub", "config": {"workload": "stub", "global_rounds": 1000000},
+                "scaling": "strong", "data": "synthetic linked chain data/chain_v1 (CPU-twin generated, seed tools/synthetic.py)",
+                "config": {"workload": "w" * 230, "global_rounds": 1000000, "rounds_per_gpu": 100000,
+                           "batches_per_gpu": 1, "hip_hw_queues": 16, "parallelism": "rounds sharded dp1"},
                 "batch_fallbacks": 0}
         tables = {"kernel_avg_us": {k: v[0] for k, v in KT.items()}, "peak": peak}
-        line = bench.report(rank, world, head, roof, cpu, {"recover": rec, "adversarial": adv, "c1": None,
-                                                           "live_latency": None, "sync": None}, tables, tables_out)
+        c2 = {"metric": "BASELINE configs[2]: VerifyPartial on all 64 shares of every round + Lagrange Recover " * 2,
+              "value": 150000.0, "unit": "recovers/s", "value_recover_from_verdicts": 200000.0,
+              "partials_verified_per_s": 1.3e7, "verify_partials_s": 0.5, "recover_s": 0.13,
+              "recover_from_verdicts_s": 0.02, "note": "y" * 400,
+              "roofline": bench.roofline_of(KT_REC, {"k_rc_straus": 50000}, peak, None, "c3vp")}
+        c1 = {"metric": "C1: n=5 t=3, 5 Signs + Recover + VerifyRecovered per round (BASELINE configs[0])",
+              "value": 13500.0, "unit": "rounds/s", "rounds": 1000, "s_per_step": 0.074, "note": "z" * 100}
+        lat = {"recover_verified_ms": 11.783, "recover_full_ms": 27.938, "verify_recovered_ms": 10.879,
+               "metric": "live-round latency, one round at n=64 t=33 (ms per call)"}
+        syn = {"metric": "syncFrom catch-up rounds/s (bulk.sync_from, beacon/beacon.go:529-607)", "value": 523540.0,
+               "unit": "rounds/s", "rounds": 100000, "batch": 25000, "s": 0.19101}
+        if rank == 0:
+            for x, v in ((c2, 40.0), (c1, 600.0)):
+                x["cpu_baseline"] = bench.cpu_label({"value": v, "unit": "x/s", "kind": "port", "sample": "stub"}, th,
+                                                    machine, quota)
+        line = bench.report(rank, world, head, roof, cpu, {"recover": rec, "adversarial": adv, "c1": c1,
+                                                           "live_latency": lat, "sync": syn, "c2_verify_all": c2},
+                            tables, tables_out)
         q.put((rank, "ok", line))
     except Exception as e:  # noqa: BLE001 -- report any failure of any rank to the test
         q.put((rank, "error: %r" % (e,), None))
@@ -85,6 +103,7 @@ def test_bench_report_world2(tmp_path, peak1):
     assert res[0][0] == "ok" and res[1][0] == "ok", res
     assert res[1][1] is None  # only rank 0 prints
     line = res[0][1]
+    print("line bytes", len(line))
     assert len(line) < 4096, len(line)
     d = json.loads(line)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
@@ -93,6 +112,7 @@ def test_bench_report_world2(tmp_path, peak1):
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["roofline"]["frac"] > 0 and d["roofline"]["chip"]["frac"] > 0
     assert d["recover"]["value"] == 300000.0 and d["recover"]["roofline"]["frac"] > 0
+    assert d["c2_verify_all"]["value"] == 150000.0 and d["c2_verify_all"]["cpu_baseline"]["value"] == 40.0
     assert "kernel_avg_us" not in d["recover"] and "note" not in d["recover"]
     assert d["cpu_baseline"]["cores"] >= 1 and d["recover"]["cpu_baseline"]["value"] == 30.0
     side = json.load(open(out))

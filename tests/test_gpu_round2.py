@@ -213,11 +213,13 @@ def test_batch_coefficients_depend_on_contents():
 
 
 def _chain_file(n):
-    p = os.path.join(ROOT, "data", "chain_v1_%d.bin" % n)
-    return p if os.path.exists(p) else None
+    """The digest-pinned chain file of n rounds (tools/synthetic.find_chain); a missing or altered file fails the
+    test instead of skipping it: configs[3] is measured on this file."""
+    got, p = S.find_chain(n)
+    assert got == n
+    return p
 
 
-@pytest.mark.skipif(_chain_file(1000000) is None, reason="data/chain_v1_1000000.bin not generated")
 def test_sharded_1m_chain_equals_one_batch():
     """BASELINE configs[3] on one GPU: the 1M-round linked chain with 1% of the signatures replaced at
     deterministic positions (a valid signature of another round), verified as one batch and as 8

@@ -49,12 +49,10 @@ def main(dst):
             for k in kernels_of(os.path.join(ROOT, "drand_amd", "csrc", tu), tmp):
                 rows.append([tu.replace(".o", ""), k[".name"]] + [k.get(f, "") for f in FIELDS])
     rows.sort(key=lambda r: (-int(r[7] or 0), r[1]))
-    with open(dst, "w", newline="") as f:
-        w = csv.writer(f)
-        w.writerow(["tu", "kernel"] + [f.lstrip(".") for f in FIELDS])
-        w.writerows(rows)
-    print(open(dst).read())
+    w = csv.writer(open(dst, "w", newline="") if dst else sys.stdout)
+    w.writerow(["tu", "kernel"] + [f.lstrip(".") for f in FIELDS])
+    w.writerows(rows)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r2_kernel_resources.csv"))
+    main(sys.argv[1] if len(sys.argv) > 1 else None)  # no argument: print only

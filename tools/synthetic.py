@@ -45,6 +45,45 @@ def chain_path(n):
     return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "chain_v1_%d.bin" % n)
 
 
+# SHA-256 of the chain files tools/gen_chain.py wrote with the CPU twin (data/ is git-ignored; the files travel to
+# the GPU box with the tree).  A chain file is trusted only if it matches: the GPU library under test must never
+# have produced the rounds it verifies.
+CHAIN_SHA256 = {
+    100000: "bd4426dc5132c730295720ec0ba6ecc5ef44d5c500e2c4c581d550cd49a3e9f0",
+    1000000: "5b33b619c02f415f794497b4cc84abcc1144e73d6bb4a35787366fa126d627a4",
+}
+
+
+class ChainFileError(RuntimeError):
+    pass
+
+
+def chain_file_sha256(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 22), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def find_chain(total, data_dir=None):
+    """(n, path) of the smallest digest-pinned chain file data/chain_v1_<n>.bin with n >= total.  Raises
+    ChainFileError when none covers `total` or when the covering file does not match its pinned SHA-256."""
+    import os
+
+    d = data_dir or os.path.dirname(chain_path(1))
+    have = sorted(n for n in CHAIN_SHA256 if n >= total and os.path.exists(os.path.join(d, "chain_v1_%d.bin" % n)))
+    if not have:
+        raise ChainFileError("no chain file covers %d rounds in %s (pinned sizes: %s; tools/gen_chain.py makes them)"
+                             % (total, d, sorted(CHAIN_SHA256)))
+    n = have[0]
+    p = os.path.join(d, "chain_v1_%d.bin" % n)
+    got = chain_file_sha256(p)
+    if got != CHAIN_SHA256[n]:
+        raise ChainFileError("%s: SHA-256 %s does not match the pinned %s" % (p, got, CHAIN_SHA256[n]))
+    return n, p
+
+
 # x * g1 for x = master_secret(): the group key C_0 of every synthetic group (= chain_t3n5.json "pk";
 # pinned by tests/test_oracle.py::test_group_pk_constant)
 GROUP_PK = bytes.fromhex("a48a078a2548dcc710aa9925a1c0cf951be802bdce52febb5f1b75af1a01c22760724cd295bdc4fe7e5ab0f6cead0564")
