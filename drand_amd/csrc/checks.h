@@ -1,0 +1,360 @@
+// Recover's per-item pass (kernels.h verify_group: e(sum rho_i X_i, H_r) == e(g1, sum rho_i S_i))
+// as a pipeline of short kernels with HBM-resident state between them, in place of one lane running a whole pairing
+// check (k_verify_groups: 512 VGPRs and ~15 KB of scratch per lane, the stack frames of its out-of-line Fp12 calls;
+// ~110 GB of scratch traffic per launch).  The kernels are compiled in translation units of their own
+// (kernels_check*.hip: DG_FP_CALL=3, DG_INLINE12=1) with every field product inlined and serialised, so each kernel's
+// live set is its own few field elements -- no calls, no scratch -- and every loop body holds one call site of each
+// formula (loops are not unrolled), so each kernel stays a few tens of thousands of instructions.
+//
+// The reference's re-verification of t shares against one message (beacon/beacon.go:488) pairs every check of a
+// round against the same H_r = h_eff(Q_r): its Miller-loop line coefficients are computed ONCE per round
+// (k_ck_round_lines: 68 lines of 3 Fp2, without the G1 point) and every check only evaluates them at its own
+// a = sum rho_i X_i (two Fp2 x Fp products per line) -- `north_star`'s precomputed line coefficients.
+//
+//   per round (once per Recover call):  k_ck_round_lines  H_r = h_eff(Q_r) and its 68 lines RL[s][r]
+//   per pass and chunk of checks (G lanes, drand_gpu.hip check_chunk):
+//     k_ck_prep      the group's members: subgroup checks, a = sum rho X, b = sum rho S (kernels.h group_combine)
+//     k_ck_lines2    the 68 lines of the pair (-g1, b) -> L2[s][g] (b's G2 state lives only here)
+//     k_ck_miller    f = the product of both pairs' lines at a and at -g1 (the Fp12 accumulator and one line)
+//     k_ck_fe1       the pieces of f^-1 down to one Fp norm per check  -> batch inversion (phases.h k_binv_*)
+//     k_ck_inv       f^-1;  k_ck_mul: f1 = f^-1 conj(f), f2 = f1 frob^2(f1)
+//     5 x [k_ck_expsq   63 compressed cyclotomic squarings (Karabina): the 6 powers, their denominators' norms
+//                       -> batch inversion of 6 G norms (Montgomery's trick across the chunk)
+//          k_ck_expdec  decompression and the product x^z  (k_ck_explain: the uncompressed chain where a
+//                       denominator is zero)
+//          k_ck_mul     the hard part's next factor]
+//     k_ck_verdict   == 1, the members' verdicts exactly as verify_group writes them.
+// Every value equals the one pair_check computes (pairing.h miller_loop, final_exp_cubed, cyc_exp_z): the same
+// formulas in the same order, only split across kernels (tests/test_host_arith.py runs the pipeline's pieces on the
+// host against pair_check).
+#pragma once
+
+namespace dg {
+
+constexpr uint32_t CK_STEPS = 68;      // Miller steps over |z| = 0xd201000000010000: 63 doublings + 5 additions
+constexpr uint32_t CK_CHUNK = 131072;  // checks per pipeline launch (~3.7 GB of workspace)
+constexpr int CK_NPOW = 6;             // set bits of |z|: the powers a^(2^k) of the compressed chain
+constexpr uint32_t CK_GRP = 4;         // members per check at most (kernels.h GRP)
+
+// one Miller-loop line without its G1 point: l = c0 + (c1 P.x) v + (c4 P.y) v w (pairing.h line_dbl / line_add)
+struct CkLine {
+  Fp2 c0, c1, c4;
+};
+// one check: up to GRP shares of one round (or one share alone)
+struct CkState {
+  G1AStore a;          // sum rho_i X_i (a single share: its key)
+  G2AStore b;          // sum rho_i S_i (a single share: its sigma)
+  uint32_t round, np;  // np bit 0: pair (a, H_r) present; bit 1: pair (-g1, b) present (pair_check drops identities)
+  uint32_t n, nl;      // members listed, members live (not rejected by the subgroup check)
+  uint32_t live[CK_GRP];  // the live members' item indices
+};
+
+// pairing.h line_dbl / line_add with c1, c4 left unscaled by P
+DGI void ck_line_dbl(G2Proj& T, CkLine& l) {
+  const Fp2 a = fp2_mul_fp(fp2_mul(T.x, T.y), fp_const(FP_TWO_INV));
+  const Fp2 b = fp2_sqr(T.y);
+  const Fp2 c = fp2_sqr(T.z);
+  const Fp2 e = fp2_mul(fp2_const(FP2_B3_G2), c);
+  const Fp2 f = fp2_add(fp2_dbl(e), e);
+  const Fp2 g = fp2_mul_fp(fp2_add(b, f), fp_const(FP_TWO_INV));
+  const Fp2 h = fp2_sub(fp2_sub(fp2_sqr(fp2_add(T.y, T.z)), b), c);
+  const Fp2 j = fp2_sqr(T.x);
+  l.c0 = fp2_sub(e, b);
+  l.c1 = fp2_add(fp2_dbl(j), j);
+  l.c4 = fp2_neg(h);
+  const Fp2 e2 = fp2_sqr(e);
+  T.x = fp2_mul(a, fp2_sub(b, f));
+  T.y = fp2_sub(fp2_sqr(g), fp2_add(fp2_dbl(e2), e2));
+  T.z = fp2_mul(b, h);
+}
+DGI void ck_line_add(G2Proj& T, const Fp2& qx, const Fp2& qy, CkLine& l) {
+  const Fp2 theta = fp2_sub(T.y, fp2_mul(qy, T.z));
+  const Fp2 lambda = fp2_sub(T.x, fp2_mul(qx, T.z));
+  const Fp2 c = fp2_sqr(theta);
+  const Fp2 d = fp2_sqr(lambda);
+  const Fp2 e = fp2_mul(lambda, d);
+  const Fp2 f = fp2_mul(T.z, c);
+  const Fp2 g = fp2_mul(T.x, d);
+  const Fp2 h = fp2_sub(fp2_add(e, f), fp2_dbl(g));
+  const Fp2 ny = fp2_sub(fp2_mul(theta, fp2_sub(g, h)), fp2_mul(e, T.y));
+  T.x = fp2_mul(lambda, h);
+  T.y = ny;
+  T.z = fp2_mul(T.z, e);
+  l.c0 = fp2_sub(fp2_mul(theta, qx), fp2_mul(lambda, qy));
+  l.c1 = fp2_neg(theta);
+  l.c4 = lambda;
+}
+// the kind of Miller step s (0..67): a doubling, or the addition after the doubling of a set bit of |z| (scalar)
+DGI bool ck_step_is_dbl(uint32_t step) {
+  uint32_t s = 0;
+  for (int b = 62; b >= 0; --b) {
+    if (s++ == step) return true;
+    if ((Z_ABS >> b) & 1 && s++ == step) return false;
+  }
+  return true;
+}
+// the 68 lines of Q (affine, not the identity) in step order: out(s, line)
+template <class Out>
+DGI void ck_lines(const Fp2& qx, const Fp2& qy, Out out) {
+  G2Proj T{qx, qy, fp2_one()};
+#pragma unroll 1
+  for (uint32_t s = 0; s < CK_STEPS; ++s) {
+    CkLine l;
+    if (ck_step_is_dbl(s))
+      ck_line_dbl(T, l);
+    else
+      ck_line_add(T, qx, qy, l);
+    out(s, l);
+  }
+}
+// the Miller value of both pairs from their lines (line(s, pair): pair 0 = (a, H_r) at (ax, ay), pair 1 = (-g1, b)),
+// conjugated (z < 0): miller_loop<2> of pairing.h step for step -- per step the squaring (not before the first),
+// then pair 0's line, then pair 1's
+template <class Line>
+DGI Fp12 ck_miller(uint32_t np, const Fp& ax, const Fp& ay, Line line) {
+  Fp12 f = fp12_one();
+  if (!np) return f;
+  const Fp gx = fp_const(G1_GEN_X), gy = fp_const(G1_GEN_NEG_Y);
+#pragma unroll 1
+  for (uint32_t it = 0; it < 2 * CK_STEPS; ++it) {
+    const uint32_t s = it >> 1, pair = it & 1;
+    if (pair == 0 && s != 0 && ck_step_is_dbl(s)) f = fp12_sqr(f);
+    if ((np >> pair) & 1) {
+      const CkLine l = line(s, pair);
+      const Fp px = fp_sel(pair != 0, ax, gx), py = fp_sel(pair != 0, ay, gy);  // fp_sel(c, a, b) = c ? b : a
+      f = fp12_mul_014(f, l.c0, fp2_mul_fp(l.c1, px), fp2_mul_fp(l.c4, py));
+    }
+  }
+  return fp12_conj(f);
+}
+
+// ---- final exponentiation in pieces (pairing.h final_exp_cubed)
+// f^-1 = (f0 t6^-1, -f1 t6^-1) with t6 = f0^2 - v f1^2 (field.h fp12_inv); t6^-1 by fp6_inv, whose one inversion
+// (of the Fp2 value t) becomes an inversion of N(t) in Fp, batched across the checks
+struct CkInv {
+  Fp6 c;  // fp6_inv's (c0, c1, c2) of t6
+  Fp2 t;  // fp6_inv's t: t6^-1 = c / t
+};
+DGI Fp ck_fe1(const Fp12& f, CkInv& out) {
+  const Fp6 a = fp6_sub(fp6_mul(f.c0, f.c0), fp6_mul_v(fp6_mul(f.c1, f.c1)));
+  out.c.c0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+  out.c.c1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+  out.c.c2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+  out.t = fp2_add(fp2_mul_xi(fp2_add(fp2_mul(a.c2, out.c.c1), fp2_mul(a.c1, out.c.c2))), fp2_mul(a.c0, out.c.c0));
+  return fp2_norm(out.t);
+}
+// f^-1 given inv_n = 1 / N(t)
+DGI Fp12 ck_inv(const Fp12& f, const CkInv& in, const Fp& inv_n) {
+  const Fp2 ti{fp_mul(in.t.c0, inv_n), fp_neg(fp_mul(in.t.c1, inv_n))};  // fp2_inv(t)
+  const Fp6 t6i{fp2_mul(in.c.c0, ti), fp2_mul(in.c.c1, ti), fp2_mul(in.c.c2, ti)};
+  return Fp12{fp6_mul(f.c0, t6i), fp6_neg(fp6_mul(f.c1, t6i))};
+}
+// a * op(b), op = frob^nfrob then conj if `conj` (the products of final_exp_cubed)
+DGI Fp12 ck_mul_op(const Fp12& a, Fp12 b, uint32_t nfrob, uint32_t conj) {
+#pragma unroll 1
+  for (uint32_t i = 0; i < nfrob; ++i) b = fp12_frob(b);
+  if (conj) b = fp12_conj(b);
+  return fp12_mul(a, b);
+}
+// the compressed chain of x^|z| (pairing.h cyc_exp_z): the six powers x^(2^k), k the set bits of |z|, and the norms
+// of their denominators 4 g2; returns whether a denominator is zero (then the check takes the uncompressed chain)
+template <class Put>
+DGI bool ck_expsq(const Fp12& x, Put put) {
+  CycC c{x.c1.c0, x.c0.c2, x.c0.c1, x.c1.c2};
+  bool zero = false;
+  int n = 0;
+#pragma unroll 1
+  for (int k = 1; k <= 63; ++k) {
+    c = cyc_sqr_c(c);
+    if ((Z_ABS >> k) & 1) {
+      const Fp2 d = fp2_dbl(fp2_dbl(c.g2));
+      zero |= fp2_is_zero(d);
+      put(n++, c, fp2_norm(d));
+    }
+  }
+  return zero;
+}
+// x^z from the six compressed powers and the inverses of their denominators' norms (get(i, c, nv))
+template <class Get>
+DGI Fp12 ck_expdec(Get get) {
+  Fp12 acc = fp12_one();
+#pragma unroll 1
+  for (int i = CK_NPOW - 1; i >= 0; --i) {
+    CycC c;
+    Fp nv;
+    get(i, c, nv);
+    const Fp2 d = fp2_dbl(fp2_dbl(c.g2));
+    const Fp2 inv{fp_mul(d.c0, nv), fp_neg(fp_mul(d.c1, nv))};  // 1 / d = conj(d) / N(d)
+    acc = fp12_mul(acc, cyc_decompress(c, inv));
+  }
+  return fp12_conj(acc);
+}
+// x^z by the uncompressed chain (pairing.h cyc_exp_z's fallback)
+DGI Fp12 ck_exp_plain(const Fp12& a) {
+  Fp12 acc = a;
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    acc = fp12_cyc_sqr(acc);
+    if ((Z_ABS >> b) & 1) acc = fp12_mul(acc, a);
+  }
+  return fp12_conj(acc);
+}
+
+#if defined(__HIP__)
+static_assert(CK_GRP == GRP, "one group per check");
+// H_r = h_eff(Q_r) and its 68 lines (once per Recover call and round): rl[s * R + r]; hinf[r]: H_r is the identity
+// (kernels_check_a.hip)
+#if DG_TU_CHECK == 1
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_round_lines(uint32_t R, const G2JStore* Q, CkLine* rl, uint8_t* hinf) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const G2A h = g2_to_aff(g2_clear_cofactor(load_g2j(Q[r])));
+  hinf[r] = h.inf ? 1 : 0;
+  if (h.inf) return;
+  ck_lines(h.x, h.y, [&](uint32_t s, const CkLine& l) { rl[(size_t)s * R + r] = l; });
+}
+// the check's members (glist group off + g), as verify_group: subgroup checks, the weighted sums (group_combine)
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
+                                                  const uint64_t* seedp, const G1AStore* keys, const uint32_t* item_slot,
+                                                  const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
+                                                  uint32_t subgroup, unsigned long long* cnt, CkState* st) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const uint32_t* mem = glist + 4 + 4 * (size_t)(off + g);
+  uint32_t n = 0;
+  while (n < GRP && mem[n] != ~0u) ++n;
+  atomicAdd(&cnt[n - 1], 1ull);
+  G1A a{fp_zero(), fp_zero(), true};
+  G2A b{fp2_zero(), fp2_zero(), true};
+  CkState c;
+  const uint32_t nl = group_combine(mem, n, *seedp, keys, item_slot, S, status, fin, subgroup, a, b, c.live);
+  c.round = mem[0] / k;
+  c.n = n;
+  c.nl = nl;
+  if (nl == 0) {
+    a = G1A{fp_zero(), fp_zero(), true};
+    b = G2A{fp2_zero(), fp2_zero(), true};
+  }
+  c.np = ((!a.inf && !hinf[c.round]) ? 1u : 0u) | (!b.inf ? 2u : 0u);
+  store_g1a(c.a, a);
+  store_g2a(c.b, b);
+  st[g] = c;
+}
+// the lines of the pair (-g1, b): l2[s * G + g]
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G || !(st[g].np & 2)) return;
+  const G2A b = load_g2a(st[g].b);
+  ck_lines(b.x, b.y, [&](uint32_t s, const CkLine& l) { l2[(size_t)s * G + g] = l; });
+}
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  CkInv c;
+  nv[g] = ck_fe1(F[g], c);
+  inv[g] = c;
+}
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_inv(uint32_t G, const Fp12* F, const CkInv* inv, const Fp* nvinv,
+                                                 Fp12* out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  out[g] = ck_inv(F[g], inv[g], nvinv[g]);
+}
+// the six compressed powers sn[i * G + g], their denominators' norms nv[i * G + g], zero[g]
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  zero[g] = ck_expsq(X[g], [&](int i, const CycC& c, const Fp& n) {
+              sn[(size_t)i * G + g] = c;
+              nv[(size_t)i * G + g] = n;
+            }) ? 1 : 0;
+}
+// the verdicts of the checks whose final exponentiation is res[g] (== 1: valid), written as verify_group writes them
+DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const Fp12* res, uint8_t* status,
+                                                   uint8_t* fin) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const CkState& c = st[g];
+  if (c.nl == 0) return;
+  const bool good = c.np == 0 || fp12_is_one(res[g]);
+  if (c.n == 1) {
+    status[c.live[0]] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
+    fin[c.live[0]] = FIN_DONE;
+    return;
+  }
+  for (uint32_t m = 0; m < c.nl; ++m) {
+    if (good) status[c.live[m]] = DG_ST_OK_;
+    fin[c.live[m]] = good ? FIN_DONE : FIN_RECHECK;
+  }
+}
+#else
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_round_lines(uint32_t R, const G2JStore* Q, CkLine* rl, uint8_t* hinf);
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
+                                                  const uint64_t* seedp, const G1AStore* keys, const uint32_t* item_slot,
+                                                  const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
+                                                  uint32_t subgroup, unsigned long long* cnt, CkState* st);
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2);
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv);
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_inv(uint32_t G, const Fp12* F, const CkInv* inv, const Fp* nvinv,
+                                                 Fp12* out);
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero);
+DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const Fp12* res, uint8_t* status,
+                                                   uint8_t* fin);
+#endif
+// the Miller value of every check (kernels_check_b.hip)
+#if DG_TU_CHECK == 2
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_miller(uint32_t G, uint32_t R, const CkState* st, const CkLine* rl,
+                                                    const CkLine* l2, Fp12* F) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const uint32_t np = st[g].np, r = st[g].round;
+  const Fp ax = st[g].a.x, ay = st[g].a.y;
+  F[g] = ck_miller(np, ax, ay, [&](uint32_t s, uint32_t pair) {
+    return pair ? l2[(size_t)s * G + g] : rl[(size_t)s * R + r];
+  });
+}
+#else
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_miller(uint32_t G, uint32_t R, const CkState* st, const CkLine* rl,
+                                                    const CkLine* l2, Fp12* F);
+#endif
+// out = a * frob^nfrob(b), conjugated if `conj` (kernels_check_c.hip)
+#if DG_TU_CHECK == 3
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_mul(uint32_t G, const Fp12* A, const Fp12* B, uint32_t nfrob, uint32_t conj,
+                                                 Fp12* out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  out[g] = ck_mul_op(A[g], B[g], nfrob, conj);
+}
+#else
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_mul(uint32_t G, const Fp12* A, const Fp12* B, uint32_t nfrob, uint32_t conj,
+                                                 Fp12* out);
+#endif
+// x^z from the compressed powers (kernels_check_d.hip); lanes whose chain hit a zero denominator are left to
+// k_ck_explain
+#if DG_TU_CHECK == 4
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_expdec(uint32_t G, const CycC* sn, const Fp* nvinv, const uint8_t* zero,
+                                                    Fp12* XZ) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G || zero[g]) return;
+  XZ[g] = ck_expdec([&](int i, CycC& c, Fp& n) {
+    c = sn[(size_t)i * G + g];
+    n = nvinv[(size_t)i * G + g];
+  });
+}
+#else
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_expdec(uint32_t G, const CycC* sn, const Fp* nvinv, const uint8_t* zero,
+                                                    Fp12* XZ);
+#endif
+// x^z by the uncompressed chain for the lanes with a zero Karabina denominator (kernels_check_e.hip)
+#if DG_TU_CHECK == 5
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_explain(uint32_t G, const uint8_t* zero, const Fp12* X, Fp12* XZ) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G || !zero[g]) return;
+  XZ[g] = ck_exp_plain(X[g]);
+}
+#else
+DG_KERNEL void __launch_bounds__(64, 1) k_ck_explain(uint32_t G, const uint8_t* zero, const Fp12* X, Fp12* XZ);
+#endif
+#endif
+
+}  // namespace dg

@@ -142,7 +142,9 @@ enum Slot {
   S_KMSM_TMP, S_KMSM_W, S_KMSM_T, S_KMSM_BT, S_DIG0, S_DIG1, S_SEED, S_VST, S_XMD, S_H2CST, S_EIN, S_EOUT, S_ISOPT, S_DECST, S_DEIN, S_DEOUT, S_BINV, S_NV, S_NVINV,
   S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_BINV_PRE, S_BINV_ROOTS, S_RC_UNI, S_RC_REF, S_RC_LIST, S_RS_DIG,
   S_RC_NAF, S_RC_EV, S_RC_TAB, S_RC_D, S_RC_PINF, S_RC_DEN, S_RC_A, S_PW, S_SLOTW, S_SFULL, S_STFULL, S_INC, S_PB, S_SLOTB,
-  S_SEED2, S_SB, S_STB, S_ISOB, S_KMSM_GOFS, S_KMSM_BP, S_KMSM_BT2, S_COUNT
+  S_SEED2, S_SB, S_STB, S_ISOB, S_KMSM_GOFS, S_KMSM_BP, S_KMSM_BT2,
+  S_CK_RL, S_CK_HINF, S_CK_ST, S_CK_L2, S_CK_F, S_CK_T0, S_CK_T1, S_CK_T2, S_CK_F2, S_CK_A, S_CK_XZA, S_CK_XZB,
+  S_CK_INV, S_CK_NV, S_CK_NVI, S_CK_SN, S_CK_ZERO, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -942,6 +944,89 @@ int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const 
 // statuses Recover reads are exact.  Up to GRP fresh items of a round are checked together (kernels.h
 // verify_group); the members of a failed group, and everything in the last pass, are checked alone.  DG_GROUP=1
 // checks every item alone.  fin: FIN_DONE for the final verdicts, FIN_PENDING for the rest.
+// The pairing-check pipeline of checks.h over the G checks glist[4 + 4 (off + g)] of one pass (G <= CK_CHUNK):
+// members and weighted sums, the (-g1, b) lines, the Miller values against the per-round lines rl, the final
+// exponentiation in pieces (one batch inversion for the easy part, one per x^z for the compressed squarings'
+// denominators), the verdicts.  Every buffer is the current set's workspace, sized for CK_CHUNK checks.
+struct CkBufs {
+  CkState* st;
+  CkLine* l2;
+  Fp12 *F, *T0, *T1, *T2, *F2, *A, *XZa, *XZb;
+  CkInv* inv;
+  Fp *nv, *nvi;
+  CycC* sn;
+  uint8_t* zero;
+};
+int ck_bufs(CkBufs& b) {
+  const size_t G = CK_CHUNK;
+  RET(wsT(S_CK_ST, G, &b.st));
+  RET(wsT(S_CK_L2, (size_t)CK_STEPS * G, &b.l2));
+  RET(wsT(S_CK_F, G, &b.F));
+  RET(wsT(S_CK_T0, G, &b.T0));
+  RET(wsT(S_CK_T1, G, &b.T1));
+  RET(wsT(S_CK_T2, G, &b.T2));
+  RET(wsT(S_CK_F2, G, &b.F2));
+  RET(wsT(S_CK_A, G, &b.A));
+  RET(wsT(S_CK_XZA, G, &b.XZa));
+  RET(wsT(S_CK_XZB, G, &b.XZb));
+  RET(wsT(S_CK_INV, G, &b.inv));
+  RET(wsT(S_CK_NV, CK_NPOW * G, &b.nv));
+  RET(wsT(S_CK_NVI, CK_NPOW * G, &b.nvi));
+  RET(wsT(S_CK_SN, CK_NPOW * G, &b.sn));
+  return wsT(S_CK_ZERO, G, &b.zero);
+}
+// XZ = X^z (pairing.h cyc_exp_z): the compressed chain, one batch inversion of the 6 G denominators' norms, the
+// decompressed product; the uncompressed chain for the lanes with a zero denominator
+int ck_expz(uint32_t G, const Fp12* X, Fp12* XZ, const CkBufs& b, hipStream_t st) {
+  RET(launch("k_ck_expsq", k_ck_expsq, G, 64, st, G, X, b.sn, b.nv, b.zero));
+  RET(batch_inv(CK_NPOW * G, b.nv, b.nvi, st));
+  RET(launch("k_ck_expdec", k_ck_expdec, G, 64, st, G, (const CycC*)b.sn, (const Fp*)b.nvi, (const uint8_t*)b.zero, XZ));
+  return launch("k_ck_explain", k_ck_explain, G, 64, st, G, (const uint8_t*)b.zero, X, XZ);
+}
+// out = a * frob^nfrob(b) (conjugated first if conj)
+int ck_mul(uint32_t G, const Fp12* a, const Fp12* b, uint32_t nfrob, uint32_t conj, Fp12* out, hipStream_t st) {
+  return launch("k_ck_mul", k_ck_mul, G, 64, st, G, a, b, nfrob, conj, out);
+}
+int check_chunk(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k, uint32_t R, const uint64_t* seed,
+                const G1AStore* keys, const uint32_t* item_slot, const uint8_t* hinf, const CkLine* rl, const G2AStore* S,
+                uint8_t* status, uint8_t* fin, uint32_t subgroup, hipStream_t st) {
+  CkBufs b;
+  RET(ck_bufs(b));
+  RET(launch("k_ck_prep", k_ck_prep, G, 64, st, G, off, glist, k, seed, keys, item_slot, hinf, S, status, fin, subgroup,
+             g_ctx.gcount, b.st));
+  RET(launch("k_ck_lines2", k_ck_lines2, G, 64, st, G, (const CkState*)b.st, b.l2));
+  RET(launch("k_ck_miller", k_ck_miller, G, 64, st, G, R, (const CkState*)b.st, rl, (const CkLine*)b.l2, b.F));
+  // easy part: f1 = f^-1 conj(f), f2 = f1 frob^2(f1)
+  RET(launch("k_ck_fe1", k_ck_fe1, G, 64, st, G, (const Fp12*)b.F, b.inv, b.nv));
+  RET(batch_inv(G, b.nv, b.nvi, st));
+  RET(launch("k_ck_inv", k_ck_inv, G, 64, st, G, (const Fp12*)b.F, (const CkInv*)b.inv, (const Fp*)b.nvi, b.T0));
+  RET(ck_mul(G, b.T0, b.F, 0, 1, b.T1, st));
+  RET(ck_mul(G, b.T1, b.T1, 2, 0, b.F2, st));
+  // hard part (final_exp_cubed): t0 = f2^z conj(f2), t1 = t0^z conj(t0), a = t1^z frob(t1),
+  // b = (a^z)^z frob^2(a) conj(a), c = f2^3, result b c
+  RET(ck_expz(G, b.F2, b.XZa, b, st));
+  RET(ck_mul(G, b.XZa, b.F2, 0, 1, b.T0, st));
+  RET(ck_expz(G, b.T0, b.XZa, b, st));
+  RET(ck_mul(G, b.XZa, b.T0, 0, 1, b.T1, st));
+  RET(ck_expz(G, b.T1, b.XZa, b, st));
+  RET(ck_mul(G, b.XZa, b.T1, 1, 0, b.A, st));
+  RET(ck_expz(G, b.A, b.XZa, b, st));
+  RET(ck_expz(G, b.XZa, b.XZb, b, st));
+  RET(ck_mul(G, b.XZb, b.A, 2, 0, b.T0, st));
+  RET(ck_mul(G, b.T0, b.A, 0, 1, b.T1, st));
+  RET(ck_mul(G, b.F2, b.F2, 0, 0, b.T0, st));
+  RET(ck_mul(G, b.T0, b.F2, 0, 0, b.T2, st));
+  RET(ck_mul(G, b.T1, b.T2, 0, 0, b.T0, st));
+  return launch("k_ck_verdict", k_ck_verdict, G, 128, st, G, (const CkState*)b.st, (const Fp12*)b.T0, status, fin);
+}
+
+// DG_CK_OLD=1 (A/B only): Recover's per-item pass as the round-3 single-lane kernel k_verify_groups instead of the
+// pipeline of checks.h
+bool ck_old() {
+  static const bool v = getenv("DG_CK_OLD") != nullptr;
+  return v;
+}
+
 int prefix_pass(uint32_t R, uint32_t k, uint32_t t, const uint64_t* seed, const G1AStore* keys, const uint32_t* item_slot,
                 const G2JStore* Q, const uint32_t* zero2, const G2AStore* S, uint8_t* status, uint8_t* fin,
                 uint32_t subgroup, hipStream_t batch_st) {
@@ -950,6 +1035,33 @@ int prefix_pass(uint32_t R, uint32_t k, uint32_t t, const uint64_t* seed, const 
   HIPCHK(hipEventRecord(set.to_fb, batch_st));
   const hipStream_t st = g_ctx.shared_fb ? batch_st : g_ctx.fb_stream;
   HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
+  if (!ck_old()) {
+    // H_r's lines once per call; per pass the group list, its size to the host, the pipeline over chunks of checks
+    CkLine* rl;
+    uint8_t* hinf;
+    uint32_t* glist;
+    RET(wsT(S_CK_RL, (size_t)CK_STEPS * R, &rl));
+    RET(wsT(S_CK_HINF, R, &hinf));
+    RET(wsT(S_LIST, 4 * (N + 1), &glist));
+    RET(launch("k_ck_round_lines", k_ck_round_lines, R, 64, st, R, Q, rl, hinf));
+    const uint32_t grp = group_size();
+    constexpr int kPasses = 8;
+    for (int pass = 0; pass <= kPasses; ++pass) {
+      HIPCHK(hipMemsetAsync(glist, 0, 4, st));
+      const uint32_t margin = grp < 2 ? 0u : (pass == 0 ? 6u : 2u);
+      RET(launch("k_prefix_groups", k_prefix_groups, R, 128, st, R, k, t, pass == kPasses ? 1u : 0u, grp, margin,
+                 (const uint8_t*)status, (const uint8_t*)fin, glist));
+      uint32_t G = 0;
+      HIPCHK(hipMemcpyAsync(&G, glist, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      for (uint32_t off = 0; off < G; off += CK_CHUNK)
+        RET(check_chunk(std::min(G - off, CK_CHUNK), off, glist, k, R, seed, keys, item_slot, hinf, rl, S, status, fin,
+                        subgroup, st));
+    }
+    HIPCHK(hipEventRecord(set.from_fb, st));
+    HIPCHK(hipStreamWaitEvent(batch_st, set.from_fb, 0));
+    return 0;
+  }
   // H_r = h_eff(Q_r) for every round (zero2: the flag pair {0, 0})
   G2AStore* H;
   RET(wsT(S_H, R, &H));

@@ -223,6 +223,26 @@ __device__ __noinline__ Fp fp_sqr_r(DG_P12(a)) {
 }
 DGI Fp fp_mul(const Fp& a, const Fp& b) { return fp_mul_r(DG_A12(a), DG_A12(b)); }
 DGI Fp fp_sqr(const Fp& a) { return fp_sqr_r(DG_A12(a)); }
+#elif DG_FP_CALL == 3
+// 3 (kernels_check.hip): inlined and serialised -- the operands are pinned in registers before the product and its
+// result after it (empty volatile asms that read and write every limb, kept in program order), so one product's
+// temporaries are live at a time whatever the formula above it; no calls, so no call frames in scratch
+#define DG_PIN_FP12(f)                                                                                                \
+  asm volatile("" : "+v"((f).l[0]), "+v"((f).l[1]), "+v"((f).l[2]), "+v"((f).l[3]), "+v"((f).l[4]), "+v"((f).l[5]), \
+               "+v"((f).l[6]), "+v"((f).l[7]), "+v"((f).l[8]), "+v"((f).l[9]), "+v"((f).l[10]), "+v"((f).l[11]))
+DGI Fp fp_mul(Fp a, Fp b) {
+  DG_PIN_FP12(a);
+  DG_PIN_FP12(b);
+  Fp r = fp28_mul(a, b);
+  DG_PIN_FP12(r);
+  return r;
+}
+DGI Fp fp_sqr(Fp a) {
+  DG_PIN_FP12(a);
+  Fp r = fp28_sqr(a);
+  DG_PIN_FP12(r);
+  return r;
+}
 #else
 DGI Fp fp_mul(const Fp& a, const Fp& b) { return fp28_mul(a, b); }
 DGI Fp fp_sqr(const Fp& a) { return fp28_sqr(a); }

@@ -28,7 +28,10 @@
 #ifndef DG_TU_VERIFY
 #define DG_TU_VERIFY 0  // 1 in kernels_verify.hip: only the per-item pairing kernels are defined there
 #endif
-#define DG_TU_LIB (!DG_TU_HOT && !DG_TU_VERIFY)  // the library translation unit (drand_gpu.hip)
+#ifndef DG_TU_CHECK
+#define DG_TU_CHECK 0  // 1 in kernels_check.hip: only the pairing-check pipeline of checks.h is defined there
+#endif
+#define DG_TU_LIB (!DG_TU_HOT && !DG_TU_VERIFY && !DG_TU_CHECK)  // the library translation unit (drand_gpu.hip)
 
 namespace dg {
 
@@ -491,7 +494,7 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_clear_rounds(uint32_t R, 
 constexpr uint32_t GRP = 4;
 constexpr uint8_t FIN_PENDING = 0, FIN_DONE = 1, FIN_RECHECK = 2;
 constexpr uint64_t GROUP_TAG = 0x67726f7570746573ull;  // domain of rho_i, apart from alpha_r and beta_s
-#if DG_TU_VERIFY
+#if DG_TU_VERIFY || DG_TU_CHECK
 // the Miller loop out of line, so its state and the final exponentiation's do not share one stack frame
 // (the per-item kernels' private segment must stay under the queue's scratch limit: ~14 KB per lane)
 DGN Fp12 miller_loop2(const G1A* P, const G2A* Q, int np) { return miller_loop<2>(P, Q, np); }
@@ -583,6 +586,8 @@ DGN void verify_group(const uint32_t* mem, uint32_t n, uint32_t k, uint64_t seed
     fin[live[m]] = good ? FIN_DONE : FIN_RECHECK;
   }
 }
+#endif
+#if DG_TU_VERIFY
 // every decoded item after a failed batch (flag[0] == 0), only the isolated ones after a passed batch
 DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
                                                     const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
@@ -607,7 +612,7 @@ DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_groups(uint32_t k
   atomicAdd(&cnt[n - 1], 1ull);
   verify_group(mem, n, k, *seedp, keys, item_slot, H, S, status, fin, subgroup);
 }
-#elif DG_TU_LIB
+#elif !DG_TU_CHECK
 // (defined in kernels_verify.hip)
 DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
                                                     const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
@@ -920,3 +925,4 @@ DG_KERNEL void __launch_bounds__(128) k_sign(uint32_t n, const uint8_t* sc32, co
 #include "phases.h"
 #include "msm.h"
 #include "recover.h"
+#include "checks.h"

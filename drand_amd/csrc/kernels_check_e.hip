@@ -1,0 +1,8 @@
+// Part 5 of Recover's pairing-check pipeline (checks.h), compiled in its own translation unit with every field
+// product inlined and serialised (DG_FP_CALL=3) and the Fp12 routines inlined (DG_INLINE12=1): each kernel of the
+// pipeline is short, so its formula fits the register file without calls or scratch.  The parts build in parallel.
+#define DG_TU_CHECK 5
+#define DG_FP_CALL 3
+#define DG_INLINE12 1
+#define DG_CYC_SQR 1
+#include "kernels.h"

@@ -438,3 +438,47 @@ extern "C" int hc_cyc_exp_check(uint64_t seed, uint32_t n) {
   }
   return bad;
 }
+
+// Recover's pairing-check pipeline (checks.h) step for step on the host against pair_check's formula
+// (final_exp_cubed(miller_loop<2>)): the per-round lines of Q1 (unevaluated, ck_lines) evaluated at P1, the lines of
+// Q2 at -g1, the easy part through ck_fe1 / ck_inv with the Fp inversion of the batch, the hard part through the
+// compressed chains (ck_expsq / ck_expdec, or ck_exp_plain where a denominator is zero) and ck_mul_op.  `np` drops
+// pairs as pair_check does (bit 0: (P1, Q1), bit 1: (-g1, Q2)).  Returns 1 when both Fp12 values are equal.
+static Fp12 hc_ck_expz(const Fp12& x) {
+  CycC sn[CK_NPOW];
+  Fp nv[CK_NPOW];
+  const bool zero = ck_expsq(x, [&](int i, const CycC& c, const Fp& n) { sn[i] = c; nv[i] = n; });
+  if (zero) return ck_exp_plain(x);
+  return ck_expdec([&](int i, CycC& c, Fp& n) { c = sn[i]; n = fp_inv(nv[i]); });
+}
+extern "C" int hc_ck_pipeline_check(const uint8_t* pk48, const uint8_t* q1_96, const uint8_t* q2_96, int np) {
+  G1A p1;
+  G2A q1, q2;
+  if (!g1_decompress(p1, pk48, true) || !g2_decompress(q1, q1_96, false) || !g2_decompress(q2, q2_96, false)) return -1;
+  G1A P[2];
+  G2A Q[2];
+  int n = 0;
+  if (np & 1) { P[n] = p1; Q[n] = q1; ++n; }
+  if (np & 2) { P[n] = G1A{fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), false}; Q[n] = q2; ++n; }
+  const Fp12 ref = n ? final_exp_cubed(miller_loop<2>(P, Q, n)) : fp12_one();
+  std::vector<CkLine> l1(CK_STEPS), l2(CK_STEPS);
+  ck_lines(q1.x, q1.y, [&](uint32_t s, const CkLine& l) { l1[s] = l; });
+  ck_lines(q2.x, q2.y, [&](uint32_t s, const CkLine& l) { l2[s] = l; });
+  const Fp12 f = ck_miller((uint32_t)np, p1.x, p1.y, [&](uint32_t s, uint32_t pair) { return pair ? l2[s] : l1[s]; });
+  CkInv inv;
+  const Fp nt = ck_fe1(f, inv);
+  const Fp12 finv = ck_inv(f, inv, fp_inv(nt));
+  const Fp12 f1 = ck_mul_op(finv, f, 0, 1);
+  const Fp12 f2 = ck_mul_op(f1, f1, 2, 0);
+  const Fp12 t0 = ck_mul_op(hc_ck_expz(f2), f2, 0, 1);
+  const Fp12 t1 = ck_mul_op(hc_ck_expz(t0), t0, 0, 1);
+  const Fp12 a = ck_mul_op(hc_ck_expz(t1), t1, 1, 0);
+  const Fp12 b = ck_mul_op(ck_mul_op(hc_ck_expz(hc_ck_expz(a)), a, 2, 0), a, 0, 1);
+  const Fp12 c = ck_mul_op(ck_mul_op(f2, f2, 0, 0), f2, 0, 0);
+  const Fp12 res = n ? ck_mul_op(b, c, 0, 0) : fp12_one();
+  const Fp2* u[6] = {&res.c0.c0, &res.c0.c1, &res.c0.c2, &res.c1.c0, &res.c1.c1, &res.c1.c2};
+  const Fp2* v[6] = {&ref.c0.c0, &ref.c0.c1, &ref.c0.c2, &ref.c1.c0, &ref.c1.c1, &ref.c1.c2};
+  for (int i = 0; i < 6; ++i)
+    if (!fp2_eq(*u[i], *v[i])) return 0;
+  return 1;
+}

@@ -252,3 +252,23 @@ def test_karabina_exponentiation_matches_granger_scott(hc):
     hc.hc_cyc_exp_check.restype = ctypes.c_int
     hc.hc_cyc_exp_check.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
     assert hc.hc_cyc_exp_check(0xD1CE5EED, 24) == 0
+
+
+def test_check_pipeline_matches_pair_check(hc):
+    """Recover's pairing-check pipeline (checks.h: per-round lines without the G1 point, the Miller value from two
+    line tables, the final exponentiation split at the batch inversions and the compressed chains) equals
+    final_exp_cubed(miller_loop<2>) on the host: valid and invalid (key, H, sigma) triples of the golden chain, each
+    pair dropped alone (np = 1, 2) and both."""
+    from tests.fixtures import chain, chain_arrays
+
+    c = chain()
+    _, _, _, sigs, msgs = chain_arrays(c)
+    pk = hx(c["pk"])
+    dst = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"
+    hc.hc_ck_pipeline_check.restype = ctypes.c_int
+    for i in range(6):
+        out = ctypes.create_string_buffer(96)
+        hc.hc_hash_to_g2(bytes(msgs[i]), 32, dst, len(dst), out)
+        h = out.raw
+        for sig, np_ in ((bytes(sigs[i]), 3), (bytes(sigs[i + 1]), 3), (bytes(sigs[i]), 1), (bytes(sigs[i]), 2)):
+            assert hc.hc_ck_pipeline_check(pk, h, sig, np_) == 1, (i, np_)
