@@ -774,10 +774,11 @@ def main():
     ap.add_argument("--no-c1", action="store_true", help="no C1 / live-latency lines")
     ap.add_argument("--status-bufs", type=int, default=int(os.environ.get("DG_SETS", "10")),
                     help="steps whose verdicts may be in flight (at least the library's workspace sets, DG_SETS = 10)")
-    ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("BENCH_HW_QUEUES", "16")),
-                    help="HIP hardware queues per process (GPU_MAX_HW_QUEUES, set before HIP starts; 0 keeps the "
-                         "environment's): the library's 10 workspace streams, its per-item stream and the caller's "
-                         "streams each want their own queue (DESIGN.md §5.3)")
+    ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("BENCH_HW_QUEUES", "0")),
+                    help="HIP hardware queues per process (GPU_MAX_HW_QUEUES, set before HIP starts).  0 (default): "
+                         "the environment's value, else the library's own default, which libdrandgpu.so asks for "
+                         "when it is loaded (16: the library's 10 workspace streams, its per-item stream and the "
+                         "caller's streams each want their own queue, DESIGN.md §5.3)")
     args = ap.parse_args()
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)  # inherited by the ranks started below
@@ -798,6 +799,12 @@ def main():
     # the chain before anything touches the GPU: no pinned file covering G rounds -> exit 3 (require_chain)
     G = args.global_rounds or (100000 if world == 1 else 1000000)
     chain = require_chain(G, args.allow_unlinked)
+    # load libdrandgpu.so before torch starts HIP, as a program linked against it would: its load-time default of
+    # the hardware queue count (GPU_MAX_HW_QUEUES, unless this process set one) then applies
+    from drand_amd import _lib as L
+
+    L.load()
+    hw_queues = L.hw_queues()
 
     import torch
     import torch.distributed as dist
@@ -980,7 +987,7 @@ def main():
                                     "one shared group key (BASELINE configs[%d])"
                                     % (G, world, -(-G // world), args.batch, 1 if G <= 100000 else 3)),
                        "global_rounds": G, "rounds_per_gpu": n, "batches_per_gpu": nb,
-                       "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                       "hip_hw_queues": hw_queues,
                        "parallelism": "rounds sharded dp%d" % world},
             "batch_fallbacks": fallbacks}
     tables = {"kernel_time_share": share, "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},

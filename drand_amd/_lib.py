@@ -84,6 +84,15 @@ def load():
     return _lib
 
 
+def hw_queues():
+    """GPU_MAX_HW_QUEUES as the C environment holds it (libdrandgpu.so sets its default there at load time, which
+    os.environ, copied at interpreter start, does not see); HIP's own default 4 if unset."""
+    libc = ctypes.CDLL(None)
+    libc.getenv.restype = ctypes.c_char_p
+    v = libc.getenv(b"GPU_MAX_HW_QUEUES")
+    return int(v) if v else 4
+
+
 def lib(device=None):
     """The library with a device selected (LOCAL_RANK, else 0)."""
     global _device

@@ -120,6 +120,16 @@ struct Ctx {
 
 std::mutex g_mu;
 Ctx g_ctx;
+
+// HIP's hardware queues per process (GPU_MAX_HW_QUEUES, default 4) are read once, when the runtime starts (the
+// process's first HIP call).  The library keeps up to DG_SETS = 10 batches in flight on streams of their own plus the
+// per-item stream, and with 4 queues those streams share queues: a cross-stream wait queued on a shared queue holds
+// every stream behind it (7.9 M against 14 M verified rounds/s).  So when the library is loaded
+// and the process has not chosen a value, it asks for kDefaultHwQueues -- for a program linked against it (the cgo
+// drand binary) this runs before main, so before any HIP call.  An explicit GPU_MAX_HW_QUEUES (any value) is kept;
+// a process that started HIP before loading the library keeps the queues it has.
+constexpr const char* kDefaultHwQueues = "16";
+__attribute__((constructor)) void dg_default_hw_queues() { setenv("GPU_MAX_HW_QUEUES", kDefaultHwQueues, 0); }
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {

@@ -4,6 +4,7 @@ fallback exists)."""
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -92,13 +93,14 @@ def test_prewarmed_kernels_hold_the_largest_private_segment():
     runs (a larger private segment needed later regrows the queue's scratch mid-pipeline: stalls, or
     HSA_STATUS_ERROR_OUT_OF_RESOURCES).  From the gfx950 code-object metadata of the built objects: the per-item
     kernels hold the largest private segment of all; the other large-scratch kernels run on the per-item stream too
-    (k_clear_rounds, k_sign, k_hash_to_g2), and k_rc_combine holds the largest of every kernel that runs on the
+    (k_clear_rounds, k_sign, k_hash_to_g2, the k_ck_* pipeline), and k_rc_combine holds the largest of every kernel that runs on the
     workspace streams."""
     import tempfile
 
     from tools import resource_usage as RU
 
-    objs = [os.path.join(ROOT, "drand_amd", "csrc", t) for t in ("drand_gpu.o", "kernels_hot.o", "kernels_verify.o")]
+    tus = ("drand_gpu.o", "kernels_hot.o", "kernels_verify.o") + tuple("kernels_check_%s.o" % p for p in "abcde")
+    objs = [os.path.join(ROOT, "drand_amd", "csrc", t) for t in tus]
     if not all(os.path.exists(o) for o in objs):
         pytest.skip("library objects not built")
     with tempfile.TemporaryDirectory() as tmp:
@@ -107,5 +109,27 @@ def test_prewarmed_kernels_hold_the_largest_private_segment():
     first = max(ks[k] for k in per_item)
     assert first == max(ks.values()), sorted(ks.items(), key=lambda x: -x[1])[:4]
     per_item_stream = per_item + ("k_clear_rounds", "k_sign", "k_hash_to_g2")
-    rest = {k: v for k, v in ks.items() if k not in per_item_stream}
+    # (Recover's pairing-check pipeline, checks.h, runs on the per-item stream as well)
+    rest = {k: v for k, v in ks.items() if k not in per_item_stream and not k.startswith("k_ck_")}
     assert ks["k_rc_combine"] == max(rest.values()), sorted(rest.items(), key=lambda x: -x[1])[:4]
+
+
+_QUEUES_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+from drand_amd import _lib as L
+L.load()
+print(L.hw_queues())
+"""
+
+
+@pytest.mark.parametrize("preset,want", [(None, 16), ("4", 4), ("24", 24)])
+def test_library_load_sets_the_default_hw_queue_count(preset, want):
+    """Loading libdrandgpu.so asks HIP for 16 hardware queues (GPU_MAX_HW_QUEUES, read when the runtime starts) unless
+    the process chose a value: the default a drand process gets without reading INTEGRATION.md (no device needed)."""
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    if preset is not None:
+        env["GPU_MAX_HW_QUEUES"] = preset
+    r = subprocess.run([sys.executable, "-c", _QUEUES_CHILD, ROOT], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert int(r.stdout.strip().splitlines()[-1]) == want
