@@ -776,9 +776,9 @@ def main():
                     help="steps whose verdicts may be in flight (at least the library's workspace sets, DG_SETS = 10)")
     ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("BENCH_HW_QUEUES", "0")),
                     help="HIP hardware queues per process (GPU_MAX_HW_QUEUES, set before HIP starts).  0 (default): "
-                         "the environment's value, else the library's own default, which libdrandgpu.so asks for "
-                         "when it is loaded (16: the library's 10 workspace streams, its per-item stream and the "
-                         "caller's streams each want their own queue, DESIGN.md §5.3)")
+                         "the environment's value, else the library's own load-time default (16: the library's 10 "
+                         "workspace streams, its per-item stream and the caller's streams each want their own queue, "
+                         "DESIGN.md §5.3)")
     args = ap.parse_args()
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)  # inherited by the ranks started below
@@ -799,12 +799,12 @@ def main():
     # the chain before anything touches the GPU: no pinned file covering G rounds -> exit 3 (require_chain)
     G = args.global_rounds or (100000 if world == 1 else 1000000)
     chain = require_chain(G, args.allow_unlinked)
-    # load libdrandgpu.so before torch starts HIP, as a program linked against it would: its load-time default of
-    # the hardware queue count (GPU_MAX_HW_QUEUES, unless this process set one) then applies
-    from drand_amd import _lib as L
-
-    L.load()
-    hw_queues = L.hw_queues()
+    # the library's load-time default of the hardware queue count (drand_gpu.hip dg_default_hw_queues: 16 unless the
+    # process set GPU_MAX_HW_QUEUES) reaches a program linked against it before its first HIP call; here torch, which
+    # brings its own HIP runtime, starts HIP and must start it first, so the bench applies the same default itself
+    if args.hw_queues <= 0:
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    hw_queues = int(os.environ["GPU_MAX_HW_QUEUES"])
 
     import torch
     import torch.distributed as dist
