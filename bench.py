@@ -158,6 +158,33 @@ def roofline_of(kt, kernel_units, peak, extra=None, config="head"):
     return out
 
 
+def pipeline_roofline(kt, checks, rounds, peak, extra=None, config="c5"):
+    """Roofline of Recover's per-item pass as the pairing-check pipeline (checks.h): the algorithmic multiply-adds of
+    every check the pass ran (profiles/opcounts.json: k_ck_prep[m] by member count m, the same rest per check) and of
+    the per-round lines, over the summed HIP-event time of every k_ck_* launch of the call.  None when the call ran
+    no k_ck_* kernel (the round-3 single-lane kernel, DG_CK_OLD=1)."""
+    ck = {k: v for k, v in kt.items() if k.startswith("k_ck_")}
+    if not ck:
+        return None
+    oc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["per_unit"]
+    rest = sum(oc[k]["macs"] for k in ("k_ck_lines2", "k_ck_miller", "k_ck_fe1", "k_ck_inv", "k_ck_mul (11 per check)",
+                                       "k_ck_expsq (5 per check)", "k_ck_expdec (5 per check)"))
+    n = sum(checks.values())
+    macs = sum(c * (oc["k_ck_prep[%d]" % m]["macs"] + rest) for m, c in checks.items()) + \
+        rounds * oc["k_ck_round_lines (per round)"]["macs"]
+    us = sum(a * l for a, l in ck.values())
+    achieved = macs / (us * 1e-6) / 1e12
+    pk = peak.get("tmac_s") if peak else None
+    trf = traffic_of("k_ck_* pipeline", config)
+    out = {"bound": "valu-int", "achieved": achieved, "peak": pk, "unit": "TMAC/s", "frac": achieved / pk if pk else None,
+           "traffic": trf, "kernel": "k_ck_* pipeline", "kernel_avg_us": us, "units_per_launch": n,
+           "macs_per_unit": macs / max(n, 1), "issue_frac": None, "peak_source": peak.get("source") if peak else None,
+           "per_kernel_share": {k: round(a * l / us, 4) for k, (a, l) in ck.items()}}
+    if extra:
+        out.update(extra)
+    return out
+
+
 COMPACT_ROOF = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_avg_us", "units_per_launch",
                 "macs_per_unit", "issue_frac", "chip", "overlapped")
 
@@ -486,10 +513,14 @@ def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=
     g1 = L.group_counts()
     L.check(L.lib().dg_set_timing(0))
     checks = {"k_verify_groups[%d]" % (m + 1): g1[m] - g0[m] for m in range(4)}
-    # k_rs_sac: one unit = one round's joint column MSM (priced at t = 129 over a scattered index set)
-    roof = roofline_of(kt, {"k_verify_groups": checks, "k_rs_sac": R}, peak,
-                       {"timing": "HIP events on the launch stream, one dg_recover call",
-                        "checks_by_members": checks}, "c5")
+    # the per-item pass as a whole (the pairing-check pipeline of checks.h), or the dominant kernel of the call when
+    # it ran the round-3 single-lane kernel (DG_CK_OLD=1); k_rs_sac: one unit = one round's joint column MSM (priced at
+    # t = 129 over a scattered index set)
+    ext = {"timing": "HIP events on the launch stream, one dg_recover call", "checks_by_members": checks}
+    roof = pipeline_roofline(kt, {m + 1: g1[m] - g0[m] for m in range(4)}, R, peak, ext, "c5")
+    if roof is None:
+        roof = roofline_of(kt, {"k_verify_groups": checks, "k_rs_sac": R}, peak, ext, "c5")
+    rs_roof = roofline_of({k: v for k, v in kt.items() if k == "k_rs_sac"}, {"k_rs_sac": R}, peak, None, "c5")
     ncorrupt = np.array([len(items)], np.int64)
     if world > 1:
         import torch
@@ -503,6 +534,7 @@ def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=
             "rounds_per_gpu": R, "partials_per_round": n, "corrupted_shares": int(ncorrupt[0]),
             "short_rounds": n_short, "s_per_step": dt, "allgather_s": gdt,
             "statuses_per_s": int((gss != 255).sum()) / (dt + gdt), "setup_s": gen_s, "roofline": roof,
+            "rs_sac_roofline": rs_roof,
             "host_api_s_per_step": host_dt, "host_api_value": R_total / (host_dt + gdt),
             "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
             "note": "inputs resident in HBM (dg_recover_dev); the batch equation fails, so the examined prefix of "
@@ -662,6 +694,7 @@ def headline_roofline(kt, kt_iso, per, peak, G, steps, world, dt):
 
 # keys of a sub-line (recover, adversarial, ...) that go to the side file instead of the printed line
 SIDE_KEYS = ("kernel_avg_us", "kernel_avg_us_isolated", "kernel_time_share", "note", "sample", "partials_generated_s",
+             "rs_sac_roofline",
              "setup_s", "checks_by_members", "timing", "allgather_s", "host_api_s_per_step", "rounds_per_gpu",
              "partials_per_round", "recover_s", "recover_from_verdicts_s")
 

@@ -230,16 +230,42 @@ DGI Fp fp_sqr(const Fp& a) { return fp_sqr_r(DG_A12(a)); }
 #define DG_PIN_FP12(f)                                                                                                \
   asm volatile("" : "+v"((f).l[0]), "+v"((f).l[1]), "+v"((f).l[2]), "+v"((f).l[3]), "+v"((f).l[4]), "+v"((f).l[5]), \
                "+v"((f).l[6]), "+v"((f).l[7]), "+v"((f).l[8]), "+v"((f).l[9]), "+v"((f).l[10]), "+v"((f).l[11]))
+// The product itself is the separated-operand-scanning form of the exponentiation kernel (fp28.h fp28_sos_*: 27
+// independent column sums, then 14 reduction rows of independent multiply-adds) unless DG_FP_SOS=0: its dependency
+// chains are a few instructions long, where the single-accumulator column scan of fp28_mont_mul chains every
+// multiply-add of a column -- latency a lone wave cannot hide (the pipeline kernels run at 1-2 waves per SIMD).
+#ifndef DG_FP_SOS
+#define DG_FP_SOS 1
+#endif
 DGI Fp fp_mul(Fp a, Fp b) {
   DG_PIN_FP12(a);
   DG_PIN_FP12(b);
+#if DG_FP_SOS
+  uint32_t x[14], y[14], d[14];
+  fp28_unpack(a.l, x);
+  fp28_unpack(b.l, y);
+  fp28_sos_mul_d(x, y, d);
+  Fp r;
+  fp28_pack(d, r.l);
+  r = fp_reduce_once(r);
+#else
   Fp r = fp28_mul(a, b);
+#endif
   DG_PIN_FP12(r);
   return r;
 }
 DGI Fp fp_sqr(Fp a) {
   DG_PIN_FP12(a);
+#if DG_FP_SOS
+  uint32_t x[14], d[14];
+  fp28_unpack(a.l, x);
+  fp28_sos_sqr_d(x, d);
+  Fp r;
+  fp28_pack(d, r.l);
+  r = fp_reduce_once(r);
+#else
   Fp r = fp28_sqr(a);
+#endif
   DG_PIN_FP12(r);
   return r;
 }

@@ -10,6 +10,8 @@
 //   6  v_add_u32, 7 v_fma_f32 (full-rate calibration: the issue rate of the probe's own structure)
 //   8  v_fma_f32 on normal floats (7 starts from the integer bit patterns c + lane, f32 denormals: the round-3 3.83-cycle
 //      reading of form 7 against the guide's 2 cycles; this form tells whether the denormal operands cost the rate)
+//   9  v_fma_f32 with an inline-constant addend (two VGPR sources instead of three: whether the VGPR operand reads,
+//      not the multiplier, set the 4-cycle issue of the three-source forms 7, 8 and v_mad_u64_u32)
 // Each workgroup stamps s_memtime / s_memrealtime (scalar counter reads) around its loop, so the clock the
 // chip held during the measured launches is known (MI355X_MICROARCH.md 'DVFS give-back' item 6): the
 // in-kernel clock is the median over workgroups of d(memtime) / d(realtime) x 100 MHz.  The rate is timed
@@ -24,14 +26,14 @@ constexpr int CH = 8;
 
 template <int KIND>
 __global__ void __launch_bounds__(256) k_probe(uint64_t* out, uint64_t* clk, uint32_t seed, int iters) {
-  uint32_t a = seed + threadIdx.x, b = KIND == 8 ? __float_as_uint(0.999f) : seed * 3 + 7;
+  uint32_t a = seed + threadIdx.x, b = KIND >= 8 ? __float_as_uint(0.999f) : seed * 3 + 7;
   uint64_t acc[CH];
   uint32_t acc32[CH];
   uint64_t cc[CH];
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     acc[c] = c + threadIdx.x;
-    acc32[c] = KIND == 8 ? __float_as_uint(1.0f + 0.001f * (c + threadIdx.x)) : c + threadIdx.x;
+    acc32[c] = KIND >= 8 ? __float_as_uint(1.0f + 0.001f * (c + threadIdx.x)) : c + threadIdx.x;
     cc[c] = 0;
   }
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
@@ -53,6 +55,8 @@ __global__ void __launch_bounds__(256) k_probe(uint64_t* out, uint64_t* clk, uin
         asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(acc32[c]) : "v"(b));
       else if (KIND == 6)
         asm volatile("v_add_u32 %0, %0, %1" : "+v"(acc32[c]) : "v"(b));
+      else if (KIND == 9)
+        asm volatile("v_fma_f32 %0, %0, %1, 1.0" : "+v"(acc32[c]) : "v"(b));
       else
         asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(acc32[c]) : "v"(b));
     }
@@ -81,6 +85,7 @@ static ProbeFn probe_fn(int kind) {
     case 5: return k_probe<5>;
     case 6: return k_probe<6>;
     case 8: return k_probe<8>;
+    case 9: return k_probe<9>;
     default: return k_probe<7>;
   }
 }

@@ -363,3 +363,99 @@ extern "C" void oc_recover_sac(const uint8_t* sigs96, const uint32_t* idx, uint3
   for (size_t q = 1; q < part.size(); ++q) s = jac_add(s, part[q]);
   take(out + 6);
 }
+
+// Recover's pairing-check pipeline (checks.h) for one check of m shares of one round: per kernel, in the order of
+// out (3 counters each): 0 k_ck_prep (m subgroup checks, the weighted sums and their affine forms), 1 k_ck_lines2
+// (the 68 lines of the pair (-g1, b)), 2 k_ck_miller, 3 k_ck_fe1, 4 k_ck_inv (+ the batch inversion's ~3 products
+// per value), 5 k_ck_mul (all eleven launches of a check together), 6 k_ck_expsq (all five), 7 k_ck_expdec (all five,
+// + the batch inversion's 3 products per value for the 6 norms of each), 8 k_ck_round_lines (per ROUND: h_eff and
+// the 68 lines of H_r).  No zero Karabina denominator occurs on these inputs (k_ck_explain: none).
+extern "C" void oc_check_pipeline(const uint8_t* pk48s, const uint8_t* msg, const uint8_t* dst, uint32_t dl,
+                                  const uint8_t* sigs96, uint32_t m, uint64_t* out) {
+  G2J q = hash_to_g2_uncleared(msg, 32, dst, dl);
+  G1A pk[4];
+  G2A s[4];
+  for (uint32_t i = 0; i < m; ++i) {
+    g1_decompress(pk[i], pk48s + 48 * i, false);
+    g2_decompress(s[i], sigs96 + 96 * i, false);
+  }
+  auto bump = [](uint64_t* o, uint32_t n) {  // Montgomery's trick of a batch inversion: ~3 products per value
+    o[0] += 3ull * n;
+  };
+  reset();
+  const G2A h = g2_to_aff(g2_clear_cofactor(q));
+  std::vector<CkLine> l1(CK_STEPS), l2(CK_STEPS);
+  ck_lines(h.x, h.y, [&](uint32_t st, const CkLine& l) { l1[st] = l; });
+  take(out + 24);
+  reset();
+  for (uint32_t i = 0; i < m; ++i) (void)g2_in_subgroup_aff(s[i].x, s[i].y);
+  G1A a = pk[0];
+  G2A b = s[0];
+  if (m > 1) {
+    G1J xp[4];
+    G2J sp[4];
+    uint64_t rho[4];
+    for (uint32_t i = 0; i < 4; ++i) {
+      xp[i] = i < m ? jac_from_aff(pk[i]) : jac_infinity<Fp>();
+      sp[i] = i < m ? jac_from_aff(s[i]) : jac_infinity<Fp2>();
+      rho[i] = i < m ? rlc_coeff(0x5eed, i) : 0;
+    }
+    a = g1_to_aff(jac_msm4_sac(xp, rho));
+    b = g2_to_aff(jac_msm4_sac(sp, rho));
+  }
+  take(out + 0);
+  reset();
+  ck_lines(b.x, b.y, [&](uint32_t st, const CkLine& l) { l2[st] = l; });
+  take(out + 3);
+  reset();
+  const Fp12 f = ck_miller(3u, a.x, a.y, [&](uint32_t st, uint32_t pair) { return pair ? l2[st] : l1[st]; });
+  take(out + 6);
+  reset();
+  CkInv inv;
+  const Fp nt = ck_fe1(f, inv);
+  take(out + 9);
+  const Fp nti = fp_inv(nt);
+  reset();
+  const Fp12 finv = ck_inv(f, inv, nti);
+  take(out + 12);
+  bump(out + 12, 1);
+  uint64_t mul[3] = {0, 0, 0}, sq[3] = {0, 0, 0}, dec[3] = {0, 0, 0};
+  auto mulop = [&](const Fp12& x, const Fp12& y, uint32_t nf, uint32_t cj) {
+    uint64_t t[3];
+    reset();
+    const Fp12 r = ck_mul_op(x, y, nf, cj);
+    take(t);
+    for (int k = 0; k < 3; ++k) mul[k] += t[k];
+    return r;
+  };
+  auto expz = [&](const Fp12& x) {
+    CycC sn[CK_NPOW];
+    Fp nv[CK_NPOW];
+    uint64_t t[3];
+    reset();
+    (void)ck_expsq(x, [&](int i, const CycC& c, const Fp& n) { sn[i] = c; nv[i] = n; });
+    take(t);
+    for (int k = 0; k < 3; ++k) sq[k] += t[k];
+    Fp ni[CK_NPOW];
+    for (int i = 0; i < CK_NPOW; ++i) ni[i] = fp_inv(nv[i]);
+    reset();
+    const Fp12 r = ck_expdec([&](int i, CycC& c, Fp& n) { c = sn[i]; n = ni[i]; });
+    take(t);
+    for (int k = 0; k < 3; ++k) dec[k] += t[k];
+    dec[0] += 3ull * CK_NPOW;
+    return r;
+  };
+  const Fp12 f1 = mulop(finv, f, 0, 1);
+  const Fp12 f2 = mulop(f1, f1, 2, 0);
+  const Fp12 t0 = mulop(expz(f2), f2, 0, 1);
+  const Fp12 t1 = mulop(expz(t0), t0, 0, 1);
+  const Fp12 aa = mulop(expz(t1), t1, 1, 0);
+  const Fp12 bb = mulop(mulop(expz(expz(aa)), aa, 2, 0), aa, 0, 1);
+  const Fp12 cc = mulop(mulop(f2, f2, 0, 0), f2, 0, 0);
+  (void)mulop(bb, cc, 0, 0);
+  for (int k = 0; k < 3; ++k) {
+    out[15 + k] = mul[k];
+    out[18 + k] = sq[k];
+    out[21 + k] = dec[k];
+  }
+}
