@@ -31,6 +31,10 @@
 
 namespace dg {
 
+// minimum waves per SIMD of the pipeline kernels (A/B knob: 1 lets a kernel use the whole 512-entry register file)
+#ifndef DG_CK_WAVES
+#define DG_CK_WAVES 1
+#endif
 constexpr uint32_t CK_STEPS = 68;      // Miller steps over |z| = 0xd201000000010000: 63 doublings + 5 additions
 constexpr uint32_t CK_CHUNK = 131072;  // checks per pipeline launch (~3.7 GB of workspace)
 constexpr int CK_NPOW = 6;             // set bits of |z|: the powers a^(2^k) of the compressed chain
@@ -205,7 +209,7 @@ static_assert(CK_GRP == GRP, "one group per check");
 // H_r = h_eff(Q_r) and its 68 lines (once per Recover call and round): rl[s * R + r]; hinf[r]: H_r is the identity
 // (kernels_check_a.hip)
 #if DG_TU_CHECK == 1
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_round_lines(uint32_t R, const G2JStore* Q, CkLine* rl, uint8_t* hinf) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_round_lines(uint32_t R, const G2JStore* Q, CkLine* rl, uint8_t* hinf) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   const G2A h = g2_to_aff(g2_clear_cofactor(load_g2j(Q[r])));
@@ -214,7 +218,7 @@ DG_KERNEL void __launch_bounds__(64, 1) k_ck_round_lines(uint32_t R, const G2JSt
   ck_lines(h.x, h.y, [&](uint32_t s, const CkLine& l) { rl[(size_t)s * R + r] = l; });
 }
 // the check's members (glist group off + g), as verify_group: subgroup checks, the weighted sums (group_combine)
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
                                                   const uint64_t* seedp, const G1AStore* keys, const uint32_t* item_slot,
                                                   const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
                                                   uint32_t subgroup, unsigned long long* cnt, CkState* st) {
@@ -241,27 +245,27 @@ DG_KERNEL void __launch_bounds__(64, 1) k_ck_prep(uint32_t G, uint32_t off, cons
   st[g] = c;
 }
 // the lines of the pair (-g1, b): l2[s * G + g]
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G || !(st[g].np & 2)) return;
   const G2A b = load_g2a(st[g].b);
   ck_lines(b.x, b.y, [&](uint32_t s, const CkLine& l) { l2[(size_t)s * G + g] = l; });
 }
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   CkInv c;
   nv[g] = ck_fe1(F[g], c);
   inv[g] = c;
 }
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_inv(uint32_t G, const Fp12* F, const CkInv* inv, const Fp* nvinv,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_inv(uint32_t G, const Fp12* F, const CkInv* inv, const Fp* nvinv,
                                                  Fp12* out) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   out[g] = ck_inv(F[g], inv[g], nvinv[g]);
 }
 // the six compressed powers sn[i * G + g], their denominators' norms nv[i * G + g], zero[g]
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   zero[g] = ck_expsq(X[g], [&](int i, const CycC& c, const Fp& n) {
@@ -288,22 +292,22 @@ DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st
   }
 }
 #else
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_round_lines(uint32_t R, const G2JStore* Q, CkLine* rl, uint8_t* hinf);
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_round_lines(uint32_t R, const G2JStore* Q, CkLine* rl, uint8_t* hinf);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
                                                   const uint64_t* seedp, const G1AStore* keys, const uint32_t* item_slot,
                                                   const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
                                                   uint32_t subgroup, unsigned long long* cnt, CkState* st);
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2);
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv);
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_inv(uint32_t G, const Fp12* F, const CkInv* inv, const Fp* nvinv,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_inv(uint32_t G, const Fp12* F, const CkInv* inv, const Fp* nvinv,
                                                  Fp12* out);
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero);
 DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const Fp12* res, uint8_t* status,
                                                    uint8_t* fin);
 #endif
 // the Miller value of every check (kernels_check_b.hip)
 #if DG_TU_CHECK == 2
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_miller(uint32_t G, uint32_t R, const CkState* st, const CkLine* rl,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, uint32_t R, const CkState* st, const CkLine* rl,
                                                     const CkLine* l2, Fp12* F) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
@@ -314,25 +318,25 @@ DG_KERNEL void __launch_bounds__(64, 1) k_ck_miller(uint32_t G, uint32_t R, cons
   });
 }
 #else
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_miller(uint32_t G, uint32_t R, const CkState* st, const CkLine* rl,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, uint32_t R, const CkState* st, const CkLine* rl,
                                                     const CkLine* l2, Fp12* F);
 #endif
 // out = a * frob^nfrob(b), conjugated if `conj` (kernels_check_c.hip)
 #if DG_TU_CHECK == 3
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_mul(uint32_t G, const Fp12* A, const Fp12* B, uint32_t nfrob, uint32_t conj,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_mul(uint32_t G, const Fp12* A, const Fp12* B, uint32_t nfrob, uint32_t conj,
                                                  Fp12* out) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   out[g] = ck_mul_op(A[g], B[g], nfrob, conj);
 }
 #else
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_mul(uint32_t G, const Fp12* A, const Fp12* B, uint32_t nfrob, uint32_t conj,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_mul(uint32_t G, const Fp12* A, const Fp12* B, uint32_t nfrob, uint32_t conj,
                                                  Fp12* out);
 #endif
 // x^z from the compressed powers (kernels_check_d.hip); lanes whose chain hit a zero denominator are left to
 // k_ck_explain
 #if DG_TU_CHECK == 4
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_expdec(uint32_t G, const CycC* sn, const Fp* nvinv, const uint8_t* zero,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expdec(uint32_t G, const CycC* sn, const Fp* nvinv, const uint8_t* zero,
                                                     Fp12* XZ) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G || zero[g]) return;
@@ -342,18 +346,18 @@ DG_KERNEL void __launch_bounds__(64, 1) k_ck_expdec(uint32_t G, const CycC* sn, 
   });
 }
 #else
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_expdec(uint32_t G, const CycC* sn, const Fp* nvinv, const uint8_t* zero,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expdec(uint32_t G, const CycC* sn, const Fp* nvinv, const uint8_t* zero,
                                                     Fp12* XZ);
 #endif
 // x^z by the uncompressed chain for the lanes with a zero Karabina denominator (kernels_check_e.hip)
 #if DG_TU_CHECK == 5
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_explain(uint32_t G, const uint8_t* zero, const Fp12* X, Fp12* XZ) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(uint32_t G, const uint8_t* zero, const Fp12* X, Fp12* XZ) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G || !zero[g]) return;
   XZ[g] = ck_exp_plain(X[g]);
 }
 #else
-DG_KERNEL void __launch_bounds__(64, 1) k_ck_explain(uint32_t G, const uint8_t* zero, const Fp12* X, Fp12* XZ);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(uint32_t G, const uint8_t* zero, const Fp12* X, Fp12* XZ);
 #endif
 #endif
 
