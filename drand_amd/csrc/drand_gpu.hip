@@ -3,6 +3,7 @@
 // runs on the device.  No CPU fallback exists: without a gfx950 device the API returns DG_E_NODEV.
 #include <hip/hip_runtime.h>
 
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1030,6 +1031,22 @@ int check_chunk(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k, uin
   return launch("k_ck_verdict", k_ck_verdict, G, 128, st, G, (const CkState*)b.st, (const Fp12*)b.T0, status, fin);
 }
 
+// The pass schedule of the pipeline: DG_CK_PASSES passes with speculative margins (DG_CK_MARGIN0 in the first,
+// DG_CK_MARGIN in the others), then the final pass over every unverified share before the t-th valid one.  Every pass
+// costs at least the latency of one check (a lane's Miller loop alone is ~13 ms), however few checks it holds.
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+int ck_passes() {
+  static const int v = env_int("DG_CK_PASSES", 8);
+  return v < 0 ? 0 : v;
+}
+uint32_t ck_margin(int which) {
+  static const int m0 = env_int("DG_CK_MARGIN0", 6), m = env_int("DG_CK_MARGIN", 2);
+  return (uint32_t)(which == 0 ? m0 : m);
+}
+
 // DG_CK_OLD=1 (A/B only): Recover's per-item pass as the round-3 single-lane kernel k_verify_groups instead of the
 // pipeline of checks.h
 bool ck_old() {
@@ -1055,15 +1072,17 @@ int prefix_pass(uint32_t R, uint32_t k, uint32_t t, const uint64_t* seed, const 
     RET(wsT(S_LIST, 4 * (N + 1), &glist));
     RET(launch("k_ck_round_lines", k_ck_round_lines, R, 64, st, R, Q, rl, hinf));
     const uint32_t grp = group_size();
-    constexpr int kPasses = 8;
+    const int kPasses = ck_passes();
     for (int pass = 0; pass <= kPasses; ++pass) {
       HIPCHK(hipMemsetAsync(glist, 0, 4, st));
-      const uint32_t margin = grp < 2 ? 0u : (pass == 0 ? 6u : 2u);
+      const uint32_t margin = grp < 2 ? 0u : (pass == 0 ? ck_margin(0) : ck_margin(1));
       RET(launch("k_prefix_groups", k_prefix_groups, R, 128, st, R, k, t, pass == kPasses ? 1u : 0u, grp, margin,
                  (const uint8_t*)status, (const uint8_t*)fin, glist));
       uint32_t G = 0;
       HIPCHK(hipMemcpyAsync(&G, glist, 4, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
+      static const bool trace = getenv("DG_CK_TRACE") != nullptr;  // diagnostics: checks per pass
+      if (trace) fprintf(stderr, "[dg] prefix pass %d: %u checks\n", pass, G);
       for (uint32_t off = 0; off < G; off += CK_CHUNK)
         RET(check_chunk(std::min(G - off, CK_CHUNK), off, glist, k, R, seed, keys, item_slot, hinf, rl, S, status, fin,
                         subgroup, st));
