@@ -36,7 +36,7 @@ namespace dg {
 #define DG_CK_WAVES 1
 #endif
 constexpr uint32_t CK_STEPS = 68;      // Miller steps over |z| = 0xd201000000010000: 63 doublings + 5 additions
-constexpr uint32_t CK_CHUNK = 131072;  // checks per pipeline launch (~3.7 GB of workspace)
+constexpr uint32_t CK_CHUNK = 524288;  // checks per pipeline launch (~15 GB of workspace: one chunk per pass at C5)
 constexpr int CK_NPOW = 6;             // set bits of |z|: the powers a^(2^k) of the compressed chain
 constexpr uint32_t CK_GRP = 4;         // members per check at most (kernels.h GRP)
 

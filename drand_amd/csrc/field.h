@@ -602,9 +602,57 @@ DGI Fp2 fp2_one() { return Fp2{fp_one(), fp_zero()}; }
 DGI bool fp2_is_zero(const Fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
 DGI bool fp2_eq(const Fp2& a, const Fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
 DGI Fp2 fp2_sel(bool c, const Fp2& a, const Fp2& b) { return Fp2{fp_sel(c, a.c0, b.c0), fp_sel(c, a.c1, b.c1)}; }
+// DG_FP2_ILV=1 (the pipeline TUs, kernels_check_*.hip): the two coefficients' carry chains interleaved limb by limb.
+// A carry chain alone puts a wait state (s_nop) between every two limbs on gfx950 -- a VALU that writes the carry
+// (VCC / an SGPR pair) and the next VALU that reads it -- about 11% of the per-item pairing kernels' instructions;
+// with the c0 and c1 chains alternating, each carry is read two instructions after it is written.
+#ifndef DG_FP2_ILV
+#define DG_FP2_ILV 0
+#endif
+#if DG_FP2_ILV
+DGI Fp2 fp2_reduce2(const Fp2& s) {
+  Fp2 d;
+  uint32_t b0 = 0, b1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    d.c0.l[i] = subb32(s.c0.l[i], P_LIMBS[i], b0, &b0);
+    d.c1.l[i] = subb32(s.c1.l[i], P_LIMBS[i], b1, &b1);
+  }
+  return Fp2{fp_sel(b0 == 0, s.c0, d.c0), fp_sel(b1 == 0, s.c1, d.c1)};
+}
+DGI Fp2 fp2_add(const Fp2& a, const Fp2& b) {
+  Fp2 s;
+  uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    s.c0.l[i] = addc32(a.c0.l[i], b.c0.l[i], c0, &c0);
+    s.c1.l[i] = addc32(a.c1.l[i], b.c1.l[i], c1, &c1);
+  }
+  return fp2_reduce2(s);
+}
+DGI Fp2 fp2_sub(const Fp2& a, const Fp2& b) {
+  Fp2 d;
+  uint32_t b0 = 0, b1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    d.c0.l[i] = subb32(a.c0.l[i], b.c0.l[i], b0, &b0);
+    d.c1.l[i] = subb32(a.c1.l[i], b.c1.l[i], b1, &b1);
+  }
+  const uint32_t m0 = 0u - b0, m1 = 0u - b1;
+  uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    d.c0.l[i] = addc32(d.c0.l[i], P_LIMBS[i] & m0, c0, &c0);
+    d.c1.l[i] = addc32(d.c1.l[i], P_LIMBS[i] & m1, c1, &c1);
+  }
+  return d;
+}
+DGI Fp2 fp2_dbl(const Fp2& a) { return fp2_add(a, a); }
+#else
 DGI Fp2 fp2_add(const Fp2& a, const Fp2& b) { return Fp2{fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
 DGI Fp2 fp2_sub(const Fp2& a, const Fp2& b) { return Fp2{fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
 DGI Fp2 fp2_dbl(const Fp2& a) { return Fp2{fp_dbl(a.c0), fp_dbl(a.c1)}; }
+#endif
 DGI Fp2 fp2_neg(const Fp2& a) { return Fp2{fp_neg(a.c0), fp_neg(a.c1)}; }
 DGI Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
 // DG_FP2_CALL=1 (the per-item pairing TU): fp2_mul / fp2_sqr are one out-of-line call each (fp2_mul_r below,

@@ -5,4 +5,5 @@
 #define DG_FP_CALL 3
 #define DG_INLINE12 1
 #define DG_CYC_SQR 1
+#define DG_FP2_ILV 1
 #include "kernels.h"
