@@ -35,6 +35,11 @@ namespace dg {
 #ifndef DG_CK_WAVES
 #define DG_CK_WAVES 1
 #endif
+// ... of the kernels with a smaller live set (k_ck_prep, k_ck_fe1, k_ck_expsq: measured faster at 2 than at 1, their
+// few spills notwithstanding; the Fp12-product kernels lost at 2)
+#ifndef DG_CK_WAVES2
+#define DG_CK_WAVES2 2
+#endif
 constexpr uint32_t CK_STEPS = 68;      // Miller steps over |z| = 0xd201000000010000: 63 doublings + 5 additions
 constexpr uint32_t CK_CHUNK = 524288;  // checks per pipeline launch (~15 GB of workspace: one chunk per pass at C5)
 constexpr int CK_NPOW = 6;             // set bits of |z|: the powers a^(2^k) of the compressed chain
@@ -218,7 +223,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_round_lines(uint32_t R, c
   ck_lines(h.x, h.y, [&](uint32_t s, const CkLine& l) { rl[(size_t)s * R + r] = l; });
 }
 // the check's members (glist group off + g), as verify_group: subgroup checks, the weighted sums (group_combine)
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
                                                   const uint64_t* seedp, const G1AStore* keys, const uint32_t* item_slot,
                                                   const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
                                                   uint32_t subgroup, unsigned long long* cnt, CkState* st) {
@@ -251,7 +256,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_lines2(uint32_t G, const 
   const G2A b = load_g2a(st[g].b);
   ck_lines(b.x, b.y, [&](uint32_t s, const CkLine& l) { l2[(size_t)s * G + g] = l; });
 }
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   CkInv c;
@@ -265,7 +270,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_inv(uint32_t G, const Fp1
   out[g] = ck_inv(F[g], inv[g], nvinv[g]);
 }
 // the six compressed powers sn[i * G + g], their denominators' norms nv[i * G + g], zero[g]
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   zero[g] = ck_expsq(X[g], [&](int i, const CycC& c, const Fp& n) {
@@ -293,15 +298,15 @@ DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st
 }
 #else
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_round_lines(uint32_t R, const G2JStore* Q, CkLine* rl, uint8_t* hinf);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
                                                   const uint64_t* seedp, const G1AStore* keys, const uint32_t* item_slot,
                                                   const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
                                                   uint32_t subgroup, unsigned long long* cnt, CkState* st);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_inv(uint32_t G, const Fp12* F, const CkInv* inv, const Fp* nvinv,
                                                  Fp12* out);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero);
 DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const Fp12* res, uint8_t* status,
                                                    uint8_t* fin);
 #endif
