@@ -168,35 +168,6 @@ DGI G2J g2_madd_lean(const G2J& p, const Fp2& qx, const Fp2& qy) {
 #define DG_MADD_MUL fp2_mul_in
 #define DG_MADD_SQR fp2_sqr_in
 #endif
-template <class S>
-DGI void g2_madd_lds(S& a, const Fp2& qx, const Fp2& qy) {
-  if (fp2_is_zero(a.z)) {
-    a.x = qx;
-    a.y = qy;
-    a.z = fp2_one();
-    return;
-  }
-  const Fp2 Z1Z1 = DG_MADD_SQR(a.z);
-  const Fp2 H = fp2_sub(DG_MADD_MUL(qx, Z1Z1), a.x);
-  const Fp2 r = fp2_dbl(fp2_sub(DG_MADD_MUL(DG_MADD_MUL(qy, a.z), Z1Z1), a.y));
-  if (fp2_is_zero(H)) {
-    const G2J t = g2_add_aff_rare(G2J{a.x, a.y, a.z}, qx, qy);
-    a.x = t.x;
-    a.y = t.y;
-    a.z = t.z;
-    return;
-  }
-  const Fp2 HH = DG_MADD_SQR(H);
-  a.z = fp2_sub(fp2_sub(DG_MADD_SQR(fp2_add(a.z, H)), Z1Z1), HH);
-  const Fp2 I = fp2_dbl(fp2_dbl(HH));
-  const Fp2 J = DG_MADD_MUL(H, I);
-  const Fp2 V = DG_MADD_MUL(a.x, I);
-  const Fp2 YJ2 = fp2_dbl(DG_MADD_MUL(a.y, J));
-  const Fp2 X3 = fp2_sub(fp2_sub(DG_MADD_SQR(r), J), fp2_dbl(V));
-  a.x = X3;
-  a.y = fp2_sub(DG_MADD_MUL(r, fp2_sub(V, X3)), YJ2);
-}
-
 // dbl-2009-l with the accumulator in LDS, products as g2_madd_lds (the identity stays the identity)
 template <class S>
 DGI void g2_dbl_lds(S& a) {
@@ -209,6 +180,33 @@ DGI void g2_dbl_lds(S& a) {
   const Fp2 X3 = fp2_sub(DG_MADD_SQR(E), fp2_dbl(D));
   a.x = X3;
   a.y = fp2_sub(DG_MADD_MUL(E, fp2_sub(D, X3)), fp2_dbl(fp2_dbl(fp2_dbl(C))));
+}
+
+template <class S>
+DGI void g2_madd_lds(S& a, const Fp2& qx, const Fp2& qy) {
+  if (fp2_is_zero(a.z)) {
+    a.x = qx;
+    a.y = qy;
+    a.z = fp2_one();
+    return;
+  }
+  const Fp2 Z1Z1 = DG_MADD_SQR(a.z);
+  const Fp2 H = fp2_sub(DG_MADD_MUL(qx, Z1Z1), a.x);
+  const Fp2 r = fp2_dbl(fp2_sub(DG_MADD_MUL(DG_MADD_MUL(qy, a.z), Z1Z1), a.y));
+  if (fp2_is_zero(H)) {  // a = +-q: the tangent, or the identity (inline: no call frame in scratch)
+    if (fp2_is_zero(r)) g2_dbl_lds(a);
+    else a.z = fp2_zero();
+    return;
+  }
+  const Fp2 HH = DG_MADD_SQR(H);
+  a.z = fp2_sub(fp2_sub(DG_MADD_SQR(fp2_add(a.z, H)), Z1Z1), HH);
+  const Fp2 I = fp2_dbl(fp2_dbl(HH));
+  const Fp2 J = DG_MADD_MUL(H, I);
+  const Fp2 V = DG_MADD_MUL(a.x, I);
+  const Fp2 YJ2 = fp2_dbl(DG_MADD_MUL(a.y, J));
+  const Fp2 X3 = fp2_sub(fp2_sub(DG_MADD_SQR(r), J), fp2_dbl(V));
+  a.x = X3;
+  a.y = fp2_sub(DG_MADD_MUL(r, fp2_sub(V, X3)), YJ2);
 }
 
 // The full addition (add-2007-bl) with the accumulator in LDS, products as g2_madd_lds; q any Jacobian point.
@@ -228,11 +226,9 @@ DGI void g2_add_lds(S& a, const G2J& q) {
   const Fp2 S1 = DG_MADD_MUL(DG_MADD_MUL(a.y, q.z), Z2Z2);
   const Fp2 H = fp2_sub(DG_MADD_MUL(q.x, Z1Z1), U1);
   const Fp2 r = fp2_dbl(fp2_sub(DG_MADD_MUL(DG_MADD_MUL(q.y, a.z), Z1Z1), S1));
-  if (fp2_is_zero(H)) {
-    const G2J t = g2_add_rare(G2J{a.x, a.y, a.z}, q);
-    a.x = t.x;
-    a.y = t.y;
-    a.z = t.z;
+  if (fp2_is_zero(H)) {  // a = +-q, as g2_madd_lds
+    if (fp2_is_zero(r)) g2_dbl_lds(a);
+    else a.z = fp2_zero();
     return;
   }
   a.z = DG_MADD_MUL(fp2_sub(fp2_sub(DG_MADD_SQR(fp2_add(a.z, q.z)), Z1Z1), Z2Z2), H);

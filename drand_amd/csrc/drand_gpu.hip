@@ -61,6 +61,18 @@ struct Set {
   bool busy = false;
 };
 
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+// a power of two in [1, hi] from the environment (rounded down), else dflt
+uint32_t env_pow2(const char* name, uint32_t dflt, uint32_t hi) {
+  const int v = env_int(name, (int)dflt);
+  uint32_t p = 1;
+  while (p * 2 <= (uint32_t)(v < 1 ? 1 : v) && p * 2 <= hi) p *= 2;
+  return p;
+}
+
 struct Ctx {
   int device = -1;
   bool ready = false;
@@ -113,6 +125,12 @@ struct Ctx {
   bool phased = getenv("DG_FUSED") == nullptr;
   // single-key MSM first levels as mixed Jacobian chunk sums (DG_MSM_JAC=1: A/B only) instead of affine levels
   bool msm_jac = getenv("DG_MSM_JAC") != nullptr;
+  // single-key MSM bucket stage (msm_run): lanes per bucket over the affine chunk sums (a power of two <= MSM_BSPLIT),
+  // and the row-sum fan-in of their partials and of the slice partials (2: pairwise levels; larger: fewer launches,
+  // longer chains per lane)
+  uint32_t msm_bsplit = env_pow2("DG_MSM_BSPLIT", MSM_BSPLIT, MSM_BSPLIT);
+  uint32_t msm_fold = env_pow2("DG_MSM_FOLD", 2, 64);
+  uint32_t slice_fold = env_pow2("DG_SLICE_FOLD", 2, 64);
   // batch inversions by the chunked form only (DG_BINV_CHUNKED=1: A/B only) instead of the block tree
   bool binv_chunked = getenv("DG_BINV_CHUNKED") != nullptr;
   // batched subgroup check as its own launch after the final exponentiation (DG_SUB_SEPARATE=1: A/B only)
@@ -440,8 +458,9 @@ int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JSt
       RET(launch("k_msm_aff_add", k_msm_aff_add, n, 128, st, l, maxg, nsides, nbk, (const uint32_t*)cnt,
                  (const uint32_t*)offset, gl, (const uint32_t*)list, PA, PB, A, (uint32_t)E, (const Fp*)dinv, bad));
     }
-    RET(launch("k_msm_buckets_aff", k_msm_buckets_aff, nbk * MSM_BSPLIT * nsides, 128, st, nsides, nbk,
-               (const uint32_t*)cnt, (const uint32_t*)offset, (const G2AStore*)A, (uint32_t)E, BP));
+    RET(launch("k_msm_buckets_aff", k_msm_buckets_aff, nbk * g_ctx.msm_bsplit * nsides, 128, st, nsides, nbk,
+               g_ctx.msm_bsplit, (const uint32_t*)cnt, (const uint32_t*)offset, (const G2AStore*)A, (uint32_t)E, BP));
+    RET(reduce_rows(BP, tmp, nbk * nsides, g_ctx.msm_bsplit, st, g_ctx.msm_fold));  // B[side][b] = BP[side * nbk + b]
   } else {
   const size_t max_chunks_sz = ((size_t)nwin * R) / MSM_CHUNK + nbk;
   if (max_chunks_sz * nsides > 0xffffffffull) return fail(DG_E_ARG, "batch too large for the MSM");
@@ -460,10 +479,10 @@ int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JSt
              (const uint32_t*)offset, (const uint32_t*)chunk_off, (const uint32_t*)list, PA, PB, chunks));
   RET(launch("k_msm_buckets", k_msm_buckets, nbk * MSM_BSPLIT * nsides, 128, st, max_chunks, nsides, nbk,
              (const uint32_t*)chunk_off, (const G2JStore*)chunks, BP));
-  }
   RET(reduce_rows(BP, tmp, nbk * nsides, MSM_BSPLIT, st));  // B[side][b] = BP[side * nbk + b]
+  }
   RET(launch("k_msm_slices", k_msm_slices, nsides * nwin * MSM_C * MSM_SLICE_LANES, 128, st, nsides, nwin, (const G2JStore*)BP, P1));
-  RET(reduce_rows(P1, tmp, nsides * nwin * MSM_C, MSM_SLICE_LANES, st));  // S[side][w][k] = P1[...]
+  RET(reduce_rows(P1, tmp, nsides * nwin * MSM_C, MSM_SLICE_LANES, st, g_ctx.slice_fold));  // S[side][w][k] = P1[...]
   RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * nwin * nsides, 128, st, nwin, 1u, (const G2JStore*)P1, W));
   RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsides, 128, st, nwin, (const G2JStore*)W, *out));
   if (win) *win = W;
@@ -1034,10 +1053,6 @@ int check_chunk(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k, uin
 // The pass schedule of the pipeline: DG_CK_PASSES passes with speculative margins (DG_CK_MARGIN0 in the first,
 // DG_CK_MARGIN in the others), then the final pass over every unverified share before the t-th valid one.  Every pass
 // costs at least the latency of one check (a lane's Miller loop alone is ~13 ms), however few checks it holds.
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
 int ck_passes() {
   static const int v = env_int("DG_CK_PASSES", 8);
   return v < 0 ? 0 : v;
@@ -1215,7 +1230,8 @@ int recover_sac(uint32_t R, uint32_t k, uint32_t t, uint32_t Rn, const uint32_t*
                 const uint32_t* d_sel, const uint8_t* d_rst, const G2AStore* d_S, G2JStore* out, hipStream_t st) {
   const size_t n = (size_t)t * Rn;
   if (3 * n > 0x7fffffffull) return fail(DG_E_ARG, "Recover batch too large for the column tables");
-  const uint32_t ngroups = (t + RS_G - 1) / RS_G;
+  static const uint32_t gs = (uint32_t)std::max(1, std::min(64, env_int("DG_RS_G", (int)RS_G)));
+  const uint32_t ngroups = (t + gs - 1) / gs;
   RsDigits* dig;
   uint4* T4;
   uint8_t* pinf;
@@ -1235,7 +1251,7 @@ int recover_sac(uint32_t R, uint32_t k, uint32_t t, uint32_t Rn, const uint32_t*
     RET(launch("k_rs_tab_add", k_rs_tab_add, (uint32_t)(3 * n), 128, st, l, R, Rn, k, t, nl, d_rst, d_sel, d_S, T4,
                (const uint8_t*)pinf, (const Fp*)dinv));
   }
-  RET(launch("k_rs_sac", k_rs_sac, ngroups * Rn, 64, st, R, Rn, t, ngroups, nl, d_rst, (const RsDigits*)dig,
+  RET(launch("k_rs_sac", k_rs_sac, ngroups * Rn, 64, st, R, Rn, t, ngroups, gs, nl, d_rst, (const RsDigits*)dig,
              (const uint4*)T4, (const uint8_t*)pinf, Aps));
   return launch("k_rs_combine", k_rs_combine, Rn, 128, st, R, Rn, ngroups, nl, d_rst, (const G2JStore*)Aps, out);
 }

@@ -739,10 +739,25 @@ DGI Fp2 fp2_sqr_rc(const Fp2& a) { return fp2_sqr(a); }
 #else
 #define DG_PIN_FP(f) ((void)0)
 #endif
+// DG_SEQ_SOS=1: the serialised product in the separated-operand-scanning form (fp28_sos_mul_d, as DG_FP_CALL=3),
+// whose dependency chains are a few instructions long, instead of fp28_mul's column scan
+#ifndef DG_SEQ_SOS
+#define DG_SEQ_SOS 0
+#endif
 DGI Fp fp_mul_seq(Fp a, Fp b) {
   DG_PIN_FP(a);
   DG_PIN_FP(b);
+#if DG_SEQ_SOS && defined(__HIP_DEVICE_COMPILE__)
+  uint32_t x[14], y[14], d[14];
+  fp28_unpack(a.l, x);
+  fp28_unpack(b.l, y);
+  fp28_sos_mul_d(x, y, d);
+  Fp r;
+  fp28_pack(d, r.l);
+  r = fp_reduce_once(r);
+#else
   Fp r = fp_mul_inl(a, b);
+#endif
   DG_PIN_FP(r);
   return r;
 }

@@ -41,7 +41,7 @@ DGI Fr fr_sub(const Fr& a, const Fr& b) {
   for (int i = 0; i < 8; ++i) d.l[i] = addc32(d.l[i], R_LIMBS[i] & mask, c, &c);
   return d;
 }
-DGN Fr fr_mul(const Fr& a, const Fr& b) {
+DGI Fr fr_mul_in(const Fr& a, const Fr& b) {
   uint32_t t[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) t[j] = 0;
@@ -68,6 +68,7 @@ DGN Fr fr_mul(const Fr& a, const Fr& b) {
   for (int j = 0; j < 8; ++j) r.l[j] = t[j];
   return fr_reduce_once(r);
 }
+DGN Fr fr_mul(const Fr& a, const Fr& b) { return fr_mul_in(a, b); }
 // small integer (< r) -> Montgomery
 DGI Fr fr_from_u32(uint32_t v) {
   Fr a;
@@ -83,40 +84,52 @@ DGI Fr fr_to_plain(const Fr& a) {
   one.l[0] = 1;
   return fr_mul(a, one);
 }
-// a^(r-2) by the width-3 window schedule of tools/gen_constants.py (as fp_pow_sched)
-DGN Fr fr_inv(const Fr& x) {
-  Fr x2 = fr_mul(x, x);
+// a^(r-2) by the width-3 window schedule of tools/gen_constants.py (as fp_pow_sched); inline products, so a
+// caller's frame holds no by-reference operands (an out-of-line fr_mul takes its operands through the stack)
+DGI Fr fr_inv_in(const Fr& x) {
+  Fr x2 = fr_mul_in(x, x);
   Fr t[4];
   t[0] = x;
-  for (int i = 1; i < 4; ++i) t[i] = fr_mul(t[i - 1], x2);
+#pragma unroll
+  for (int i = 1; i < 4; ++i) t[i] = fr_mul_in(t[i - 1], x2);
   Fr acc = t[EXP_RM2_FIRST];
   for (int s = 0; s < EXP_RM2_NSTEPS; ++s) {
     int k = EXP_RM2_STEPS[s][0];
     int idx = EXP_RM2_STEPS[s][1];
-    for (int j = 0; j < k; ++j) acc = fr_mul(acc, acc);
+    for (int j = 0; j < k; ++j) acc = fr_mul_in(acc, acc);
     if (idx >= 0) {
       Fr m = fr_sel(idx == 1, t[0], t[1]);
       m = fr_sel(idx == 2, m, t[2]);
       m = fr_sel(idx == 3, m, t[3]);
-      acc = fr_mul(acc, m);
+      acc = fr_mul_in(acc, m);
     }
   }
   return acc;
 }
+DGN Fr fr_inv(const Fr& x) { return fr_inv_in(x); }
 
 // Lagrange coefficient at 0 of position j among the t interpolation points x_m = idx[m] + 1
 // (kyber share.RecoverCommit / lagrangeBasis): lambda_j = prod_{m != j} x_m / (x_m - x_j).
-// Returns the plain (non-Montgomery) scalar, little-endian limbs.
-DGN Fr lagrange_at_zero(const uint32_t* idx, uint32_t t, uint32_t j) {
-  Fr num = fr_const(FR_ONE), den = fr_const(FR_ONE);
-  Fr xj = fr_from_u32(idx[j] + 1);
+// Returns the plain (non-Montgomery) scalar, little-endian limbs.  One lane per coefficient (k_rs_digits), so
+// the products are inline and the factors enter in plain form: num and den each take t - 1 Montgomery products
+// starting from R, so both carry the same R^(2-t) and it cancels in num / den (no per-factor conversion).
+DGI Fr lagrange_at_zero(const uint32_t* idx, uint32_t t, uint32_t j) {
+  Fr num = fr_const(FR_ONE), den = fr_const(FR_ONE), xj;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) xj.l[i] = 0;
+  xj.l[0] = idx[j] + 1;
   for (uint32_t m = 0; m < t; ++m) {
     if (m == j) continue;
-    Fr xm = fr_from_u32(idx[m] + 1);
-    num = fr_mul(num, xm);
-    den = fr_mul(den, fr_sub(xm, xj));
+    Fr xm = xj;
+    xm.l[0] = idx[m] + 1;
+    num = fr_mul_in(num, xm);
+    den = fr_mul_in(den, fr_sub(xm, xj));
   }
-  return fr_to_plain(fr_mul(num, fr_inv(den)));
+  Fr one;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) one.l[i] = 0;
+  one.l[0] = 1;
+  return fr_mul_in(fr_mul_in(num, fr_inv_in(den)), one);
 }
 
 }  // namespace dg

@@ -372,32 +372,32 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_aff_add(uint32_t l, ui
                                                                  const Fp* ninv, uint32_t* bad);
 #endif
 
-// the bucket sums from the affine chunk sums: lane (side, b, q < MSM_BSPLIT) adds chunks q, q + MSM_BSPLIT, ...
-// of bucket b (A[offset[b] + c 2^L]) with mixed additions, the running sum in LDS (g2_madd_lds); the partials
-// are then row-summed as before
+// the bucket sums from the affine chunk sums: lane (side, b, q < bsplit) adds chunks q, q + bsplit, ... of bucket b
+// (A[offset[b] + c 2^L]) with mixed additions, the running sum in LDS (g2_madd_lds); the bsplit partials
+// BP[sb * bsplit + q] are then row-summed (bsplit <= MSM_BSPLIT, a power of two: DG_MSM_BSPLIT)
 #if defined(__HIP__) && DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_msm_buckets_aff(uint32_t nsides, uint32_t nbk, const uint32_t* count,
-                                                                      const uint32_t* offset, const G2AStore* A,
-                                                                      uint32_t E, G2JStore* BP) {
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_msm_buckets_aff(uint32_t nsides, uint32_t nbk, uint32_t bsplit,
+                                                                      const uint32_t* count, const uint32_t* offset,
+                                                                      const G2AStore* A, uint32_t E, G2JStore* BP) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nbk * MSM_BSPLIT * nsides) return;
-  uint32_t q = g % MSM_BSPLIT, sb = g / MSM_BSPLIT;
+  if (g >= nbk * bsplit * nsides) return;
+  uint32_t q = g % bsplit, sb = g / bsplit;
   uint32_t side = sb / nbk, b = sb % nbk;
   const uint32_t nch = side && b >= MSM_NBK ? 0u : (count[b] + (1u << MSM_AFF_L) - 1) >> MSM_AFF_L;
   const G2AStore* As = A + (size_t)side * E + offset[b];
   __shared__ G2JStore s_acc[128];
   G2JStore& acc = s_acc[threadIdx.x];
   store_g2j(acc, jac_infinity<Fp2>());
-  for (uint32_t c = q; c < nch; c += MSM_BSPLIT) {
+  for (uint32_t c = q; c < nch; c += bsplit) {
     const G2AStore& a = As[c << MSM_AFF_L];
     if (!a.inf) g2_madd_lds(acc, a.x, a.y);
   }
   BP[g] = acc;
 }
 #elif defined(__HIP__)
-DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_msm_buckets_aff(uint32_t nsides, uint32_t nbk, const uint32_t* count,
-                                                                      const uint32_t* offset, const G2AStore* A,
-                                                                      uint32_t E, G2JStore* BP);
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_msm_buckets_aff(uint32_t nsides, uint32_t nbk, uint32_t bsplit,
+                                                                      const uint32_t* count, const uint32_t* offset,
+                                                                      const G2AStore* A, uint32_t E, G2JStore* BP);
 #endif
 
 #if defined(__HIP__) && DG_TU_LIB

@@ -402,7 +402,7 @@ DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rc_straus(uint32_t R, uin
 //   k_rs_tab_den / batch inversion / k_rs_tab_add     three levels of the 8-entry tables
 //   k_rs_sac       lane (share group, round): the group's joint column loop, running point in LDS
 //   k_rs_combine   per round: the sum of its group partial sums
-constexpr uint32_t RS_G = 8;  // shares per lane
+constexpr uint32_t RS_G = 8;  // shares per lane (default; DG_RS_G)
 
 // sign-aligned recoding of one share's psi digits (g2_mul_u256_psi_sac): bit c of sgn set = +T in column c
 // (c < 64; column 64 is always +), um[i] bit c = u_{i+1, c}, top = the column-64 entry, even: d0 was even (add
@@ -537,15 +537,15 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_rs_tab_add(uint32_t l, uin
 }
 
 // lane (share group q, divergent round u), grid RS lanes = ngroups * Rn padded to whole waves: the columns of
-// its <= RS_G shares, one doubling per column, then the even-d0 corrections; Aps[q * Rn + u]
+// its <= gs shares (RS_G unless DG_RS_G), one doubling per column, then the even-d0 corrections; Aps[q * Rn + u]
 DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rs_sac(uint32_t R, uint32_t Rn, uint32_t t, uint32_t ngroups,
-                                                              const uint32_t* nl, const uint8_t* rst,
+                                                              uint32_t gs, const uint32_t* nl, const uint8_t* rst,
                                                               const RsDigits* dig, const uint4* T4,
                                                               const uint8_t* pinf, G2JStore* Aps) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t q = g / Rn, u = g % Rn;
   const bool live = q < ngroups && nl[u] < R && rst[nl[u]] == DG_ST_OK_;
-  const uint32_t j0 = q * RS_G, j1 = j0 + RS_G < t ? j0 + RS_G : t;
+  const uint32_t j0 = q * gs, j1 = j0 + gs < t ? j0 + gs : t;
   __shared__ G2JStore s_acc[64];
   G2JStore& acc = s_acc[threadIdx.x];
   acc.x = fp2_zero();
@@ -588,7 +588,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_rs_tab_add(uint32_t l, uin
                                                                  const uint32_t* sel, const G2AStore* S, uint4* T4,
                                                                  const uint8_t* pinf, const Fp* ninv);
 DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rs_sac(uint32_t R, uint32_t Rn, uint32_t t, uint32_t ngroups,
-                                                              const uint32_t* nl, const uint8_t* rst,
+                                                              uint32_t gs, const uint32_t* nl, const uint8_t* rst,
                                                               const RsDigits* dig, const uint4* T4,
                                                               const uint8_t* pinf, G2JStore* Aps);
 #endif

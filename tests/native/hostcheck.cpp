@@ -210,6 +210,29 @@ extern "C" int hc_aff_add_check(const uint8_t* sig_a, const uint8_t* sig_b, int 
   return jac_eq(jac_from_aff(r), want) ? 1 : 0;
 }
 
+// The LDS-form additions' exceptional cases (curve.h g2_madd_lds / g2_add_lds: a = q takes the tangent, a = -q gives
+// the identity, inline), with the accumulator a rescaled Jacobian copy of a (Z != 1), against jac_add; mode 0 chord
+// (a + b), 1 a + a, 2 a + (-a); `full` uses g2_add_lds with a Jacobian q.  1 if equal.
+extern "C" int hc_lds_add_check(const uint8_t* sig_a, const uint8_t* sig_b, int mode, int full) {
+  G2A a, b;
+  if (!g2_decompress(a, sig_a, false) || !g2_decompress(b, sig_b, false)) return -1;
+  G2A q = b;
+  if (mode == 1) q = a;
+  if (mode == 2) q = G2A{a.x, fp2_neg(a.y), false};
+  const G2J aj = jac_dbl(jac_add(jac_from_aff(a), jac_from_aff(a)));  // 4a with Z != 1 ...
+  G2J acc = jac_add(aj, jac_neg(jac_add(jac_from_aff(a), jac_dbl(jac_from_aff(a)))));  // ... minus 3a: a, Z != 1
+  if (!jac_eq(acc, jac_from_aff(a)) || fp2_eq(acc.z, fp2_one())) return -2;
+  const G2J want = jac_add(acc, jac_from_aff(q));
+  if (full) {
+    const G2J qj = jac_add(jac_dbl(jac_from_aff(q)), jac_neg(jac_from_aff(q)));  // q with Z != 1
+    g2_add_lds(acc, qj);
+  } else {
+    g2_madd_lds(acc, q.x, q.y);
+  }
+  if (jac_is_inf(acc) != jac_is_inf(want)) return 0;
+  return jac_eq(acc, want) ? 1 : 0;
+}
+
 // [k]P with the accumulator as a memory slot (curve.h g2_mul_u256_psi_lds, LDS on the device) against the
 // register form; 1 if equal
 extern "C" int hc_g2_mul_lds_check(const uint8_t* sig96, const uint32_t* k8) {

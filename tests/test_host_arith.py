@@ -195,6 +195,17 @@ def test_affine_pair_addition_matches_jacobian(hc):
             assert hc.hc_aff_add_check(sigs[i], sigs[i + 1], mode) == 1, (i, mode)
 
 
+def test_lds_addition_exceptional_cases(hc):
+    """curve.h g2_madd_lds / g2_add_lds (Recover's MSM lanes, the keyed chunk sums): a chord, a + a (the tangent) and
+    a + (-a) (the identity), the accumulator with Z != 1, against the Jacobian addition."""
+    c = load("chain_t3n5.json")
+    sigs = [hx(r["sig"]) for r in c["rounds"][:4]]
+    for i in range(len(sigs) - 1):
+        for mode in range(3):
+            for full in (0, 1):
+                assert hc.hc_lds_add_check(sigs[i], sigs[i + 1], mode, full) == 1, (i, mode, full)
+
+
 def test_wnaf_digits_host_build(hc):
     """recover.h rc_wnaf: width-5 signed digits (odd, |d| <= 15, >= 5 apart) that evaluate back to the scalar,
     including the 65th position a carry can reach."""
