@@ -886,17 +886,22 @@ def main():
     pkb = ctypes.c_char_p(pk)
     counter = [0]
 
+    # one batch per step on one rank: the verdict bitmap is packed on the batch's own stream (dg_last_batch_stream), so
+    # no cross-stream wait is queued -- with HIP's default 4 hardware queues a wait on a queue shared with another
+    # workspace set stalls that set; several batches or ranks: a side stream waits for them all
+    on_set = world == 1 and len(bounds) == 1 and not args.use_sync
+
     def enqueue(lo, hi, d_st, seed, blocking):
         args_ = (pkb, hi - lo, L.ptr(d_pr[lo:]), L.ptr(d_r[lo:]), L.ptr(d_ps), L.ptr(d_off[lo:]), L.ptr(d_sig[lo:]),
                  L.ptr(d_st[lo:]), seed)
         if blocking:
             L.check(lib.dg_verify_beacons_dev(*args_, None))
         else:
-            L.check(lib.dg_verify_beacons_dev_async(*args_, None, ctypes.c_void_p(side.cuda_stream)))
+            L.check(lib.dg_verify_beacons_dev_async(*args_, None, None if on_set else ctypes.c_void_p(side.cuda_stream)))
 
     def step(seed):
         """Enqueue this rank's batches (asynchronously: consecutive batches overlap) and the all-gather of the
-        rank's verdict bitmap on a side stream that waits for them; returns the gathered bitmap tensor."""
+        rank's verdict bitmap on a stream that follows them; returns the gathered bitmap tensor."""
         i = counter[0] % nbuf
         counter[0] += 1
         if gathered[i] is not None:
@@ -906,10 +911,15 @@ def main():
             enqueue(lo, hi, d_st, seed * 64 + j, args.use_sync)
         if args.use_sync:
             side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
+        gs = side
+        if on_set:
+            sp = ctypes.c_void_p()
+            L.check(lib.dg_last_batch_stream(ctypes.byref(sp)))
+            gs = torch.cuda.ExternalStream(sp.value, device=dev)
+        with torch.cuda.stream(gs):
             bits = shard.allgather_verdicts(d_st, world, m=mbytes)
             ev = torch.cuda.Event()
-            ev.record(side)
+            ev.record(gs)
         gathered[i] = (bits, ev)
         return bits
 

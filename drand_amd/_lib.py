@@ -49,6 +49,7 @@ SIGNATURES = {
     "dg_verify_beacons_dev": ([_P, _SZ, _P, _P, _P, _P, _P, _P, _U64, _P], _I),
     "dg_verify_beacons_dev_async": ([_P, _SZ, _P, _P, _P, _P, _P, _P, _U64, _P, _P], _I),
     "dg_wait_all": ([], _I),
+    "dg_last_batch_stream": ([_P], _I),
     "dg_last_batch_flags": ([_P], _I),
     "dg_fallback_count": ([_P], _I),
     "dg_group_counts": ([_P], _I),
@@ -168,7 +169,7 @@ def group_counts():
 def timings():
     """Per-kernel average launch time (us) accumulated since dg_set_timing(1)."""
     L = load()
-    cap = 64
+    cap = 256
     names = (ctypes.c_char_p * cap)()
     us = (ctypes.c_double * cap)()
     launches = (ctypes.c_int * cap)()

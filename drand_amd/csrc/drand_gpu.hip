@@ -83,9 +83,14 @@ struct Ctx {
   // queues stay at the ~5.7 KB of k_sign (with 8 hardware queues, every queue holding 14.5 KB failed
   // with HSA_STATUS_ERROR_OUT_OF_RESOURCES).  Only failed or isolating batches reach it.
   hipStream_t fb_stream = nullptr;
-  // DG_SHARED_FB=1 (A/B only): the per-item kernels on the batch's own stream, every workspace queue prewarmed with
-  // their private segment (the round-2 arrangement)
-  bool shared_fb = getenv("DG_SHARED_FB") != nullptr;
+  // shared_fb: the per-item kernels on the batch's own stream instead, every workspace queue prewarmed with their
+  // private segment.  Chosen in dg_init by the hardware queue count (GPU_MAX_HW_QUEUES, HIP's default 4): with fewer
+  // queues than the active sets' streams + the per-item stream + one for the caller, streams share queues, and the
+  // per-item stream's two cross-stream barriers per batch then stall whatever stream shares their queue (headline
+  // at 4 queues, 10 sets: 8.7 M rounds/s with the hop, 11.1 M without; at 16 queues the hop is free and keeps the
+  // large scratch reservation on one queue).  DG_SHARED_FB=0 / 1 forces either.
+  bool shared_fb = false;
+  hipStream_t last_stream = nullptr;  // the set stream of the last asynchronous batch (dg_last_batch_stream)
   int cur = 0, next = 0;
   bool timing = false;
   std::vector<Timing> timings;
@@ -686,21 +691,26 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
     out->batched_sub = batched_sub;
     return 0;
   }
-  // the per-item pass on the per-item stream (g_ctx.fb_stream), ordered after and before this set's stream; the
-  // per-round H_r = h_eff(Q_r) there too (k_clear_rounds: ~5 KB of private segment, kept off the set streams)
+  // the per-item pass on the per-item stream (g_ctx.fb_stream), ordered after and before this set's stream, or on
+  // the set's own stream (shared_fb); the per-round H_r = h_eff(Q_r) there too (k_clear_rounds: ~5 KB of private
+  // segment, kept off the set streams unless shared_fb)
   G2AStore* H;
   RET(wsT(S_H, b.R, &H));
   Set& set = cur_set();
   const hipStream_t batch_st = st;
-  HIPCHK(hipEventRecord(set.to_fb, batch_st));
-  st = g_ctx.shared_fb ? batch_st : g_ctx.fb_stream;
-  HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
+  if (!g_ctx.shared_fb) {
+    HIPCHK(hipEventRecord(set.to_fb, batch_st));
+    st = g_ctx.fb_stream;
+    HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
+  }
   RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, (const uint32_t*)flag, b.Q, H));
   RET(launch_shm("k_verify_items", k_verify_items, N, 64, verify_lds(), st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
              (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status, batched_sub));
-  HIPCHK(hipEventRecord(set.from_fb, st));
-  st = batch_st;
-  HIPCHK(hipStreamWaitEvent(st, set.from_fb, 0));
+  if (!g_ctx.shared_fb) {
+    HIPCHK(hipEventRecord(set.from_fb, st));
+    st = batch_st;
+    HIPCHK(hipStreamWaitEvent(st, set.from_fb, 0));
+  }
   RET(launch("k_count_fallback", k_count_fallback, 1, 64, st, (const uint32_t*)flag, g_ctx.fallbacks));
   return 0;
 }
@@ -1390,6 +1400,12 @@ int dg_init(int device) {
   // k_hash_to_g2) all run on the per-item stream, and the workspace streams are prewarmed with the largest of the
   // rest, k_rc_combine (~4 KB; tests/test_abi.py checks both orderings against the code-object metadata):
   // with 12 workspace streams on 32 queues at k_sign's 5.7 KB, dg_init failed with that error.
+  if (const char* e = getenv("DG_SHARED_FB")) {
+    g_ctx.shared_fb = atoi(e) != 0;
+  } else {
+    const int hwq = env_int("GPU_MAX_HW_QUEUES", 4);
+    g_ctx.shared_fb = hwq < active_sets() + 2;
+  }
   hipFuncAttributes fa_items{}, fa_groups{};
   HIPCHK(hipFuncGetAttributes(&fa_items, reinterpret_cast<const void*>(k_verify_items)));
   HIPCHK(hipFuncGetAttributes(&fa_groups, reinterpret_cast<const void*>(k_verify_groups)));
@@ -1627,6 +1643,7 @@ static int enqueue_beacons_dev(const uint8_t* pk48_host, size_t n, const uint64_
   RET(verify_single_key(pk48_host, (uint32_t)n, d_msgs, 32, d_sigs, d_status, fresh_seed(seed), st));
   HIPCHK(hipEventRecord(set.done, st));
   set.busy = true;
+  g_ctx.last_stream = st;
   if (done_stream) HIPCHK(hipStreamWaitEvent(done_stream, set.done, 0));
   return 0;
 }
@@ -1693,6 +1710,15 @@ int dg_verify_beacons_dev_async(const uint8_t* pk48_host, size_t n, const uint64
   RET(check_args_n(n));
   return enqueue_beacons_dev(pk48_host, n, d_prev_round, d_round, d_prev_sigs, d_prev_sig_off, d_sigs96, d_status, seed,
                              (hipStream_t)in_stream, (hipStream_t)done_stream);
+}
+
+int dg_last_batch_stream(void** out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  if (!out) return fail(DG_E_ARG, "bad arguments");
+  if (!g_ctx.last_stream) return fail(DG_E_ARG, "no asynchronous batch enqueued yet");
+  *out = (void*)g_ctx.last_stream;
+  return 0;
 }
 
 int dg_last_batch_flags(uint32_t* out2) {

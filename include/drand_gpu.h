@@ -167,6 +167,13 @@ int dg_verify_beacons_dev_async(const uint8_t* pk48_host, size_t n, const uint64
                                 const uint64_t* d_round, const uint8_t* d_prev_sigs, const uint32_t* d_prev_sig_off,
                                 const uint8_t* d_sigs96, uint8_t* d_status, uint64_t seed, void* in_stream,
                                 void* done_stream);
+/* The HIP stream (hipStream_t) the most recent dg_verify_beacons_dev_async batch was enqueued on.  Work the caller
+ * enqueues there runs after that batch with no cross-stream wait: with fewer hardware queues than streams
+ * (GPU_MAX_HW_QUEUES, HIP's default 4) a wait queued on a shared queue holds every stream behind it, so a consumer
+ * of one batch's statuses (an all-gather, a copy) is cheapest on this stream.  The stream stays owned by the library
+ * (valid until dg_shutdown); DG_E_ARG before the first asynchronous batch.  (No reference counterpart: drand verifies
+ * beacons one at a time, beacon/chain.go:65-71.) */
+int dg_last_batch_stream(void** out);
 /* Diagnostics of the most recent verification batch: out2[0] = 1 if the random-linear-combination
  * batch equation held, out2[1] = 1 if some item was checked on its own (duplicate key cell).  A valid
  * batch must pass on the batch path; the per-item fallback only decides failures. */

@@ -38,6 +38,7 @@ EXPECT_TYPE(dg_verify_beacons_dev, int (*)(const uint8_t*, size_t, const uint64_
 EXPECT_TYPE(dg_verify_beacons_dev_async, int (*)(const uint8_t*, size_t, const uint64_t*, const uint64_t*,
                                                  const uint8_t*, const uint32_t*, const uint8_t*, uint8_t*, uint64_t,
                                                  void*, void*));
+EXPECT_TYPE(dg_last_batch_stream, int (*)(void**));
 EXPECT_TYPE(dg_last_batch_flags, int (*)(uint32_t*));
 EXPECT_TYPE(dg_fallback_count, int (*)(uint64_t*));
 EXPECT_TYPE(dg_group_counts, int (*)(uint64_t*));
@@ -89,6 +90,8 @@ int main() {
   expect("dg_verify_beacons_dev", dg_verify_beacons_dev(pk, 1, pr, rr, msg, off, sig, st, 1, nullptr), DG_E_NODEV);
   expect("dg_verify_beacons_dev_async",
          dg_verify_beacons_dev_async(pk, 1, pr, rr, msg, off, sig, st, 1, nullptr, nullptr), DG_E_NODEV);
+  void* stream_out = nullptr;
+  expect("dg_last_batch_stream", dg_last_batch_stream(&stream_out), DG_E_NODEV);
   expect("dg_last_batch_flags", dg_last_batch_flags(flags), DG_E_NODEV);
   expect("dg_fallback_count", dg_fallback_count(&u64), DG_E_NODEV);
   uint64_t u64x4[4];
