@@ -40,6 +40,10 @@ namespace dg {
 #ifndef DG_CK_WAVES2
 #define DG_CK_WAVES2 2
 #endif
+// ... of k_ck_sub (its accumulator in LDS: 18 KB per 64-lane workgroup, so at most 2 per SIMD anyway)
+#ifndef DG_CK_SUB_WAVES
+#define DG_CK_SUB_WAVES 2
+#endif
 constexpr uint32_t CK_STEPS = 68;      // Miller steps over |z| = 0xd201000000010000: 63 doublings + 5 additions
 constexpr uint32_t CK_CHUNK = 524288;  // checks per pipeline launch (~15 GB of workspace: one chunk per pass at C5)
 constexpr int CK_NPOW = 6;             // set bits of |z|: the powers a^(2^k) of the compressed chain
@@ -209,6 +213,27 @@ DGI Fp12 ck_exp_plain(const Fp12& a) {
   return fp12_conj(acc);
 }
 
+// curve.h g2_in_subgroup_aff with the accumulator in LDS (g2_dbl_lds / g2_madd_lds, serialised products): the same
+// test, [|z|]P by double-and-add and psi(P) == [z]P compared projectively, without a register-resident Jacobian
+// point beside the formulas' temporaries (inlined as in g2_in_subgroup_aff, 221 spilled VGPRs at 2 waves per SIMD)
+template <class Slot>
+DGI bool ck_in_subgroup(const Fp2& x, const Fp2& y, Slot& acc) {
+  acc.x = x;
+  acc.y = y;
+  acc.z = fp2_one();
+#pragma unroll 1
+  for (int b = 62; b >= 0; --b) {
+    g2_dbl_lds(acc);
+    if ((Z_ABS >> b) & 1) g2_madd_lds(acc, x, y);
+  }
+  const Fp2 az = acc.z;
+  if (fp2_is_zero(az)) return false;
+  const Fp2 zz = fp2_sqr_seq(az);
+  const Fp2 px = fp2_mul_seq(fp2_conj(x), fp2_const(PSI_CX));
+  if (!fp2_eq(fp2_mul_seq(px, zz), acc.x)) return false;
+  const Fp2 py = fp2_mul_seq(fp2_conj(y), fp2_const(PSI_CY));
+  return fp2_eq(fp2_mul_seq(py, fp2_mul_seq(zz, az)), fp2_neg(acc.y));
+}
 #if defined(__HIP__)
 static_assert(CK_GRP == GRP, "one group per check");
 // H_r = h_eff(Q_r) and its 68 lines (once per Recover call and round): rl[s * R + r]; hinf[r]: H_r is the identity
@@ -222,7 +247,25 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_round_lines(uint32_t R, c
   if (h.inf) return;
   ck_lines(h.x, h.y, [&](uint32_t s, const CkLine& l) { rl[(size_t)s * R + r] = l; });
 }
-// the check's members (glist group off + g), as verify_group: subgroup checks, the weighted sums (group_combine)
+// the G2 subgroup checks of the members (one lane per member slot 4 (off + g) + m of the list), ahead of k_ck_prep:
+// a dense single-purpose launch instead of up to four checks in a row inside a k_ck_prep lane.  A member outside G2
+// gets group_combine's decode-error verdict here (fin = FIN_DONE, so group_combine leaves it out); a recheck was
+// subgroup-checked by its group.
+DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_ck_sub(uint32_t G, uint32_t off, const uint32_t* glist,
+                                                                const G2AStore* S, uint8_t* status, uint8_t* fin) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ G2JStore s_acc[64];
+  if (g >= 4 * G) return;
+  const uint32_t i = glist[4 + 4 * (size_t)off + g];
+  if (i == ~0u || fin[i] == FIN_RECHECK) return;
+  const G2A s = load_g2a(S[i]);
+  if (!s.inf && !ck_in_subgroup(s.x, s.y, s_acc[threadIdx.x])) {
+    status[i] = DG_ST_SIG_DECODE_;
+    fin[i] = FIN_DONE;
+  }
+}
+// the check's members (glist group off + g), as verify_group: subgroup checks (unless k_ck_sub ran: subgroup = 0),
+// the weighted sums (group_combine)
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
                                                   const uint64_t* seedp, const G1AStore* keys, const uint32_t* item_slot,
                                                   const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
@@ -302,6 +345,8 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep(uint32_t G, uint32_
                                                   const uint64_t* seedp, const G1AStore* keys, const uint32_t* item_slot,
                                                   const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
                                                   uint32_t subgroup, unsigned long long* cnt, CkState* st);
+DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_ck_sub(uint32_t G, uint32_t off, const uint32_t* glist,
+                                                                const G2AStore* S, uint8_t* status, uint8_t* fin);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_inv(uint32_t G, const Fp12* F, const CkInv* inv, const Fp* nvinv,

@@ -1032,8 +1032,11 @@ int check_chunk(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k, uin
                 uint8_t* status, uint8_t* fin, uint32_t subgroup, hipStream_t st) {
   CkBufs b;
   RET(ck_bufs(b));
-  RET(launch("k_ck_prep", k_ck_prep, G, 64, st, G, off, glist, k, seed, keys, item_slot, hinf, S, status, fin, subgroup,
-             g_ctx.gcount, b.st));
+  static const bool sub_inline = getenv("DG_CK_SUB_INLINE") != nullptr;  // A/B: subgroup checks inside k_ck_prep
+  if (subgroup && !sub_inline)
+    RET(launch("k_ck_sub", k_ck_sub, 4 * G, 64, st, G, off, glist, (const G2AStore*)S, status, fin));
+  RET(launch("k_ck_prep", k_ck_prep, G, 64, st, G, off, glist, k, seed, keys, item_slot, hinf, S, status, fin,
+             sub_inline ? subgroup : 0u, g_ctx.gcount, b.st));
   RET(launch("k_ck_lines2", k_ck_lines2, G, 64, st, G, (const CkState*)b.st, b.l2));
   RET(launch("k_ck_miller", k_ck_miller, G, 64, st, G, R, (const CkState*)b.st, rl, (const CkLine*)b.l2, b.F));
   // easy part: f1 = f^-1 conj(f), f2 = f1 frob^2(f1)

@@ -537,6 +537,7 @@ DGN uint32_t group_combine(const uint32_t* mem, uint32_t n, uint64_t seed, const
   uint32_t nl = 0;
   for (uint32_t m = 0; m < n; ++m) {
     const uint32_t i = mem[m];
+    if (fin[i] == FIN_DONE) continue;  // decided before the check (checks.h k_ck_sub: outside G2)
     const G2A s = load_g2a(S[i]);
     // (a recheck was subgroup-checked by its group)
     if (subgroup && fin[i] != FIN_RECHECK && !s.inf && !g2_in_subgroup_aff(s.x, s.y)) {

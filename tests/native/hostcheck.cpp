@@ -233,6 +233,17 @@ extern "C" int hc_lds_add_check(const uint8_t* sig_a, const uint8_t* sig_b, int 
   return jac_eq(acc, want) ? 1 : 0;
 }
 
+// checks.h ck_in_subgroup (k_ck_sub: the LDS-accumulator form) against curve.h g2_in_subgroup_aff for the point
+// decoded from in96 without a subgroup check (any point of E'(Fp2)); -1 if in96 is not on the curve, else the
+// verdict (1 in G2, 0 not) when both agree, 2 when they differ
+extern "C" int hc_ck_subgroup_check(const uint8_t* in96) {
+  G2A a;
+  if (!g2_decompress(a, in96, false) || a.inf) return -1;
+  G2J slot;
+  const bool x = ck_in_subgroup(a.x, a.y, slot), y = g2_in_subgroup_aff(a.x, a.y);
+  return x != y ? 2 : (x ? 1 : 0);
+}
+
 // [k]P with the accumulator as a memory slot (curve.h g2_mul_u256_psi_lds, LDS on the device) against the
 // register form; 1 if equal
 extern "C" int hc_g2_mul_lds_check(const uint8_t* sig96, const uint32_t* k8) {

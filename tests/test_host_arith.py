@@ -206,6 +206,26 @@ def test_lds_addition_exceptional_cases(hc):
                 assert hc.hc_lds_add_check(sigs[i], sigs[i + 1], mode, full) == 1, (i, mode, full)
 
 
+def test_ck_subgroup_matches_curve_check(hc):
+    """checks.h ck_in_subgroup (Recover's k_ck_sub, accumulator in LDS) decides G2 membership as curve.h
+    g2_in_subgroup_aff: chain signatures (in G2) and points of E'(Fp2) outside G2 (one bit of x flipped, the
+    corrupt.py bitflip_x mode, where the flipped x is still on the curve)."""
+    c = load("chain_t3n5.json")
+    sigs = [hx(r["sig"]) for r in c["rounds"][:8]]
+    seen = {0: 0, 1: 0}
+    for sig in sigs:
+        assert hc.hc_ck_subgroup_check(sig) == 1
+        seen[1] += 1
+        for bit in range(8, 40):
+            b = bytearray(sig)
+            b[95 - bit // 8] ^= 1 << (bit % 8)
+            v = hc.hc_ck_subgroup_check(bytes(b))
+            assert v in (-1, 0), v
+            if v == 0:
+                seen[0] += 1
+    assert seen[0] >= 20, seen
+
+
 def test_wnaf_digits_host_build(hc):
     """recover.h rc_wnaf: width-5 signed digits (odd, |d| <= 15, >= 5 apart) that evaluate back to the scalar,
     including the 65th position a carry can reach."""
