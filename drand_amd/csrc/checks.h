@@ -13,7 +13,8 @@
 //
 //   per round (once per Recover call):  k_ck_round_lines  H_r = h_eff(Q_r) and its 68 lines RL[s][r]
 //   per pass and chunk of checks (G lanes, drand_gpu.hip check_chunk):
-//     k_ck_prep      the group's members: subgroup checks, a = sum rho X, b = sum rho S (kernels.h group_combine)
+//     k_ck_sub       one lane per member: the G2 subgroup check of S_i (accumulator in LDS)
+//     k_ck_prep      the group's members: a = sum rho X, b = sum rho S (kernels.h group_combine)
 //     k_ck_lines2    the 68 lines of the pair (-g1, b) -> L2[s][g] (b's G2 state lives only here)
 //     k_ck_miller    f = the product of both pairs' lines at a and at -g1 (the Fp12 accumulator and one line)
 //     k_ck_fe1       the pieces of f^-1 down to one Fp norm per check  -> batch inversion (phases.h k_binv_*)
