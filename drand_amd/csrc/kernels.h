@@ -360,23 +360,6 @@ DG_KERNEL void __launch_bounds__(256) k_key_combine(uint32_t nslots, const uint6
 }
 #endif
 
-// 2-D segmented sum: out[row * ocols + j] = sum_{c in [j*chunk, (j+1)*chunk) and < cols} in[row * cols + c]
-#if DG_TU_LIB
-// (rows of a block with skip[row / 64] != 0 are left alone: skip may be null)
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_sum_rows(uint32_t rows, uint32_t cols, uint32_t chunk, const G2JStore* in,
-                                                 G2JStore* out, const uint8_t* skip) {
-  uint32_t ocols = (cols + chunk - 1) / chunk;
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= rows * ocols) return;
-  uint32_t row = g / ocols, j = g % ocols;
-  if (skip && skip[row / 64]) return;
-  uint32_t a = j * chunk, b = a + chunk < cols ? a + chunk : cols;
-  const G2JStore* p = in + (size_t)row * cols;
-  G2J acc = load_g2j(p[a]);
-  for (uint32_t c = a + 1; c < b; ++c) acc = jac_add(acc, load_g2j(p[c]));
-  store_g2j(out[g], acc);
-}
-#endif
 
 // Pair s on one 128-lane workgroup (coop.h): P side and Q side prepared cooperatively (for key pairs the
 // hash-side sum is cofactor-cleared here, once per key and batch), then the cooperative Miller loop.

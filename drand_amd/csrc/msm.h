@@ -372,6 +372,31 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_aff_add(uint32_t l, ui
                                                                  const Fp* ninv, uint32_t* bad);
 #endif
 
+// 2-D segmented sum: out[row * ocols + j] = sum_{c in [j*chunk, (j+1)*chunk) and < cols} in[row * cols + c]
+// (rows of a block with skip[row / 64] != 0 are left alone: skip may be null).  Hot TU: the running sum in LDS and
+// the additions inlined with serialised products (curve.h g2_add_lds), no call frames -- these launches sit on a
+// batch's critical path (11 per headline batch), where the library TU's out-of-line products cost ~180 us each.
+#if defined(__HIP__) && DG_TU_HOT
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_sum_rows(uint32_t rows, uint32_t cols, uint32_t chunk,
+                                                                const G2JStore* in, G2JStore* out, const uint8_t* skip) {
+  __shared__ G2JStore s_acc[128];
+  uint32_t ocols = (cols + chunk - 1) / chunk;
+  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= rows * ocols) return;
+  uint32_t row = g / ocols, j = g % ocols;
+  if (skip && skip[row / 64]) return;
+  uint32_t a = j * chunk, b = a + chunk < cols ? a + chunk : cols;
+  const G2JStore* p = in + (size_t)row * cols;
+  G2JStore& acc = s_acc[threadIdx.x];
+  acc = p[a];
+  for (uint32_t c = a + 1; c < b; ++c) g2_add_lds(acc, load_g2j(p[c]));
+  out[g] = acc;
+}
+#elif defined(__HIP__)
+DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_sum_rows(uint32_t rows, uint32_t cols, uint32_t chunk,
+                                                                const G2JStore* in, G2JStore* out, const uint8_t* skip);
+#endif
+
 // the bucket sums from the affine chunk sums: lane (side, b, q < bsplit) adds chunks q, q + bsplit, ... of bucket b
 // (A[offset[b] + c 2^L]) with mixed additions, the running sum in LDS (g2_madd_lds); the bsplit partials
 // BP[sb * bsplit + q] are then row-summed (bsplit <= MSM_BSPLIT, a power of two: DG_MSM_BSPLIT)

@@ -41,7 +41,13 @@ def load(prof):
             acc[cfg][names[d]][c].append(v)
             if c in ("FETCH_SIZE", "WRITE_SIZE"):
                 acc[cfg][names[d]]["_dur_" + c].append(dur[d])
-    return {cfg: {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in ks.items()} for cfg, ks in acc.items()}
+    out = {cfg: {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in ks.items()} for cfg, ks in acc.items()}
+    for cfg, ks in acc.items():  # dispatch counts, for the per-call sums of a multi-kernel pipeline
+        for k, cs in ks.items():
+            for c in ("FETCH_SIZE", "WRITE_SIZE"):
+                if c in cs:
+                    out[cfg][k]["_n_" + c] = len(cs[c])
+    return out
 
 
 def main(prof, out_csv, out_json=None):
@@ -61,6 +67,16 @@ def main(prof, out_csv, out_json=None):
                     sec[k]["bytes_per_launch"] = None
                     sec[k]["note"] = ("FETCH/WRITE_SIZE imply %.0f TB/s over the launch, beyond the memory "
                                       "system: counter not usable for this (long, scratch-heavy) kernel" % (b / t / 1e12))
+        # Recover's pairing-check pipeline (checks.h k_ck_*) as one unit, as bench.py prices it: the bytes of every
+        # k_ck_* dispatch of the run over the number of per-item passes (one k_ck_round_lines per dg_recover call)
+        calls = ks.get("k_ck_round_lines", {}).get("_n_FETCH_SIZE", 0)
+        if calls:
+            tot = 0.0
+            for k, c in ks.items():
+                if k.startswith("k_ck_") and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                    tot += (2 * c["FETCH_SIZE"] * c["_n_FETCH_SIZE"] + c["WRITE_SIZE"] * c["_n_WRITE_SIZE"]) * 1024
+            sec["k_ck_* pipeline"] = {"bytes_per_launch": tot / calls, "calls": calls,
+                                      "note": "sum over every k_ck_* dispatch / dg_recover calls of the run"}
         out["configs"][cfg] = sec
     json.dump(out, open(out_json or os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
     cols = sorted({c for ks in m.values() for cs in ks.values() for c in cs if not c.startswith("_")})
