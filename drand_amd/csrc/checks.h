@@ -314,13 +314,17 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_inv(uint32_t G, const Fp1
   out[g] = ck_inv(F[g], inv[g], nvinv[g]);
 }
 // the six compressed powers sn[i * G + g], their denominators' norms nv[i * G + g], zero[g]
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero) {
+// (a lane with a zero denominator also appends itself to zl: zl[0] the count, zl[1..] the lanes)
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero,
+                                                            uint32_t* zl) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
-  zero[g] = ck_expsq(X[g], [&](int i, const CycC& c, const Fp& n) {
-              sn[(size_t)i * G + g] = c;
-              nv[(size_t)i * G + g] = n;
-            }) ? 1 : 0;
+  const bool z = ck_expsq(X[g], [&](int i, const CycC& c, const Fp& n) {
+    sn[(size_t)i * G + g] = c;
+    nv[(size_t)i * G + g] = n;
+  });
+  zero[g] = z ? 1 : 0;
+  if (z) zl[1 + atomicAdd(zl, 1u)] = g;
 }
 // the verdicts of the checks whose final exponentiation is res[g] (== 1: valid), written as verify_group writes them
 DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const Fp12* res, uint8_t* status,
@@ -352,7 +356,8 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_lines2(uint32_t G, const 
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_inv(uint32_t G, const Fp12* F, const CkInv* inv, const Fp* nvinv,
                                                  Fp12* out);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero,
+                                                            uint32_t* zl);
 DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const Fp12* res, uint8_t* status,
                                                    uint8_t* fin);
 #endif
@@ -401,14 +406,19 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expdec(uint32_t G, const 
                                                     Fp12* XZ);
 #endif
 // x^z by the uncompressed chain for the lanes with a zero Karabina denominator (kernels_check_e.hip)
+// over the work list zl (k_ck_expsq) with a fixed grid of CK_EXPLAIN_LANES lanes striding it; every lane exits when
+// the list is done
+constexpr uint32_t CK_EXPLAIN_LANES = 4096;
 #if DG_TU_CHECK == 5
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(uint32_t G, const uint8_t* zero, const Fp12* X, Fp12* XZ) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G || !zero[g]) return;
-  XZ[g] = ck_exp_plain(X[g]);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(const uint32_t* zl, const Fp12* X, Fp12* XZ) {
+  const uint32_t n = zl[0];
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const uint32_t g = zl[1 + j];
+    XZ[g] = ck_exp_plain(X[g]);
+  }
 }
 #else
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(uint32_t G, const uint8_t* zero, const Fp12* X, Fp12* XZ);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(const uint32_t* zl, const Fp12* X, Fp12* XZ);
 #endif
 #endif
 

@@ -190,7 +190,7 @@ enum Slot {
   S_RC_NAF, S_RC_EV, S_RC_TAB, S_RC_D, S_RC_PINF, S_RC_DEN, S_RC_A, S_PW, S_SLOTW, S_SFULL, S_STFULL, S_INC, S_PB, S_SLOTB,
   S_SEED2, S_SB, S_STB, S_ISOB, S_KMSM_GOFS, S_KMSM_BP, S_KMSM_BT2,
   S_CK_RL, S_CK_HINF, S_CK_ST, S_CK_L2, S_CK_F, S_CK_T0, S_CK_T1, S_CK_T2, S_CK_F2, S_CK_A, S_CK_XZA, S_CK_XZB,
-  S_CK_INV, S_CK_NV, S_CK_NVI, S_CK_SN, S_CK_ZERO, S_COUNT
+  S_CK_INV, S_CK_NV, S_CK_NVI, S_CK_SN, S_CK_ZERO, S_CK_ZL, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -1008,6 +1008,7 @@ struct CkBufs {
   Fp *nv, *nvi;
   CycC* sn;
   uint8_t* zero;
+  uint32_t* zl;  // [0] = count, then the checks with a zero Karabina denominator (k_ck_explain's work list)
 };
 int ck_bufs(CkBufs& b) {
   const size_t G = CK_CHUNK;
@@ -1025,15 +1026,19 @@ int ck_bufs(CkBufs& b) {
   RET(wsT(S_CK_NV, CK_NPOW * G, &b.nv));
   RET(wsT(S_CK_NVI, CK_NPOW * G, &b.nvi));
   RET(wsT(S_CK_SN, CK_NPOW * G, &b.sn));
+  RET(wsT(S_CK_ZL, G + 1, &b.zl));
   return wsT(S_CK_ZERO, G, &b.zero);
 }
 // XZ = X^z (pairing.h cyc_exp_z): the compressed chain, one batch inversion of the 6 G denominators' norms, the
 // decompressed product; the uncompressed chain for the lanes with a zero denominator
+// (the uncompressed chain runs over a device-built work list in CK_EXPLAIN_LANES lanes: it is rare, and a launch of G
+// lanes that mostly return cost ~1 ms at one wave per SIMD)
 int ck_expz(uint32_t G, const Fp12* X, Fp12* XZ, const CkBufs& b, hipStream_t st) {
-  RET(launch("k_ck_expsq", k_ck_expsq, G, 64, st, G, X, b.sn, b.nv, b.zero));
+  HIPCHK(hipMemsetAsync(b.zl, 0, 4, st));
+  RET(launch("k_ck_expsq", k_ck_expsq, G, 64, st, G, X, b.sn, b.nv, b.zero, b.zl));
   RET(batch_inv(CK_NPOW * G, b.nv, b.nvi, st));
   RET(launch("k_ck_expdec", k_ck_expdec, G, 64, st, G, (const CycC*)b.sn, (const Fp*)b.nvi, (const uint8_t*)b.zero, XZ));
-  return launch("k_ck_explain", k_ck_explain, G, 64, st, G, (const uint8_t*)b.zero, X, XZ);
+  return launch("k_ck_explain", k_ck_explain, CK_EXPLAIN_LANES, 64, st, (const uint32_t*)b.zl, X, XZ);
 }
 // out = a * frob^nfrob(b) (conjugated first if conj)
 int ck_mul(uint32_t G, const Fp12* a, const Fp12* b, uint32_t nfrob, uint32_t conj, Fp12* out, hipStream_t st) {
