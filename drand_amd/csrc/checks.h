@@ -314,12 +314,20 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_inv(uint32_t G, const Fp1
   out[g] = ck_inv(F[g], inv[g], nvinv[g]);
 }
 // the six compressed powers sn[i * G + g], their denominators' norms nv[i * G + g], zero[g]
-// (a lane with a zero denominator also appends itself to zl: zl[0] the count, zl[1..] the lanes)
+// (a lane with a zero denominator also appends itself to zl: zl[0] the count, zl[1..] the lanes; x = 1 -- the dead
+// checks, whose verdict k_ck_verdict ignores -- skips the chain: 1^z = 1, zero[g] = 2)
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero,
                                                             uint32_t* zl) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
-  const bool z = ck_expsq(X[g], [&](int i, const CycC& c, const Fp& n) {
+  const Fp12 x = X[g];
+  if (fp12_is_one(x)) {  // 1^z = 1 (a check with no live member or no pair): zero = 2, norms 1 for the batch inversion
+#pragma unroll 1
+    for (int i = 0; i < CK_NPOW; ++i) nv[(size_t)i * G + g] = fp_one();
+    zero[g] = 2;
+    return;
+  }
+  const bool z = ck_expsq(x, [&](int i, const CycC& c, const Fp& n) {
     sn[(size_t)i * G + g] = c;
     nv[(size_t)i * G + g] = n;
   });
@@ -395,7 +403,11 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_mul(uint32_t G, const Fp1
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expdec(uint32_t G, const CycC* sn, const Fp* nvinv, const uint8_t* zero,
                                                     Fp12* XZ) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G || zero[g]) return;
+  if (g >= G || zero[g] == 1) return;
+  if (zero[g] == 2) {  // x = 1 (k_ck_expsq)
+    XZ[g] = fp12_one();
+    return;
+  }
   XZ[g] = ck_expdec([&](int i, CycC& c, Fp& n) {
     c = sn[(size_t)i * G + g];
     n = nvinv[(size_t)i * G + g];
