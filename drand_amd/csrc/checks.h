@@ -235,6 +235,61 @@ DGI bool ck_in_subgroup(const Fp2& x, const Fp2& y, Slot& acc) {
   const Fp2 py = fp2_mul_seq(fp2_conj(y), fp2_const(PSI_CY));
   return fp2_eq(fp2_mul_seq(py, fp2_mul_seq(zz, az)), fp2_neg(acc.y));
 }
+// ---- the G2 sum b = sum rho_i S_i of a group check off the lane's stack (DG_CK_SPLIT, default on): the four-point
+// sign-aligned column form of curve.h jac_msm4_sac (the same recoding: recover.h rs_recode; the same table
+// T[u] = P0 + u1 P1 + u2 P2 + u3 P3), but the 8-entry table is AFFINE, built in three levels of batched affine pair
+// additions (curve.h g2_aff_kind / g2_aff_den / g2_aff_sum: chord, tangent, P + (-P), identity operands -- members
+// may repeat or cancel) into an HBM table, and the column loop adds its entries with mixed additions into an LDS
+// accumulator (g2_madd_lds).  Inside k_ck_prep the Jacobian table lived in scratch (6.1 KB private segment, ~54 GB
+// of scratch traffic per launch at C5).  b's affine form comes from one batch inversion of N(Z) across the chunk.
+// member m of a check (the identity past the live members)
+DGI G2A ck_member(const CkState& c, const G2AStore* S, uint32_t m) {
+  return m < c.nl ? load_g2a(S[c.live[m]]) : G2A{fp2_zero(), fp2_zero(), true};
+}
+// table level l, element e: the operands A (an earlier entry, or P0) and B = P[pb] of the entry dst it writes
+template <class GetT>
+DGI bool ck_tab_operands(uint32_t l, uint32_t e, const CkState& c, const G2AStore* S, GetT getT, G2A& A, G2A& B,
+                         uint32_t& dst) {
+  uint32_t src, pb;
+  if (!rs_level(l, e, src, pb, dst)) return false;
+  A = src ? getT(src) : ck_member(c, S, 0);
+  B = ck_member(c, S, pb);
+  return true;
+}
+// the column loop over the affine table (getT(u) = T[u]), accumulator `acc` (LDS slot on the device)
+template <class GetT, class Slot>
+DGI void ck_sac_g2(const RsDigits& d, GetT getT, Slot& acc) {
+  acc.x = fp2_zero();
+  acc.y = fp2_zero();
+  acc.z = fp2_zero();
+#pragma unroll 1
+  for (int c = 64; c >= 0; --c) {
+    if (c < 64) g2_dbl_lds(acc);
+    uint32_t e;
+    bool pos;
+    if (c == 64) {
+      e = d.top;
+      pos = true;
+    } else {
+      e = (uint32_t)((d.um[0] >> c) & 1u) | (uint32_t)((d.um[1] >> c) & 1u) << 1 | (uint32_t)((d.um[2] >> c) & 1u) << 2;
+      pos = (d.sgn >> c) & 1u;
+    }
+    const G2A t = getT(e);
+    if (!t.inf) g2_madd_lds(acc, t.x, pos ? t.y : fp2_neg(t.y));
+  }
+  if (d.even) {
+    const G2A t = getT(0);
+    if (!t.inf) g2_madd_lds(acc, t.x, fp2_neg(t.y));
+  }
+}
+// affine form of a Jacobian b given ninv = 1 / N(Z) (0 for the identity)
+DGI G2A ck_g2_affine(const G2J& b, const Fp& ninv) {
+  if (fp2_is_zero(b.z)) return G2A{fp2_zero(), fp2_zero(), true};
+  const Fp2 zi = Fp2{fp_mul_seq(b.z.c0, ninv), fp_neg(fp_mul_seq(b.z.c1, ninv))};
+  const Fp2 zi2 = fp2_sqr_seq(zi);
+  return G2A{fp2_mul_seq(b.x, zi2), fp2_mul_seq(b.y, fp2_mul_seq(zi2, zi)), false};
+}
+
 #if defined(__HIP__)
 static_assert(CK_GRP == GRP, "one group per check");
 // H_r = h_eff(Q_r) and its 68 lines (once per Recover call and round): rl[s * R + r]; hinf[r]: H_r is the identity
@@ -267,10 +322,12 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_ck_sub(uint32_t G, uint3
 }
 // the check's members (glist group off + g), as verify_group: subgroup checks (unless k_ck_sub ran: subgroup = 0),
 // the weighted sums (group_combine)
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
-                                                  const uint64_t* seedp, const G1AStore* keys, const uint32_t* item_slot,
-                                                  const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
-                                                  uint32_t subgroup, unsigned long long* cnt, CkState* st) {
+// (g2m != null: the G2 sum of a group is left to k_ck_tab_* / k_ck_sac / k_ck_bfin -- g2m[g] = 1 and dig[g] its
+// column digits -- and so is np)
+template <bool kSplit>
+DGI void ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k, const uint64_t* seedp, const G1AStore* keys,
+                 const uint32_t* item_slot, const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
+                 uint32_t subgroup, unsigned long long* cnt, CkState* st, uint8_t* g2m, RsDigits* dig) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   const uint32_t* mem = glist + 4 + 4 * (size_t)(off + g);
@@ -280,7 +337,8 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep(uint32_t G, uint32_
   G1A a{fp_zero(), fp_zero(), true};
   G2A b{fp2_zero(), fp2_zero(), true};
   CkState c;
-  const uint32_t nl = group_combine(mem, n, *seedp, keys, item_slot, S, status, fin, subgroup, a, b, c.live);
+  uint64_t rho[GRP];
+  const uint32_t nl = group_combine_t<!kSplit>(mem, n, *seedp, keys, item_slot, S, status, fin, subgroup, a, b, c.live, rho);
   c.round = mem[0] / k;
   c.n = n;
   c.nl = nl;
@@ -288,10 +346,33 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep(uint32_t G, uint32_
     a = G1A{fp_zero(), fp_zero(), true};
     b = G2A{fp2_zero(), fp2_zero(), true};
   }
+  const bool later = kSplit && n > 1 && nl > 0;  // b from the table kernels
+  if (kSplit) {
+    g2m[g] = later ? 1 : 0;
+    if (later) {
+      const uint64_t d[4] = {rho[0], rho[1], rho[2], rho[3]};
+      dig[g] = rs_recode(d);
+    }
+  }
   c.np = ((!a.inf && !hinf[c.round]) ? 1u : 0u) | (!b.inf ? 2u : 0u);
   store_g1a(c.a, a);
   store_g2a(c.b, b);
   st[g] = c;
+}
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
+                                                  const uint64_t* seedp, const G1AStore* keys, const uint32_t* item_slot,
+                                                  const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
+                                                  uint32_t subgroup, unsigned long long* cnt, CkState* st,
+                                                  uint8_t* g2m, RsDigits* dig) {
+  ck_prep<true>(G, off, glist, k, seedp, keys, item_slot, hinf, S, status, fin, subgroup, cnt, st, g2m, dig);
+}
+// DG_CK_SPLIT=0 (A/B): the G2 sums in the lane as well (group_combine's Jacobian table in scratch)
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep_g2(uint32_t G, uint32_t off, const uint32_t* glist,
+                                                  uint32_t k, const uint64_t* seedp, const G1AStore* keys,
+                                                  const uint32_t* item_slot, const uint8_t* hinf, const G2AStore* S,
+                                                  uint8_t* status, uint8_t* fin, uint32_t subgroup,
+                                                  unsigned long long* cnt, CkState* st) {
+  ck_prep<false>(G, off, glist, k, seedp, keys, item_slot, hinf, S, status, fin, subgroup, cnt, st, nullptr, nullptr);
 }
 // the lines of the pair (-g1, b): l2[s * G + g]
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2) {
@@ -357,7 +438,13 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_round_lines(uint32_t R, c
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k,
                                                   const uint64_t* seedp, const G1AStore* keys, const uint32_t* item_slot,
                                                   const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
-                                                  uint32_t subgroup, unsigned long long* cnt, CkState* st);
+                                                  uint32_t subgroup, unsigned long long* cnt, CkState* st,
+                                                  uint8_t* g2m, RsDigits* dig);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep_g2(uint32_t G, uint32_t off, const uint32_t* glist,
+                                                  uint32_t k, const uint64_t* seedp, const G1AStore* keys,
+                                                  const uint32_t* item_slot, const uint8_t* hinf, const G2AStore* S,
+                                                  uint8_t* status, uint8_t* fin, uint32_t subgroup,
+                                                  unsigned long long* cnt, CkState* st);
 DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_ck_sub(uint32_t G, uint32_t off, const uint32_t* glist,
                                                                 const G2AStore* S, uint8_t* status, uint8_t* fin);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2);
@@ -421,7 +508,72 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expdec(uint32_t G, const 
 // over the work list zl (k_ck_expsq) with a fixed grid of CK_EXPLAIN_LANES lanes striding it; every lane exits when
 // the list is done
 constexpr uint32_t CK_EXPLAIN_LANES = 4096;
+// the split G2 sums (kernels_check_e.hip): table levels, column loop, affine form.  T4: the affine table entries
+// SoA (entry u of check g at T4 + u * RC_Q * G + g, stride G), tinf[u * G + g] its identity flag.
 #if DG_TU_CHECK == 5
+DGI G2A ck_tab_get(const uint4* T4, const uint8_t* tinf, uint32_t G, uint32_t g, uint32_t u) {
+  G2A t;
+  t.inf = tinf[(size_t)u * G + g] != 0;
+  rc_ld(T4 + (size_t)u * RC_Q * G + g, G, t.x, t.y);
+  return t;
+}
+DGI void ck_tab_put(uint4* T4, uint8_t* tinf, uint32_t G, uint32_t g, uint32_t u, const G2A& t) {
+  tinf[(size_t)u * G + g] = t.inf ? 1 : 0;
+  rc_st(T4 + (size_t)u * RC_Q * G + g, G, t.inf ? fp2_zero() : t.x, t.inf ? fp2_zero() : t.y);
+}
+// lane e G + g: den[lane] = N(d) of element e of level l (1 where nothing is inverted); level 0 also stores T0 = P0
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_tab_den(uint32_t l, uint32_t G, const CkState* st,
+                                                               const uint8_t* g2m, const G2AStore* S, uint4* T4,
+                                                               uint8_t* tinf, Fp* den) {
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= 3 * G) return;
+  const uint32_t g = lane % G, e = lane / G;
+  Fp v = fp_one();
+  G2A A, B;
+  uint32_t dst;
+  if (g2m[g] && ck_tab_operands(l, e, st[g], S, [&](uint32_t u) { return ck_tab_get(T4, tinf, G, g, u); }, A, B, dst)) {
+    if (l == 0 && e == 0) ck_tab_put(T4, tinf, G, g, 0, ck_member(st[g], S, 0));
+    v = g2_aff_den(A, B, g2_aff_kind(A, B));
+  }
+  den[lane] = v;
+}
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_tab_add(uint32_t l, uint32_t G, const CkState* st,
+                                                               const uint8_t* g2m, const G2AStore* S, uint4* T4,
+                                                               uint8_t* tinf, const Fp* dinv) {
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= 3 * G) return;
+  const uint32_t g = lane % G, e = lane / G;
+  G2A A, B;
+  uint32_t dst;
+  if (!g2m[g] || !ck_tab_operands(l, e, st[g], S, [&](uint32_t u) { return ck_tab_get(T4, tinf, G, g, u); }, A, B, dst))
+    return;
+  ck_tab_put(T4, tinf, G, g, dst, g2_aff_sum(A, B, g2_aff_kind(A, B), dinv[lane]));
+}
+// the column loop: bj[g] = b (Jacobian), bn[g] = N(Z) (1 for the lanes not on this path)
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_sac(uint32_t G, const uint8_t* g2m, const RsDigits* dig,
+                                                           const uint4* T4, const uint8_t* tinf, G2JStore* bj, Fp* bn) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ G2JStore s_acc[64];
+  if (g >= G) return;
+  if (!g2m[g]) {
+    bn[g] = fp_one();
+    return;
+  }
+  G2JStore& acc = s_acc[threadIdx.x];
+  ck_sac_g2(dig[g], [&](uint32_t u) { return ck_tab_get(T4, tinf, G, g, u); }, acc);
+  bj[g] = acc;
+  bn[g] = fp2_norm(acc.z);
+}
+// st[g].b = the affine b, and np
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_bfin(uint32_t G, const uint8_t* g2m, const G2JStore* bj,
+                                                            const Fp* bni, const uint8_t* hinf, CkState* st) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G || !g2m[g]) return;
+  const G2A b = ck_g2_affine(load_g2j(bj[g]), bni[g]);
+  store_g2a(st[g].b, b);
+  const G1A a = load_g1a(st[g].a);
+  st[g].np = ((!a.inf && !hinf[st[g].round]) ? 1u : 0u) | (!b.inf ? 2u : 0u);
+}
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(const uint32_t* zl, const Fp12* X, Fp12* XZ) {
   const uint32_t n = zl[0];
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
@@ -430,6 +582,16 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(const uint32_t* z
   }
 }
 #else
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_tab_den(uint32_t l, uint32_t G, const CkState* st,
+                                                               const uint8_t* g2m, const G2AStore* S, uint4* T4,
+                                                               uint8_t* tinf, Fp* den);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_tab_add(uint32_t l, uint32_t G, const CkState* st,
+                                                               const uint8_t* g2m, const G2AStore* S, uint4* T4,
+                                                               uint8_t* tinf, const Fp* dinv);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_sac(uint32_t G, const uint8_t* g2m, const RsDigits* dig,
+                                                           const uint4* T4, const uint8_t* tinf, G2JStore* bj, Fp* bn);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_bfin(uint32_t G, const uint8_t* g2m, const G2JStore* bj,
+                                                            const Fp* bni, const uint8_t* hinf, CkState* st);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(const uint32_t* zl, const Fp12* X, Fp12* XZ);
 #endif
 #endif

@@ -190,7 +190,8 @@ enum Slot {
   S_RC_NAF, S_RC_EV, S_RC_TAB, S_RC_D, S_RC_PINF, S_RC_DEN, S_RC_A, S_PW, S_SLOTW, S_SFULL, S_STFULL, S_INC, S_PB, S_SLOTB,
   S_SEED2, S_SB, S_STB, S_ISOB, S_KMSM_GOFS, S_KMSM_BP, S_KMSM_BT2,
   S_CK_RL, S_CK_HINF, S_CK_ST, S_CK_L2, S_CK_F, S_CK_T0, S_CK_T1, S_CK_T2, S_CK_F2, S_CK_A, S_CK_XZA, S_CK_XZB,
-  S_CK_INV, S_CK_NV, S_CK_NVI, S_CK_SN, S_CK_ZERO, S_CK_ZL, S_COUNT
+  S_CK_INV, S_CK_NV, S_CK_NVI, S_CK_SN, S_CK_ZERO, S_CK_ZL, S_CK_T4, S_CK_TINF, S_CK_DIG, S_CK_TDEN, S_CK_BJ,
+  S_CK_BN, S_CK_G2M, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -1009,7 +1010,18 @@ struct CkBufs {
   CycC* sn;
   uint8_t* zero;
   uint32_t* zl;  // [0] = count, then the checks with a zero Karabina denominator (k_ck_explain's work list)
+  // the split G2 sums (checks.h k_ck_tab_* / k_ck_sac / k_ck_bfin)
+  uint4* T4;
+  uint8_t *tinf, *g2m;
+  RsDigits* dig;
+  Fp *tden, *bn;
+  G2JStore* bj;
 };
+// DG_CK_SPLIT=0 (A/B only): the G2 sums of group checks inside k_ck_prep (group_combine, Jacobian table in scratch)
+bool ck_split() {
+  static const bool v = env_int("DG_CK_SPLIT", 1) != 0;
+  return v;
+}
 int ck_bufs(CkBufs& b) {
   const size_t G = CK_CHUNK;
   RET(wsT(S_CK_ST, G, &b.st));
@@ -1027,6 +1039,15 @@ int ck_bufs(CkBufs& b) {
   RET(wsT(S_CK_NVI, CK_NPOW * G, &b.nvi));
   RET(wsT(S_CK_SN, CK_NPOW * G, &b.sn));
   RET(wsT(S_CK_ZL, G + 1, &b.zl));
+  if (ck_split()) {
+    RET(wsT(S_CK_T4, 8 * RC_Q * G, &b.T4));
+    RET(wsT(S_CK_TINF, 8 * G, &b.tinf));
+    RET(wsT(S_CK_DIG, G, &b.dig));
+    RET(wsT(S_CK_TDEN, 6 * G, &b.tden));
+    RET(wsT(S_CK_BJ, G, &b.bj));
+    RET(wsT(S_CK_BN, 2 * G, &b.bn));
+    RET(wsT(S_CK_G2M, G, &b.g2m));
+  }
   return wsT(S_CK_ZERO, G, &b.zero);
 }
 // XZ = X^z (pairing.h cyc_exp_z): the compressed chain, one batch inversion of the 6 G denominators' norms, the
@@ -1052,8 +1073,28 @@ int check_chunk(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k, uin
   static const bool sub_inline = getenv("DG_CK_SUB_INLINE") != nullptr;  // A/B: subgroup checks inside k_ck_prep
   if (subgroup && !sub_inline)
     RET(launch("k_ck_sub", k_ck_sub, 4 * G, 64, st, G, off, glist, (const G2AStore*)S, status, fin));
-  RET(launch("k_ck_prep", k_ck_prep, G, 64, st, G, off, glist, k, seed, keys, item_slot, hinf, S, status, fin,
-             sub_inline ? subgroup : 0u, g_ctx.gcount, b.st));
+  const bool split = ck_split();
+  if (split)
+    RET(launch("k_ck_prep", k_ck_prep, G, 64, st, G, off, glist, k, seed, keys, item_slot, hinf, S, status, fin,
+               sub_inline ? subgroup : 0u, g_ctx.gcount, b.st, b.g2m, b.dig));
+  else
+    RET(launch("k_ck_prep", k_ck_prep_g2, G, 64, st, G, off, glist, k, seed, keys, item_slot, hinf, S, status, fin,
+               sub_inline ? subgroup : 0u, g_ctx.gcount, b.st));
+  if (split) {
+    Fp *den = b.tden, *dinv = b.tden + 3 * (size_t)G;
+    for (uint32_t l = 0; l < 3; ++l) {
+      RET(launch("k_ck_tab_den", k_ck_tab_den, 3 * G, 64, st, l, G, (const CkState*)b.st, (const uint8_t*)b.g2m,
+                 S, b.T4, b.tinf, den));
+      RET(batch_inv(3 * G, den, dinv, st));
+      RET(launch("k_ck_tab_add", k_ck_tab_add, 3 * G, 64, st, l, G, (const CkState*)b.st, (const uint8_t*)b.g2m,
+                 S, b.T4, b.tinf, (const Fp*)dinv));
+    }
+    RET(launch("k_ck_sac", k_ck_sac, G, 64, st, G, (const uint8_t*)b.g2m, (const RsDigits*)b.dig, (const uint4*)b.T4,
+               (const uint8_t*)b.tinf, b.bj, b.bn));
+    RET(batch_inv(G, b.bn, b.bn + G, st));
+    RET(launch("k_ck_bfin", k_ck_bfin, G, 64, st, G, (const uint8_t*)b.g2m, (const G2JStore*)b.bj,
+               (const Fp*)(b.bn + G), hinf, b.st));
+  }
   RET(launch("k_ck_lines2", k_ck_lines2, G, 64, st, G, (const CkState*)b.st, b.l2));
   RET(launch("k_ck_miller", k_ck_miller, G, 64, st, G, R, (const CkState*)b.st, rl, (const CkLine*)b.l2, b.F));
   // easy part: f1 = f^-1 conj(f), f2 = f1 frob^2(f1)

@@ -511,9 +511,12 @@ DGN void verify_item(size_t i, uint32_t k, const G1AStore* keys, const uint32_t*
 
 // the members' weighted sums a = sum rho_i X_i, b = sum rho_i S_i; members failing the subgroup check are
 // decided here (decode error) and left out.  Returns the live members (their item indices in live[]).
-DGN uint32_t group_combine(const uint32_t* mem, uint32_t n, uint64_t seed, const G1AStore* keys,
-                           const uint32_t* item_slot, const G2AStore* S, uint8_t* status, uint8_t* fin,
-                           uint32_t subgroup, G1A& a, G2A& b, uint32_t* live) {
+// With g2 = false (Recover's pipeline, checks.h) the G2 sum b is left to the table kernels (k_ck_tab_*, k_ck_sac),
+// except for a single share (b = its sigma); rho[] receives the live members' coefficients.
+template <bool g2>
+DGN uint32_t group_combine_t(const uint32_t* mem, uint32_t n, uint64_t seed, const G1AStore* keys,
+                             const uint32_t* item_slot, const G2AStore* S, uint8_t* status, uint8_t* fin,
+                             uint32_t subgroup, G1A& a, G2A& b, uint32_t* live, uint64_t* rho_out) {
   G1J xp[GRP];
   G2J sp[GRP];
   uint64_t rho[GRP];
@@ -535,20 +538,27 @@ DGN uint32_t group_combine(const uint32_t* mem, uint32_t n, uint64_t seed, const
       return 1;
     }
     xp[nl] = jac_from_aff(load_g1a(keys[item_slot ? item_slot[i] : 0u]));
-    sp[nl] = jac_from_aff(s);
+    if (g2) sp[nl] = jac_from_aff(s);
     rho[nl] = rlc_coeff(seed ^ GROUP_TAG, i);
     live[nl++] = i;
   }
   for (uint32_t m = nl; m < GRP; ++m) {
     xp[m] = jac_infinity<Fp>();
-    sp[m] = jac_infinity<Fp2>();
+    if (g2) sp[m] = jac_infinity<Fp2>();
     rho[m] = 0;
   }
+  if (rho_out)
+    for (uint32_t m = 0; m < GRP; ++m) rho_out[m] = rho[m];
   if (nl) {
     a = g1_to_aff(jac_msm4_sac(xp, rho));
-    b = g2_to_aff(jac_msm4_sac(sp, rho));
+    if (g2) b = g2_to_aff(jac_msm4_sac(sp, rho));
   }
   return nl;
+}
+DGI uint32_t group_combine(const uint32_t* mem, uint32_t n, uint64_t seed, const G1AStore* keys,
+                           const uint32_t* item_slot, const G2AStore* S, uint8_t* status, uint8_t* fin,
+                           uint32_t subgroup, G1A& a, G2A& b, uint32_t* live, uint64_t* rho_out = nullptr) {
+  return group_combine_t<true>(mem, n, seed, keys, item_slot, S, status, fin, subgroup, a, b, live, rho_out);
 }
 DGN void verify_group(const uint32_t* mem, uint32_t n, uint32_t k, uint64_t seed, const G1AStore* keys,
                       const uint32_t* item_slot, const G2AStore* H, const G2AStore* S, uint8_t* status,

@@ -244,6 +244,50 @@ extern "C" int hc_ck_subgroup_check(const uint8_t* in96) {
   return x != y ? 2 : (x ? 1 : 0);
 }
 
+// checks.h's split G2 sum of a group check (k_ck_tab_den / k_ck_tab_add levels with exact inverses, k_ck_sac's column
+// loop, k_ck_bfin's affine form) against group_combine's g2_to_aff(jac_msm4_sac(...)).  sigs: 4 compressed G2 points
+// (any may repeat, cancel or be the identity), rho: 4 coefficients, nl live members (rho and points past nl unused).
+// 1 if equal.
+extern "C" int hc_ck_g2_split_check(const uint8_t* sigs384, const uint64_t* rho_in, uint32_t nl) {
+  G2AStore S[4];
+  CkState c{};
+  c.nl = nl;
+  G2J sp[4];
+  uint64_t rho[4];
+  for (uint32_t m = 0; m < 4; ++m) {
+    G2A a;
+    if (!g2_decompress(a, sigs384 + 96 * m, false)) return -1;
+    store_g2a(S[m], a);
+    c.live[m] = m;
+    sp[m] = m < nl ? jac_from_aff(a) : jac_infinity<Fp2>();
+    rho[m] = m < nl ? rho_in[m] : 0;
+  }
+  G2A T[8];
+  for (auto& t : T) t = G2A{fp2_zero(), fp2_zero(), true};
+  auto getT = [&](uint32_t u) { return T[u]; };
+  for (uint32_t l = 0; l < 3; ++l) {
+    G2A out[3];
+    uint32_t dsts[3];
+    bool on[3] = {false, false, false};
+    for (uint32_t e = 0; e < 3; ++e) {
+      G2A A, B;
+      if (!ck_tab_operands(l, e, c, S, getT, A, B, dsts[e])) continue;
+      if (l == 0 && e == 0) T[0] = ck_member(c, S, 0);
+      const uint32_t kind = g2_aff_kind(A, B);
+      out[e] = g2_aff_sum(A, B, kind, fp_inv(g2_aff_den(A, B, kind)));
+      on[e] = true;
+    }
+    for (uint32_t e = 0; e < 3; ++e)
+      if (on[e]) T[dsts[e]] = out[e];
+  }
+  G2J acc;
+  ck_sac_g2(rs_recode(rho), getT, acc);
+  const G2A b = ck_g2_affine(acc, fp2_is_zero(acc.z) ? fp_zero() : fp_inv(fp2_norm(acc.z)));
+  const G2A want = g2_to_aff(jac_msm4_sac(sp, rho));
+  if (b.inf != want.inf) return 0;
+  return b.inf || (fp2_eq(b.x, want.x) && fp2_eq(b.y, want.y)) ? 1 : 0;
+}
+
 // [k]P with the accumulator as a memory slot (curve.h g2_mul_u256_psi_lds, LDS on the device) against the
 // register form; 1 if equal
 extern "C" int hc_g2_mul_lds_check(const uint8_t* sig96, const uint32_t* k8) {

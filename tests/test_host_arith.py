@@ -226,6 +226,27 @@ def test_ck_subgroup_matches_curve_check(hc):
     assert seen[0] >= 20, seen
 
 
+def test_ck_split_g2_sum_matches_group_combine(hc):
+    """checks.h's G2 group sum off the stack (affine 8-entry table in three batched levels, column loop with an LDS-style
+    accumulator, batched affine form) equals group_combine's jac_msm4_sac: distinct members, a repeated member (the
+    index_rewritten corruption), a member and its negation, the identity, 1..4 live members, edge coefficients."""
+    c = load("chain_t3n5.json")
+    sigs = [hx(r["sig"]) for r in c["rounds"][:8]]
+    neg = lambda s: bytes([s[0] ^ 0x20]) + s[1:]
+    ident = bytes([0xc0]) + bytes(95)
+    rng = random.Random(5)
+    groups = [sigs[0:4], sigs[4:8], [sigs[0], sigs[0], sigs[1], sigs[2]], [sigs[0], neg(sigs[0]), sigs[3], sigs[3]],
+              [ident, sigs[1], sigs[2], sigs[3]], [sigs[5], ident, ident, neg(sigs[5])]]
+    rhos = [[rng.getrandbits(64) | 1 for _ in range(4)] for _ in range(3)]
+    rhos += [[1, 1, 1, 1], [(1 << 64) - 1, 1 << 63, 3, (1 << 64) - 1], [2, 4, 6, 8]]
+    for g in groups:
+        buf = b"".join(g)
+        for rho in rhos:
+            arr = (ctypes.c_uint64 * 4)(*rho)
+            for nl in (1, 2, 3, 4):
+                assert hc.hc_ck_g2_split_check(buf, arr, nl) == 1, (g.index if False else groups.index(g), rho, nl)
+
+
 def test_wnaf_digits_host_build(hc):
     """recover.h rc_wnaf: width-5 signed digits (odd, |d| <= 15, >= 5 apart) that evaluate back to the scalar,
     including the 65th position a carry can reach."""
