@@ -687,8 +687,41 @@ __device__ __noinline__ Fp2 fp2_sqr_r(DG_P12(a), DG_P12(b));
 DGI Fp2 fp2_mul(const Fp2& a, const Fp2& b) { return fp2_mul_r(DG_A12(a.c0), DG_A12(a.c1), DG_A12(b.c0), DG_A12(b.c1)); }
 DGI Fp2 fp2_sqr(const Fp2& a) { return fp2_sqr_r(DG_A12(a.c0), DG_A12(a.c1)); }
 #else
+// DG_FP_PIN2=1 (with DG_FP_CALL=3; the one-wave pipeline kernels): the pins at the Fp2 level instead -- operands
+// pinned before the Karatsuba triple, results after -- so its three independent Fp products may interleave (three
+// times the independent work per wave, where the 512-entry register file has room for it)
+#ifndef DG_FP_PIN2
+#define DG_FP_PIN2 0
+#endif
+#if DG_FP_PIN2 && DG_FP_CALL == 3 && defined(__HIP_DEVICE_COMPILE__)
+DGI Fp fp_mul_np(const Fp& a, const Fp& b) {
+  uint32_t x[14], y[14], d[14];
+  fp28_unpack(a.l, x);
+  fp28_unpack(b.l, y);
+  fp28_sos_mul_d(x, y, d);
+  Fp r;
+  fp28_pack(d, r.l);
+  return fp_reduce_once(r);
+}
+#define DG_FP2_PINNED 1
+#else
+#define DG_FP2_PINNED 0
+#endif
 DGH Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
-#if DG_FP2_LAZY && !(defined(__HIP_DEVICE_COMPILE__) && DG_FP_CALL == 1)
+#if DG_FP2_PINNED
+  Fp2 x = a, y = b;
+  DG_PIN_FP12(x.c0);
+  DG_PIN_FP12(x.c1);
+  DG_PIN_FP12(y.c0);
+  DG_PIN_FP12(y.c1);
+  const Fp t0 = fp_mul_np(x.c0, y.c0);
+  const Fp t1 = fp_mul_np(x.c1, y.c1);
+  const Fp t2 = fp_mul_np(fp_add(x.c0, x.c1), fp_add(y.c0, y.c1));
+  Fp2 r{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+  DG_PIN_FP12(r.c0);
+  DG_PIN_FP12(r.c1);
+  return r;
+#elif DG_FP2_LAZY && !(defined(__HIP_DEVICE_COMPILE__) && DG_FP_CALL == 1)
   return fp2_mul_lazy(a, b);
 #else
   Fp t0 = fp_mul(a.c0, b.c0);
@@ -698,8 +731,19 @@ DGH Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
 #endif
 }
 DGH Fp2 fp2_sqr(const Fp2& a) {
+#if DG_FP2_PINNED
+  Fp2 x = a;
+  DG_PIN_FP12(x.c0);
+  DG_PIN_FP12(x.c1);
+  const Fp m = fp_mul_np(x.c0, x.c1);
+  Fp2 r{fp_mul_np(fp_add(x.c0, x.c1), fp_sub(x.c0, x.c1)), fp_dbl(m)};
+  DG_PIN_FP12(r.c0);
+  DG_PIN_FP12(r.c1);
+  return r;
+#else
   Fp m = fp_mul(a.c0, a.c1);
   return Fp2{fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(m)};
+#endif
 }
 #endif
 // Fp2 products as one out-of-line call each, operands and result in VGPRs (48 / 24 scalar arguments, the
