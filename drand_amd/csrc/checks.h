@@ -41,6 +41,10 @@ namespace dg {
 #ifndef DG_CK_WAVES2
 #define DG_CK_WAVES2 2
 #endif
+// ... of k_ck_lines2 / k_ck_round_lines (a G2 point and one line live)
+#ifndef DG_CK_L2_WAVES
+#define DG_CK_L2_WAVES 1
+#endif
 // ... of k_ck_sub (its accumulator in LDS: 18 KB per 64-lane workgroup, so at most 2 per SIMD anyway)
 #ifndef DG_CK_SUB_WAVES
 #define DG_CK_SUB_WAVES 2
@@ -375,7 +379,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep_g2(uint32_t G, uint
   ck_prep<false>(G, off, glist, k, seedp, keys, item_slot, hinf, S, status, fin, subgroup, cnt, st, nullptr, nullptr);
 }
 // the lines of the pair (-g1, b): l2[s * G + g]
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_L2_WAVES) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G || !(st[g].np & 2)) return;
   const G2A b = load_g2a(st[g].b);
@@ -447,7 +451,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep_g2(uint32_t G, uint
                                                   unsigned long long* cnt, CkState* st);
 DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_ck_sub(uint32_t G, uint32_t off, const uint32_t* glist,
                                                                 const G2AStore* S, uint8_t* status, uint8_t* fin);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2);
+DG_KERNEL void __launch_bounds__(64, DG_CK_L2_WAVES) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_inv(uint32_t G, const Fp12* F, const CkInv* inv, const Fp* nvinv,
                                                  Fp12* out);

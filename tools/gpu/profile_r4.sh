@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 profiles: rocprofv3 --kernel-trace --stats of the headline (overlapped and --sync), of Recover at C3
 # (100k rounds, n=64) and of the adversarial Recover at C5 (10k rounds, n=256, 10% corrupted); then PMC passes,
-# each counter group its own run and config: HBM-side bytes (FETCH_SIZE, WRITE_SIZE), VALU instruction counts and
+# each counter group its own run and config (CONFIGS, default "head c3 c5"): HBM-side bytes (FETCH_SIZE, WRITE_SIZE), VALU instruction counts and
 # wave cycles (SQ_*), GRBM_GUI_ACTIVE (the clock).  Stops at the first failure.  PASSES=stats|pmc|all (default all)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -22,10 +22,15 @@ run() {  # name limit args...
   timeout -k 10 $lim rocprofv3 "$@" > $O/$name.log 2>&1 || { echo "$name failed"; tail -20 $O/$name.log; exit 1; }
 }
 if [ "$P" = all ] || [ "$P" = stats ]; then
+for cfg in ${CONFIGS:-head c3 c5}; do case $cfg in
+head)
 run stats_async 300 --kernel-trace --stats --output-format csv -d $O/stats_async -o run -- python3 $R/bench.py $HEAD --steps 20
-run stats_sync 300 --kernel-trace --stats --output-format csv -d $O/stats_sync -o run -- python3 $R/bench.py $HEAD --sync --steps 10
-run stats_c3 300 --kernel-trace --stats --output-format csv -d $O/stats_c3 -o run -- python3 $R/bench.py $C3
-run stats_c5 300 --kernel-trace --stats --output-format csv -d $O/stats_c5 -o run -- python3 $R/bench.py $C5
+run stats_sync 300 --kernel-trace --stats --output-format csv -d $O/stats_sync -o run -- python3 $R/bench.py $HEAD --sync --steps 10;;
+c3)
+run stats_c3 300 --kernel-trace --stats --output-format csv -d $O/stats_c3 -o run -- python3 $R/bench.py $C3;;
+c5)
+run stats_c5 300 --kernel-trace --stats --output-format csv -d $O/stats_c5 -o run -- python3 $R/bench.py $C5;;
+esac; done
 fi
 if [ "$P" = all ] || [ "$P" = pmc ]; then
 pmc() {  # tag counters config-name config-args
@@ -34,7 +39,7 @@ pmc() {  # tag counters config-name config-args
   echo "[profile] pmc $cfg $tag" >&2
   timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d $O/pmc_${cfg}_$tag -o run -- python3 $R/bench.py "$@" > $O/pmc_${cfg}_$tag.log 2>&1 || { echo "pmc $cfg $tag failed"; tail -5 $O/pmc_${cfg}_$tag.log; exit 1; }
 }
-for cfg in head c3 c5; do
+for cfg in ${CONFIGS:-head c3 c5}; do
   case $cfg in head) A="$HEAD --sync --steps 1 --warmup 1";; c3) A="$C3";; c5) A="$C5";; esac
   pmc FETCH_SIZE FETCH_SIZE $cfg $A
   pmc WRITE_SIZE WRITE_SIZE $cfg $A
