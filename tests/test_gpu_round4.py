@@ -8,7 +8,11 @@ statuses, every share status; bit-exact):
   block, a NOT_ENOUGH round inside an otherwise uniform block: the ub / nl block lists of recover_tail);
 - the exact per-item mode (DG_GROUP=1: every examined share gets its own pairing check, no group tests) at a C5
   shape (n = 256, t = 129, 30% corrupted) in a child process;
-- the HBM-resident VerifyPartial + Recover-from-verdicts pair that bench.py times as configs[2]."""
+- the HBM-resident VerifyPartial + Recover-from-verdicts pair that bench.py times as configs[2];
+- the per-item pass in its A/B forms (child processes: the G2 group sums inside k_ck_prep, DG_CK_SPLIT=0; the
+  subgroup checks inside k_ck_prep, DG_CK_SUB_INLINE=1; the per-item kernels on the batch's own stream or on the
+  dedicated one, DG_SHARED_FB=1 / 0) with repeated and cancelling members inside group tests;
+- asynchronous beacon batches consumed on the batch's own stream (dg_last_batch_stream)."""
 import hashlib
 import json
 import os
@@ -21,7 +25,7 @@ import pytest
 from drand_amd import _lib as L
 from drand_amd import tbls
 from oracle import twin
-from tests.fixtures import group
+from tests.fixtures import chain, chain_arrays, group, hx
 from tools import corrupt as C
 from tools import synthetic as S
 
@@ -187,3 +191,102 @@ def test_wrong_length_placeholder_is_skipped():
     assert not rs.any() and ss[1, 2] == L.ST_SIG_DECODE and ss[1, t] == 0
     for r in range(R):
         assert bytes(sigs[r]) == twin.sign(coeffs[0], msgs[r])
+
+
+_FORM_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from drand_amd import _lib as L
+from drand_amd import tbls
+z = np.load(sys.argv[2])
+commits = [bytes(c) for c in z["commits"]]
+sigs, rs, ss = tbls.recover_batch(tbls.PubPoly(commits), z["msgs"], z["parts"], int(z["t"]), int(z["n"]), seed=36)
+np.savez(sys.argv[3], sigs=sigs, rs=rs, ss=ss)
+"""
+
+
+def test_pipeline_forms_with_repeated_and_cancelling_members(tmp_path):
+    """n = 256, t = 129, 8 rounds, 15% corrupted, plus members that repeat (a partial copied whole over its neighbour:
+    the same sigma twice in one group test -- the affine table's tangent case) and cancel (a neighbour's sigma
+    negated: P + (-P) = O in the table) inside the examined prefix.  The default library and child processes with
+    the A/B forms of the per-item pass all give the twin's signatures and statuses."""
+    t, n, R = 129, 256, 8
+    coeffs, commits, shares = group(t, n)
+    msgs = [hashlib.sha256(b"forms/%d" % r).digest() for r in range(R)]
+    parts = tbls.sign_batch([v for _ in range(R) for _, v in shares], [m for m in msgs for _ in range(n)],
+                            [i for _ in range(R) for i, _ in shares]).reshape(R, n, 98)
+
+    def resign(reqs):
+        return tbls.sign_batch([(shares[i][1] + ds) % S.R for (r, i, ds, dr) in reqs],
+                               [msgs[(r + dr) % R] if dr else msgs[r] for (r, i, ds, dr) in reqs])
+
+    C.corrupt_batch(parts, C.pick(R, n, 0.15, seed=b"forms"), n, resign)
+    for r in range(R):
+        j = 8 + 12 * r
+        parts[r, j] = parts[r, j + 1]                # the same partial twice (index included)
+        parts[r, j + 4] = parts[r, j + 5]
+        parts[r, j + 4, 2] ^= 0x20                   # ... and a neighbour's sigma negated (index j + 5)
+    tw = _twin(commits, t, n, msgs, parts)
+    assert (tw[2] == L.ST_BAD_SIG).any()
+    _equal(tbls.recover_batch(tbls.PubPoly(commits), msgs, parts, t, n, seed=36), tw)
+    inp = tmp_path / "in.npz"
+    np.savez(inp, commits=np.array([list(c) for c in commits], np.uint8), msgs=np.array([list(m) for m in msgs],
+             np.uint8), parts=parts, t=t, n=n)
+    for k, (var, val) in enumerate([("DG_CK_SPLIT", "0"), ("DG_CK_SUB_INLINE", "1"), ("DG_SHARED_FB", "1"),
+                                    ("DG_SHARED_FB", "0")]):
+        out = tmp_path / ("out%d.npz" % k)
+        r = subprocess.run([sys.executable, "-c", _FORM_CHILD, ROOT, str(inp), str(out)],
+                           env=dict(os.environ, **{var: val}), capture_output=True, text=True, timeout=300, cwd=ROOT)
+        assert r.returncode == 0, (var, r.stderr[-2000:])
+        z = np.load(out)
+        _equal((z["sigs"], z["rs"], z["ss"]), tw)
+
+
+def test_async_batches_consumed_on_the_batch_stream():
+    """dg_verify_beacons_dev_async without a done stream, its statuses packed on dg_last_batch_stream()'s stream
+    (bench.py's arrangement at N = 1): four overlapped batches of the committed chain, one of them corrupted, equal
+    the blocking entry point's statuses and the twin's."""
+    import ctypes
+
+    import torch
+
+    from drand_amd import shard
+
+    c = chain()
+    pr, rr, ps, sigs, msgs = chain_arrays(c)
+    pk = hx(c["pk"])
+    bad = sigs.copy()
+    bad[3] = sigs[4]
+    bad[7, 0] ^= 0x20
+    want = [twin.verify(pk, bytes(msgs[i]), bytes(bad[i])) for i in range(len(rr))]
+    assert tbls.verify_beacons(pk, pr, rr, ps, bad, seed=37).tolist() == want
+    dev = torch.device("cuda", 0)
+    p_, r_, psb, off = tbls._beacon_arrays(pr, rr, ps)
+    d_pr = torch.from_numpy(p_.astype(np.int64)).to(dev)
+    d_r = torch.from_numpy(r_.astype(np.int64)).to(dev)
+    d_ps = torch.from_numpy(psb).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int32)).to(dev)
+    n = len(rr)
+    lib = L.lib()
+    outs = []
+    for k in range(4):
+        d_sig = torch.from_numpy(np.ascontiguousarray(bad if k == 2 else sigs)).to(dev)
+        d_st = torch.full((n,), 99, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        L.check(lib.dg_verify_beacons_dev_async(L.ptr(pk), n, L.ptr(d_pr), L.ptr(d_r), L.ptr(d_ps), L.ptr(d_off),
+                                                L.ptr(d_sig), L.ptr(d_st), 40 + k, None, None))
+        sp = ctypes.c_void_p()
+        L.check(lib.dg_last_batch_stream(ctypes.byref(sp)))
+        gs = torch.cuda.ExternalStream(sp.value, device=dev)
+        with torch.cuda.stream(gs):
+            bits = shard.pack_bits(d_st)
+            st_copy = d_st.clone()
+        outs.append((k, bits, st_copy, d_sig, d_st))  # (the batch writes d_sig's statuses into d_st until done)
+    L.check(lib.dg_wait_all())
+    torch.cuda.synchronize()
+    for k, bits, st_copy, _, _ in outs:
+        got = st_copy.cpu().numpy()
+        exp = np.array(want if k == 2 else [0] * n, np.uint8)
+        assert np.array_equal(got, exp), k
+        assert np.array_equal(bits.cpu().numpy(), np.packbits(exp != 0, bitorder="little")), k
