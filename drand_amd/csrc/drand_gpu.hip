@@ -191,7 +191,7 @@ enum Slot {
   S_SEED2, S_SB, S_STB, S_ISOB, S_KMSM_GOFS, S_KMSM_BP, S_KMSM_BT2,
   S_CK_RL, S_CK_HINF, S_CK_ST, S_CK_L2, S_CK_F, S_CK_T0, S_CK_T1, S_CK_T2, S_CK_F2, S_CK_A, S_CK_XZA, S_CK_XZB,
   S_CK_INV, S_CK_NV, S_CK_NVI, S_CK_SN, S_CK_ZERO, S_CK_ZL, S_CK_T4, S_CK_TINF, S_CK_DIG, S_CK_TDEN, S_CK_BJ,
-  S_CK_BN, S_CK_G2M, S_COUNT
+  S_CK_BN, S_CK_G2M, S_KOK, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -1997,6 +1997,17 @@ int dg_recover_dev(const uint8_t* commits48, uint32_t t, uint32_t nshares, size_
   return recover_tail(R, k, t, d_partials98, d_st, d_S, d_out_sig96, d_round_status, d_share_status, st);
 }
 
+// sigma of every partial decoded by the phase kernels, then the known verdicts carried over (k_merge_verified)
+static int decode_verified(uint32_t N, const uint8_t* d_p, const uint8_t* d_vst, G2AStore* d_S, uint8_t* d_st,
+                           hipStream_t st) {
+  uint8_t *kok, *iso;
+  RET(wsT(S_KOK, 16, &kok));
+  RET(wsT(S_ISO, N, &iso));
+  HIPCHK(hipMemsetAsync(kok, 0, 16, st));  // one "key" with an OK status: no key side on this path
+  RET(decode_items(N, 1, 0, d_p, 98, 2, nullptr, kok, d_S, d_st, nullptr, iso, 0u, st));
+  return launch("k_merge_verified", k_merge_verified, N, 128, st, N, d_vst, d_S, d_st);
+}
+
 int dg_recover_verified(uint32_t t, uint32_t nshares, size_t rounds, uint32_t k, const uint8_t* partials98,
                         const uint8_t* verified_status, uint8_t* out_sig96, uint8_t* round_status,
                         uint8_t* share_status) {
@@ -2017,8 +2028,7 @@ int dg_recover_verified(uint32_t t, uint32_t nshares, size_t rounds, uint32_t k,
   RET(upload(S_VST, verified_status, N, &d_vst, st));
   RET(wsT(S_STATUS, N, &d_st));
   RET(wsT(S_S, N, &d_S));
-  RET(launch("k_decode_verified", k_decode_verified, (uint32_t)N, 128, st, (uint32_t)N, (const uint8_t*)d_p,
-             (const uint8_t*)d_vst, d_S, d_st));
+  RET(decode_verified((uint32_t)N, d_p, d_vst, d_S, d_st, st));
   return recover_tail(R, k, t, d_p, d_st, d_S, out_sig96, round_status, share_status, st);
 }
 
@@ -2040,8 +2050,7 @@ int dg_recover_verified_dev(uint32_t t, uint32_t nshares, size_t rounds, uint32_
   G2AStore* d_S;
   RET(wsT(S_STATUS, N, &d_st));
   RET(wsT(S_S, N, &d_S));
-  RET(launch("k_decode_verified", k_decode_verified, (uint32_t)N, 128, st, (uint32_t)N, d_partials98, d_verified_status,
-             d_S, d_st));
+  RET(decode_verified((uint32_t)N, d_partials98, d_verified_status, d_S, d_st, st));
   return recover_tail(R, k, t, d_partials98, d_st, d_S, d_out_sig96, d_round_status, d_share_status, st);
 }
 
