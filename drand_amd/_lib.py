@@ -49,6 +49,7 @@ SIGNATURES = {
     "dg_verify_beacons_dev": ([_P, _SZ, _P, _P, _P, _P, _P, _P, _U64, _P], _I),
     "dg_verify_beacons_dev_async": ([_P, _SZ, _P, _P, _P, _P, _P, _P, _U64, _P, _P], _I),
     "dg_wait_all": ([], _I),
+    "dg_queue_plan": ([_I, _P, _P], _I),
     "dg_last_batch_stream": ([_P], _I),
     "dg_last_batch_flags": ([_P], _I),
     "dg_fallback_count": ([_P], _I),

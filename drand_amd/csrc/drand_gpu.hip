@@ -35,24 +35,43 @@ struct Timing {
 #ifndef DG_MAX_SETS
 #define DG_MAX_SETS 12
 #endif
-constexpr int kSets = DG_MAX_SETS;  // capacity; DG_SETS (environment) sets are used, by default:
-// 10 with 12 or more hardware queues (GPU_MAX_HW_QUEUES); with fewer, a multiple of the queue count (8 at HIP's default
-// 4).  HIP binds streams to queues as they first dispatch (1, 2, 3, 4, 4, 3, 2, 1, 4, 3, ... on the box), and a queue
-// runs its streams' kernels one after another, so 10 sets on 4 queues put 3 batches in 10 on two queues and 2 on the
-// others: the two busy queues set the pace (trace: 94-97% busy against 59-65%).  Headline at 4 queues: 10 sets
-// 11.2 M rounds/s, 8 sets 12.0 M, 12 sets 12.0 M, 4 sets 11.8 M.
+constexpr int kSets = DG_MAX_SETS;  // capacity; DG_SETS (environment) overrides the plan below
+// The workspace plan for a hardware queue count (GPU_MAX_HW_QUEUES; HIP's default 4).  HIP binds streams to queues as
+// they first dispatch (1, 2, 3, 4, 4, 3, 2, 1, 4, 3, ... on the box), a queue runs its streams' kernels one after
+// another, and a cross-stream wait queued on a shared queue stalls every stream behind it:
+//   >= 12 queues: 10 sets, the per-item kernels on their own stream (its queue alone reserves their ~15 KB scratch);
+//   5..11 queues: queues - 2 sets and the per-item stream, so no two library streams share a queue (the caller keeps
+//                 one); the per-item kernels cannot go on the set streams here -- every queue would reserve their
+//                 scratch, and 8 such queues failed dg_init with HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+//   <= 4 queues:  a multiple of the queue count (8 at 4), each queue carrying the same share of batches, and the
+//                 per-item kernels on each set's own stream (no hand-over barriers; 4 queues reserve their scratch
+//                 fine).  Headline at 4 queues: 10 sets with the hop 8.7 M rounds/s, without it 11.1 M, 8 sets 12.0 M.
+void queue_plan(int hwq, int* sets, int* shared_fb) {
+  if (hwq < 1) hwq = 4;
+  int v;
+  if (hwq >= 12)
+    v = 10;
+  else if (hwq > 4)
+    v = hwq - 2;
+  else
+    v = (10 / hwq) * hwq;
+  v = v < 1 ? 1 : (v > kSets ? kSets : v);
+  *sets = v;
+  *shared_fb = hwq <= 4 && hwq < v + 2 ? 1 : 0;
+}
+int env_hw_queues() {
+  const char* q = getenv("GPU_MAX_HW_QUEUES");
+  return q && atoi(q) > 0 ? atoi(q) : 4;
+}
 int active_sets() {
   static const int n = [] {
-    const char* e = getenv("DG_SETS");
-    int v;
-    if (e) {
-      v = atoi(e);
-    } else {
-      const char* q = getenv("GPU_MAX_HW_QUEUES");
-      const int hwq = q && atoi(q) > 0 ? atoi(q) : 4;
-      v = hwq >= 12 ? 10 : (hwq >= 10 ? hwq : (10 / hwq) * hwq);
+    if (const char* e = getenv("DG_SETS")) {
+      const int v = atoi(e);
+      return v < 1 ? 1 : (v > kSets ? kSets : v);
     }
-    return v < 1 ? 1 : (v > kSets ? kSets : v);
+    int sets, shared;
+    queue_plan(env_hw_queues(), &sets, &shared);
+    return sets;
   }();
   return n;
 }
@@ -1464,8 +1483,10 @@ int dg_init(int device) {
   if (const char* e = getenv("DG_SHARED_FB")) {
     g_ctx.shared_fb = atoi(e) != 0;
   } else {
-    const int hwq = env_int("GPU_MAX_HW_QUEUES", 4);
-    g_ctx.shared_fb = hwq < active_sets() + 2;
+    const int hwq = env_hw_queues();
+    int sets, shared;
+    queue_plan(hwq, &sets, &shared);
+    g_ctx.shared_fb = shared != 0 && hwq < active_sets() + 2;  // (DG_SETS may leave every stream its own queue)
   }
   hipFuncAttributes fa_items{}, fa_groups{};
   HIPCHK(hipFuncGetAttributes(&fa_items, reinterpret_cast<const void*>(k_verify_items)));
@@ -1771,6 +1792,12 @@ int dg_verify_beacons_dev_async(const uint8_t* pk48_host, size_t n, const uint64
   RET(check_args_n(n));
   return enqueue_beacons_dev(pk48_host, n, d_prev_round, d_round, d_prev_sigs, d_prev_sig_off, d_sigs96, d_status, seed,
                              (hipStream_t)in_stream, (hipStream_t)done_stream);
+}
+
+int dg_queue_plan(int hw_queues, int* sets, int* per_item_on_set_streams) {
+  if (!sets || !per_item_on_set_streams) return fail(DG_E_ARG, "bad arguments");
+  queue_plan(hw_queues, sets, per_item_on_set_streams);
+  return 0;
 }
 
 int dg_last_batch_stream(void** out) {

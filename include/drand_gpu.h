@@ -167,6 +167,10 @@ int dg_verify_beacons_dev_async(const uint8_t* pk48_host, size_t n, const uint64
                                 const uint64_t* d_round, const uint8_t* d_prev_sigs, const uint32_t* d_prev_sig_off,
                                 const uint8_t* d_sigs96, uint8_t* d_status, uint64_t seed, void* in_stream,
                                 void* done_stream);
+/* The workspace plan dg_init uses for a hardware queue count (GPU_MAX_HW_QUEUES; HIP's default 4): *sets workspace
+ * sets (batches in flight; DG_SETS overrides) and whether the per-item pass runs on each set's own stream (1) or on a
+ * dedicated stream (0).  Host-only, no device needed.  (No reference counterpart.) */
+int dg_queue_plan(int hw_queues, int* sets, int* per_item_on_set_streams);
 /* The HIP stream (hipStream_t) the most recent dg_verify_beacons_dev_async batch was enqueued on.  Work the caller
  * enqueues there runs after that batch with no cross-stream wait: with fewer hardware queues than streams
  * (GPU_MAX_HW_QUEUES, HIP's default 4) a wait queued on a shared queue holds every stream behind it, so a consumer

@@ -38,6 +38,7 @@ EXPECT_TYPE(dg_verify_beacons_dev, int (*)(const uint8_t*, size_t, const uint64_
 EXPECT_TYPE(dg_verify_beacons_dev_async, int (*)(const uint8_t*, size_t, const uint64_t*, const uint64_t*,
                                                  const uint8_t*, const uint32_t*, const uint8_t*, uint8_t*, uint64_t,
                                                  void*, void*));
+EXPECT_TYPE(dg_queue_plan, int (*)(int, int*, int*));
 EXPECT_TYPE(dg_last_batch_stream, int (*)(void**));
 EXPECT_TYPE(dg_last_batch_flags, int (*)(uint32_t*));
 EXPECT_TYPE(dg_fallback_count, int (*)(uint64_t*));
@@ -98,6 +99,9 @@ int main() {
   expect("dg_group_counts", dg_group_counts(u64x4), DG_E_NODEV);
   expect("dg_wait_all", dg_wait_all(), DG_E_NODEV);
   // host-only state works without a device
+  int plan_sets = 0, plan_shared = 0;
+  expect("dg_queue_plan", dg_queue_plan(4, &plan_sets, &plan_shared), 0);
+  expect("dg_queue_plan sets", plan_sets, 8);
   expect("dg_set_timing", dg_set_timing(0), 0);
   expect("dg_last_timings", dg_last_timings(names, us, launches, 4), 0);
   expect("dg_get_hash_dst", dg_get_hash_dst(out, sizeof out, &len), 0);

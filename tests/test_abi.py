@@ -133,3 +133,26 @@ def test_library_load_sets_the_default_hw_queue_count(preset, want):
     r = subprocess.run([sys.executable, "-c", _QUEUES_CHILD, ROOT], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert int(r.stdout.strip().splitlines()[-1]) == want
+
+
+def test_queue_plan():
+    """dg_queue_plan (drand_gpu.hip queue_plan): 10 sets and a dedicated per-item stream from 12
+    hardware queues up; between 5 and 11 queues, queues - 2 sets and the dedicated stream, so no two library streams
+    share a queue and only one queue reserves the per-item kernels' scratch (8 queues with it on every set queue
+    failed dg_init); at 4 queues or fewer a multiple of the queue count, with the per-item pass on the set streams."""
+    import ctypes
+
+    lib = L.load()
+    got = {}
+    for q in range(0, 33):
+        sets, shared = ctypes.c_int(), ctypes.c_int()
+        assert lib.dg_queue_plan(q, ctypes.byref(sets), ctypes.byref(shared)) == 0
+        got[q] = (sets.value, shared.value)
+    assert got[0] == got[4] == (8, 1)  # HIP's default when unset
+    assert got[1] == (10, 1) and got[2] == (10, 1) and got[3] == (9, 1)
+    for q in range(5, 12):
+        assert got[q] == (q - 2, 0) and got[q][0] + 1 <= q - 1
+    for q in range(12, 33):
+        assert got[q] == (10, 0)
+    for q in range(1, 5):
+        assert got[q][0] % q == 0
