@@ -403,9 +403,6 @@ DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rc_straus(uint32_t R, uin
 //   k_rs_sac       lane (share group, round): the group's joint column loop, running point in LDS
 //   k_rs_combine   per round: the sum of its group partial sums
 constexpr uint32_t RS_G = 8;  // shares per lane (default; DG_RS_G)
-#ifndef DG_RS_REGACC
-#define DG_RS_REGACC 0
-#endif
 
 // sign-aligned recoding of one share's psi digits (g2_mul_u256_psi_sac): bit c of sgn set = +T in column c
 // (c < 64; column 64 is always +), um[i] bit c = u_{i+1, c}, top = the column-64 entry, even: d0 was even (add
@@ -549,12 +546,8 @@ DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rs_sac(uint32_t R, uint32
   const uint32_t q = g / Rn, u = g % Rn;
   const bool live = q < ngroups && nl[u] < R && rst[nl[u]] == DG_ST_OK_;
   const uint32_t j0 = q * gs, j1 = j0 + gs < t ? j0 + gs : t;
-#if DG_RS_REGACC  // A/B: the running point in registers instead of LDS
-  G2J acc;
-#else
   __shared__ G2JStore s_acc[64];
   G2JStore& acc = s_acc[threadIdx.x];
-#endif
   acc.x = fp2_zero();
   acc.y = fp2_zero();
   acc.z = fp2_zero();
@@ -584,11 +577,7 @@ DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rs_sac(uint32_t R, uint32
     rc_ld(T4 + (size_t)j * 8 * RC_Q * Rn + u, Rn, x, y);
     g2_madd_lds(acc, x, fp2_neg(y));
   }
-#if DG_RS_REGACC
-  store_g2j(Aps[(size_t)q * Rn + u], acc);
-#else
   Aps[(size_t)q * Rn + u] = acc;
-#endif
 }
 #elif defined(__HIP__)
 DG_KERNEL void __launch_bounds__(128) k_rs_tab_den(uint32_t l, uint32_t R, uint32_t Rn, uint32_t k, uint32_t t,
