@@ -707,8 +707,67 @@ DGI Fp fp_mul_np(const Fp& a, const Fp& b) {
 #else
 #define DG_FP2_PINNED 0
 #endif
+// The Karatsuba triple with each operand unpacked to digit form once (fp28.h) and the two sums a0 + a1, b0 + b1 made
+// digit-wise (digits < 2^29, values < 2p: the SOS product's column sums stay below 2^62 and its output below 2p, since
+// (2p)^2 < p 2^392): 4 unpacks instead of 6 and no Fp additions for the sums.  DG_FP2_DIG=1 (the one-wave pipeline
+// kernels, where the digit arrays fit the register file) makes it fp2_mul's form; tests/test_host_arith.py checks it
+// against fp2_mul on the host.
+DGI Fp fp28_product_packed(const uint32_t (&x)[14], const uint32_t (&y)[14]) {
+  uint32_t d[14];
+  fp28_sos_mul_d(x, y, d);
+  Fp r;
+  fp28_pack(d, r.l);
+  return fp_reduce_once(r);
+}
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DG_PIN_D14(d)                                                                                                 \
+  asm volatile("" : "+v"((d)[0]), "+v"((d)[1]), "+v"((d)[2]), "+v"((d)[3]), "+v"((d)[4]), "+v"((d)[5]), "+v"((d)[6]), \
+               "+v"((d)[7]), "+v"((d)[8]), "+v"((d)[9]), "+v"((d)[10]), "+v"((d)[11]), "+v"((d)[12]), "+v"((d)[13]))
+#define DG_PIN_T12(f)                                                                                                 \
+  asm volatile("" : "+v"((f).l[0]), "+v"((f).l[1]), "+v"((f).l[2]), "+v"((f).l[3]), "+v"((f).l[4]), "+v"((f).l[5]), \
+               "+v"((f).l[6]), "+v"((f).l[7]), "+v"((f).l[8]), "+v"((f).l[9]), "+v"((f).l[10]), "+v"((f).l[11]))
+#else
+#define DG_PIN_D14(d) ((void)0)
+#define DG_PIN_T12(f) ((void)0)
+#endif
+// (the three products serialised: each one's operands are pinned after the previous one's result)
+DGI Fp2 fp2_mul_dig(const Fp2& a, const Fp2& b) {
+  uint32_t x0[14], x1[14], y0[14], y1[14], xs[14], ys[14];
+  fp28_unpack(a.c0.l, x0);
+  fp28_unpack(a.c1.l, x1);
+  fp28_unpack(b.c0.l, y0);
+  fp28_unpack(b.c1.l, y1);
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    xs[i] = x0[i] + x1[i];
+    ys[i] = y0[i] + y1[i];
+  }
+  Fp t0 = fp28_product_packed(x0, y0);
+  DG_PIN_T12(t0);
+  DG_PIN_D14(x1);
+  DG_PIN_D14(y1);
+  Fp t1 = fp28_product_packed(x1, y1);
+  DG_PIN_T12(t1);
+  DG_PIN_D14(xs);
+  DG_PIN_D14(ys);
+  const Fp t2 = fp28_product_packed(xs, ys);
+  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+#ifndef DG_FP2_DIG
+#define DG_FP2_DIG 0
+#endif
 DGH Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
-#if DG_FP2_PINNED
+#if DG_FP2_DIG && DG_FP_CALL == 3 && defined(__HIP_DEVICE_COMPILE__)
+  Fp2 x = a, y = b;
+  DG_PIN_FP12(x.c0);
+  DG_PIN_FP12(x.c1);
+  DG_PIN_FP12(y.c0);
+  DG_PIN_FP12(y.c1);
+  Fp2 r = fp2_mul_dig(x, y);
+  DG_PIN_FP12(r.c0);
+  DG_PIN_FP12(r.c1);
+  return r;
+#elif DG_FP2_PINNED
   Fp2 x = a, y = b;
   DG_PIN_FP12(x.c0);
   DG_PIN_FP12(x.c1);

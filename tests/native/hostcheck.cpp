@@ -288,6 +288,39 @@ extern "C" int hc_ck_g2_split_check(const uint8_t* sigs384, const uint64_t* rho_
   return b.inf || (fp2_eq(b.x, want.x) && fp2_eq(b.y, want.y)) ? 1 : 0;
 }
 
+// field.h fp2_mul_dig (the Karatsuba triple in digit form, DG_FP2_DIG) against fp2_mul on n pseudo-random Fp2 pairs
+// below p and the edge values 0, 1, p - 1; 1 if every product is equal
+extern "C" int hc_fp2_mul_dig_check(uint64_t seed, uint32_t n) {
+  uint64_t s = seed | 1;
+  auto rnd = [&]() {
+    Fp a;
+    for (int i = 0; i < 12; ++i) {
+      s ^= s << 13;
+      s ^= s >> 7;
+      s ^= s << 17;
+      a.l[i] = (uint32_t)s;
+    }
+    a.l[11] &= 0x0fffffffu;  // below 2^380 < p
+    return a;
+  };
+  Fp pm1 = fp_const(P_LIMBS);
+  pm1.l[0] -= 1;
+  const Fp edges[3] = {fp_zero(), fp_one(), pm1};
+  for (uint32_t k = 0; k < n + 9; ++k) {
+    Fp2 a, b;
+    if (k < 9) {
+      a = Fp2{edges[k % 3], edges[(k / 3) % 3]};
+      b = Fp2{edges[(k + 1) % 3], pm1};
+    } else {
+      a = Fp2{rnd(), rnd()};
+      b = Fp2{rnd(), rnd()};
+    }
+    const Fp2 x = fp2_mul_dig(a, b), y = fp2_mul(a, b);
+    if (!fp2_eq(x, y)) return 0;
+  }
+  return 1;
+}
+
 // [k]P with the accumulator as a memory slot (curve.h g2_mul_u256_psi_lds, LDS on the device) against the
 // register form; 1 if equal
 extern "C" int hc_g2_mul_lds_check(const uint8_t* sig96, const uint32_t* k8) {

@@ -247,6 +247,12 @@ def test_ck_split_g2_sum_matches_group_combine(hc):
                 assert hc.hc_ck_g2_split_check(buf, arr, nl) == 1, (g.index if False else groups.index(g), rho, nl)
 
 
+def test_fp2_mul_digit_form_matches(hc):
+    """field.h fp2_mul_dig (the pipeline's Fp2 product with each operand unpacked once and the Karatsuba sums made
+    digit-wise, DG_FP2_DIG) equals fp2_mul on random operands below p and on 0, 1, p - 1."""
+    assert hc.hc_fp2_mul_dig_check(ctypes.c_uint64(12345), 3000) == 1
+
+
 def test_wnaf_digits_host_build(hc):
     """recover.h rc_wnaf: width-5 signed digits (odd, |d| <= 15, >= 5 apart) that evaluate back to the scalar,
     including the 65th position a carry can reach."""
