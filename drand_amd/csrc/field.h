@@ -712,9 +712,13 @@ DGI Fp fp_mul_np(const Fp& a, const Fp& b) {
 // (2p)^2 < p 2^392): 4 unpacks instead of 6 and no Fp additions for the sums.  DG_FP2_DIG=1 (the one-wave pipeline
 // kernels, where the digit arrays fit the register file) makes it fp2_mul's form; tests/test_host_arith.py checks it
 // against fp2_mul on the host.
+template <bool kSos = true>
 DGI Fp fp28_product_packed(const uint32_t (&x)[14], const uint32_t (&y)[14]) {
   uint32_t d[14];
-  fp28_sos_mul_d(x, y, d);
+  if (kSos)
+    fp28_sos_mul_d(x, y, d);
+  else
+    fp28_mont_mul_d(x, y, d);
   Fp r;
   fp28_pack(d, r.l);
   return fp_reduce_once(r);
@@ -731,6 +735,7 @@ DGI Fp fp28_product_packed(const uint32_t (&x)[14], const uint32_t (&y)[14]) {
 #define DG_PIN_T12(f) ((void)0)
 #endif
 // (the three products serialised: each one's operands are pinned after the previous one's result)
+template <bool kSos = true>
 DGI Fp2 fp2_mul_dig(const Fp2& a, const Fp2& b) {
   uint32_t x0[14], x1[14], y0[14], y1[14], xs[14], ys[14];
   fp28_unpack(a.c0.l, x0);
@@ -742,16 +747,32 @@ DGI Fp2 fp2_mul_dig(const Fp2& a, const Fp2& b) {
     xs[i] = x0[i] + x1[i];
     ys[i] = y0[i] + y1[i];
   }
-  Fp t0 = fp28_product_packed(x0, y0);
+  Fp t0 = fp28_product_packed<kSos>(x0, y0);
   DG_PIN_T12(t0);
   DG_PIN_D14(x1);
   DG_PIN_D14(y1);
-  Fp t1 = fp28_product_packed(x1, y1);
+  Fp t1 = fp28_product_packed<kSos>(x1, y1);
   DG_PIN_T12(t1);
   DG_PIN_D14(xs);
   DG_PIN_D14(ys);
-  const Fp t2 = fp28_product_packed(xs, ys);
+  const Fp t2 = fp28_product_packed<kSos>(xs, ys);
   return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+// a^2 = ((a0 + a1)(a0 - a1), 2 a0 a1): a0, a1 unpacked once, a0 + a1 digit-wise, a0 - a1 (mod p) unpacked
+template <bool kSos = true>
+DGI Fp2 fp2_sqr_dig(const Fp2& a) {
+  uint32_t x0[14], x1[14], xs[14], xd[14];
+  fp28_unpack(a.c0.l, x0);
+  fp28_unpack(a.c1.l, x1);
+  fp28_unpack(fp_sub(a.c0, a.c1).l, xd);
+#pragma unroll
+  for (int i = 0; i < 14; ++i) xs[i] = x0[i] + x1[i];
+  Fp m = fp28_product_packed<kSos>(x0, x1);
+  DG_PIN_T12(m);
+  DG_PIN_D14(xs);
+  DG_PIN_D14(xd);
+  const Fp c0 = fp28_product_packed<kSos>(xs, xd);
+  return Fp2{c0, fp_dbl(m)};
 }
 #ifndef DG_FP2_DIG
 #define DG_FP2_DIG 0
@@ -790,7 +811,15 @@ DGH Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
 #endif
 }
 DGH Fp2 fp2_sqr(const Fp2& a) {
-#if DG_FP2_PINNED
+#if DG_FP2_DIG && DG_FP_CALL == 3 && defined(__HIP_DEVICE_COMPILE__)
+  Fp2 x = a;
+  DG_PIN_FP12(x.c0);
+  DG_PIN_FP12(x.c1);
+  Fp2 r = fp2_sqr_dig(x);
+  DG_PIN_FP12(r.c0);
+  DG_PIN_FP12(r.c1);
+  return r;
+#elif DG_FP2_PINNED
   Fp2 x = a;
   DG_PIN_FP12(x.c0);
   DG_PIN_FP12(x.c1);
@@ -864,7 +893,24 @@ DGI Fp fp_mul_seq(Fp a, Fp b) {
   DG_PIN_FP(r);
   return r;
 }
+// DG_SEQ_DIG=1: the serialised Fp2 forms in digit form (fp2_mul_dig / fp2_sqr_dig with the column-scan product)
+#ifndef DG_SEQ_DIG
+#define DG_SEQ_DIG 0
+#endif
 DGI Fp2 fp2_mul_seq(const Fp2& a, const Fp2& b) {
+#if DG_SEQ_DIG && defined(__HIP_DEVICE_COMPILE__)
+  {
+    Fp2 x = a, y = b;
+    DG_PIN_FP(x.c0);
+    DG_PIN_FP(x.c1);
+    DG_PIN_FP(y.c0);
+    DG_PIN_FP(y.c1);
+    Fp2 r = fp2_mul_dig<false>(x, y);
+    DG_PIN_FP(r.c0);
+    DG_PIN_FP(r.c1);
+    return r;
+  }
+#endif
 #if DG_FP2_LAZY
   Fp2 x = a, y = b;
   DG_PIN_FP(x.c0);
@@ -882,6 +928,17 @@ DGI Fp2 fp2_mul_seq(const Fp2& a, const Fp2& b) {
   return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
 DGI Fp2 fp2_sqr_seq(const Fp2& a) {
+#if DG_SEQ_DIG && defined(__HIP_DEVICE_COMPILE__)
+  {
+    Fp2 x = a;
+    DG_PIN_FP(x.c0);
+    DG_PIN_FP(x.c1);
+    Fp2 r = fp2_sqr_dig<false>(x);
+    DG_PIN_FP(r.c0);
+    DG_PIN_FP(r.c1);
+    return r;
+  }
+#endif
   const Fp m = fp_mul_seq(a.c0, a.c1);
   return Fp2{fp_mul_seq(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(m)};
 }

@@ -288,7 +288,7 @@ extern "C" int hc_ck_g2_split_check(const uint8_t* sigs384, const uint64_t* rho_
   return b.inf || (fp2_eq(b.x, want.x) && fp2_eq(b.y, want.y)) ? 1 : 0;
 }
 
-// field.h fp2_mul_dig (the Karatsuba triple in digit form, DG_FP2_DIG) against fp2_mul on n pseudo-random Fp2 pairs
+// field.h fp2_mul_dig / fp2_sqr_dig (digit form, DG_FP2_DIG) against fp2_mul / fp2_sqr on n pseudo-random Fp2 pairs
 // below p and the edge values 0, 1, p - 1; 1 if every product is equal
 extern "C" int hc_fp2_mul_dig_check(uint64_t seed, uint32_t n) {
   uint64_t s = seed | 1;
@@ -317,6 +317,8 @@ extern "C" int hc_fp2_mul_dig_check(uint64_t seed, uint32_t n) {
     }
     const Fp2 x = fp2_mul_dig(a, b), y = fp2_mul(a, b);
     if (!fp2_eq(x, y)) return 0;
+    if (!fp2_eq(fp2_sqr_dig(a), fp2_sqr(a)) || !fp2_eq(fp2_sqr_dig(b), fp2_sqr(b))) return 0;
+    if (!fp2_eq(fp2_mul_dig<false>(a, b), y) || !fp2_eq(fp2_sqr_dig<false>(a), fp2_sqr(a))) return 0;
   }
   return 1;
 }
