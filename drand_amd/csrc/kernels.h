@@ -295,49 +295,81 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_scale_items(uint32_t n, u
 // of key s is K_s = K - C_s with K = sum over the active rounds of alpha_r Q_r (one Pippenger MSM, msm.h)
 // and C_s = sum of A_r over the active rounds without an item of s (k_key_accum) -- nothing when every
 // share is present in every round
-#if DG_TU_LIB
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_round_combine(uint32_t R, uint32_t k, uint32_t nslots, const uint64_t* seedp,
+// (hot TU: the running sums in LDS, additions and the 64-bit scalar multiplication inlined with serialised products,
+// curve.h g2_add_lds / g2_dbl_lds -- round 3 ran it in the library TU with out-of-line products)
+#if DG_TU_HOT
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_round_combine(uint32_t R, uint32_t k, uint32_t nslots, const uint64_t* seedp,
                                                       const G2JStore* U, const uint8_t* status,
                                                       const uint8_t* isolate, const G2JStore* Q, const uint32_t* cell,
                                                       G2JStore* V, G2JStore* A, uint8_t* active) {
   const uint64_t seed = *seedp;
+  __shared__ G2JStore s_acc[128];
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
+  G2JStore& v = s_acc[threadIdx.x];
+  v.x = fp2_zero();
+  v.y = fp2_zero();
+  v.z = fp2_zero();
   bool any = false;
-  G2J v = jac_infinity<Fp2>();
   for (uint32_t j = 0; j < k; ++j) {
     size_t i = (size_t)r * k + j;
     if (status[i] == DG_ST_OK_ && !isolate[i]) {
-      if (U) v = any ? jac_add(v, load_g2j(U[i])) : load_g2j(U[i]);
+      if (U) g2_add_lds(v, load_g2j(U[i]));
       any = true;
     }
   }
-  if (V) store_g2j(V[r], v);  // V (and U) only on the single-key path; the keyed MSM reads S directly
+  if (V) V[r] = v;  // V (and U) only on the single-key path; the keyed MSM reads S directly
   active[r] = any ? 1 : 0;
   if (nslots > 1) {
     bool gap = false;
     for (uint32_t s = 0; any && s < nslots && !gap; ++s) gap = cell[(size_t)r * nslots + s] == 0u;
-    if (gap) store_g2j(A[r], jac_mul_u64(load_g2j(Q[r]), rlc_alpha(seed, r)));
+    if (gap) {  // A_r = alpha_r Q_r, MSB first
+      const uint64_t a = rlc_alpha(seed, r);
+      const G2J q = load_g2j(Q[r]);
+      v.x = fp2_zero();
+      v.y = fp2_zero();
+      v.z = fp2_zero();
+#pragma unroll 1
+      for (int b = 63; b >= 0; --b) {
+        g2_dbl_lds(v);
+        if ((a >> b) & 1) g2_add_lds(v, q);
+      }
+      A[r] = v;
+    }
   }
 }
+#elif defined(__HIP__)
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_round_combine(uint32_t R, uint32_t k, uint32_t nslots, const uint64_t* seedp,
+                                                      const G2JStore* U, const uint8_t* status,
+                                                      const uint8_t* isolate, const G2JStore* Q, const uint32_t* cell,
+                                                      G2JStore* V, G2JStore* A, uint8_t* active);
 #endif
 
 // Kp[s * nchunks + c] = -(sum of A_r over the active rounds r in chunk c without an item of key s), so the
 // row sums are -C_s (k_round_combine)
-#if DG_TU_LIB
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_key_accum(uint32_t R, uint32_t nslots, uint32_t chunk, uint32_t nchunks,
+#if DG_TU_HOT
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_key_accum(uint32_t R, uint32_t nslots, uint32_t chunk, uint32_t nchunks,
                                                   const uint32_t* cell, const uint8_t* active, const G2JStore* A,
                                                   G2JStore* Kp) {
+  __shared__ G2JStore s_acc[128];
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nslots * nchunks) return;
   uint32_t s = g / nchunks, c = g % nchunks;
   uint32_t a = c * chunk, b = a + chunk < R ? a + chunk : R;
-  G2J acc = jac_infinity<Fp2>();
+  G2JStore& acc = s_acc[threadIdx.x];
+  acc.x = fp2_zero();
+  acc.y = fp2_zero();
+  acc.z = fp2_zero();
   for (uint32_t r = a; r < b; ++r)
-    if (active[r] && !cell[(size_t)r * nslots + s]) acc = jac_add(acc, load_g2j(A[r]));
-  store_g2j(Kp[g], jac_neg(acc));
+    if (active[r] && !cell[(size_t)r * nslots + s]) g2_add_lds(acc, load_g2j(A[r]));
+  store_g2j(Kp[g], jac_neg(load_g2j(acc)));
 }
-
+#elif defined(__HIP__)
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_key_accum(uint32_t R, uint32_t nslots, uint32_t chunk, uint32_t nchunks,
+                                                  const uint32_t* cell, const uint8_t* active, const G2JStore* A,
+                                                  G2JStore* Kp);
+#endif
+#if DG_TU_LIB
 // Xc = sum_s beta_s X_s over the key slots with a decoded key: per-lane 64-bit products, LDS tree sum
 DG_KERNEL void __launch_bounds__(256) k_key_combine(uint32_t nslots, const uint64_t* seedp, const G1AStore* keys,
                                                    const uint8_t* key_status, G1AStore* out) {
