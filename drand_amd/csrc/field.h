@@ -893,7 +893,8 @@ DGI Fp fp_mul_seq(Fp a, Fp b) {
   DG_PIN_FP(r);
   return r;
 }
-// DG_SEQ_DIG=1: the serialised Fp2 forms in digit form (fp2_mul_dig / fp2_sqr_dig with the column-scan product)
+// DG_SEQ_DIG=1: the serialised Fp2 forms in digit form (fp2_mul_dig / fp2_sqr_dig with the column-scan product; 2: with
+// the SOS product)
 #ifndef DG_SEQ_DIG
 #define DG_SEQ_DIG 0
 #endif
@@ -905,7 +906,7 @@ DGI Fp2 fp2_mul_seq(const Fp2& a, const Fp2& b) {
     DG_PIN_FP(x.c1);
     DG_PIN_FP(y.c0);
     DG_PIN_FP(y.c1);
-    Fp2 r = fp2_mul_dig<false>(x, y);
+    Fp2 r = fp2_mul_dig<DG_SEQ_DIG == 2>(x, y);
     DG_PIN_FP(r.c0);
     DG_PIN_FP(r.c1);
     return r;
@@ -933,7 +934,7 @@ DGI Fp2 fp2_sqr_seq(const Fp2& a) {
     Fp2 x = a;
     DG_PIN_FP(x.c0);
     DG_PIN_FP(x.c1);
-    Fp2 r = fp2_sqr_dig<false>(x);
+    Fp2 r = fp2_sqr_dig<DG_SEQ_DIG == 2>(x);
     DG_PIN_FP(r.c0);
     DG_PIN_FP(r.c1);
     return r;
