@@ -1025,7 +1025,83 @@ DGI Fp6 fp6_add(const Fp6& a, const Fp6& b) { return Fp6{fp2_add(a.c0, b.c0), fp
 DGI Fp6 fp6_sub(const Fp6& a, const Fp6& b) { return Fp6{fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
 DGI Fp6 fp6_neg(const Fp6& a) { return Fp6{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
 DGI Fp6 fp6_mul_v(const Fp6& a) { return Fp6{fp2_mul_xi(a.c2), a.c0, a.c1}; }
+// ---- Fp6 products with each Fp2 operand unpacked to digit form once (DG_FP6_DIG, the one-wave pipeline kernels):
+// an operand feeding two or three Fp2 products is converted once, and the Karatsuba sums (a0 + a1 ...) are made
+// digit-wise.  Digits stay below 2^30 (a sum of sums), values below 4p: the SOS column sums stay below 2^64
+// (14 (2^30)^2 + 14 2^56 < 2^63.9) and (4p)^2 < p 2^392 keeps the output below 2p.  Same results as fp6_mul /
+// fp6_mul_01 / fp6_mul_1 (tests/test_host_arith.py::test_fp6_digit_forms_match).
+struct Fp2D {
+  uint32_t c0[14], c1[14];
+};
+DGI Fp2D fp2d_of(const Fp2& a) {
+  Fp2D d;
+  fp28_unpack(a.c0.l, d.c0);
+  fp28_unpack(a.c1.l, d.c1);
+  return d;
+}
+DGI Fp2D fp2d_add(const Fp2D& a, const Fp2D& b) {
+  Fp2D d;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    d.c0[i] = a.c0[i] + b.c0[i];
+    d.c1[i] = a.c1[i] + b.c1[i];
+  }
+  return d;
+}
+DGI Fp2 fp2d_mul(Fp2D x, Fp2D y) {
+  DG_PIN_D14(x.c0);
+  DG_PIN_D14(y.c0);
+  Fp t0 = fp28_product_packed(x.c0, y.c0);
+  DG_PIN_T12(t0);
+  DG_PIN_D14(x.c1);
+  DG_PIN_D14(y.c1);
+  Fp t1 = fp28_product_packed(x.c1, y.c1);
+  DG_PIN_T12(t1);
+  uint32_t xs[14], ys[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    xs[i] = x.c0[i] + x.c1[i];
+    ys[i] = y.c0[i] + y.c1[i];
+  }
+  DG_PIN_D14(xs);
+  DG_PIN_D14(ys);
+  Fp t2 = fp28_product_packed(xs, ys);
+  DG_PIN_T12(t2);
+  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+DGI Fp6 fp6_mul_dig(const Fp6& a, const Fp6& b) {
+  const Fp2D A0 = fp2d_of(a.c0), A1 = fp2d_of(a.c1), A2 = fp2d_of(a.c2);
+  const Fp2D B0 = fp2d_of(b.c0), B1 = fp2d_of(b.c1), B2 = fp2d_of(b.c2);
+  const Fp2 v0 = fp2d_mul(A0, B0), v1 = fp2d_mul(A1, B1), v2 = fp2d_mul(A2, B2);
+  const Fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2d_mul(fp2d_add(A1, A2), fp2d_add(B1, B2)), v1), v2)), v0);
+  const Fp2 c1 = fp2_add(fp2_sub(fp2_sub(fp2d_mul(fp2d_add(A0, A1), fp2d_add(B0, B1)), v0), v1), fp2_mul_xi(v2));
+  const Fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2d_mul(fp2d_add(A0, A2), fp2d_add(B0, B2)), v0), v2), v1);
+  return Fp6{c0, c1, c2};
+}
+DGI Fp6 fp6_mul_01_dig(const Fp6& a, const Fp2& b0, const Fp2& b1) {
+  const Fp2D A0 = fp2d_of(a.c0), A1 = fp2d_of(a.c1), A2 = fp2d_of(a.c2), B0 = fp2d_of(b0), B1 = fp2d_of(b1);
+  const Fp2 v0 = fp2d_mul(A0, B0), v1 = fp2d_mul(A1, B1);
+  const Fp2 c0 = fp2_add(fp2_mul_xi(fp2d_mul(A2, B1)), v0);
+  const Fp2 c1 = fp2_sub(fp2_sub(fp2d_mul(fp2d_add(A0, A1), fp2d_add(B0, B1)), v0), v1);
+  const Fp2 c2 = fp2_add(fp2d_mul(A2, B0), v1);
+  return Fp6{c0, c1, c2};
+}
+DGI Fp6 fp6_mul_1_dig(const Fp6& a, const Fp2& b1) {
+  const Fp2D B1 = fp2d_of(b1);
+  return Fp6{fp2_mul_xi(fp2d_mul(fp2d_of(a.c2), B1)), fp2d_mul(fp2d_of(a.c0), B1), fp2d_mul(fp2d_of(a.c1), B1)};
+}
+#ifndef DG_FP6_DIG
+#define DG_FP6_DIG 0
+#endif
+#if DG_FP6_DIG && DG_FP_CALL == 3 && defined(__HIP_DEVICE_COMPILE__)
+#define DG_FP6_DIG_ON 1
+#else
+#define DG_FP6_DIG_ON 0
+#endif
 DGH Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
+#if DG_FP6_DIG_ON
+  return fp6_mul_dig(a, b);
+#endif
   Fp2 v0 = fp2_mul(a.c0, b.c0);
   Fp2 v1 = fp2_mul(a.c1, b.c1);
   Fp2 v2 = fp2_mul(a.c2, b.c2);
@@ -1058,6 +1134,9 @@ DG12 Fp6 fp6_inv(const Fp6& a) {
 }
 // (a0 + a1 v + a2 v^2) * (b0 + b1 v)
 DGH Fp6 fp6_mul_01(const Fp6& a, const Fp2& b0, const Fp2& b1) {
+#if DG_FP6_DIG_ON
+  return fp6_mul_01_dig(a, b0, b1);
+#endif
   Fp2 v0 = fp2_mul(a.c0, b0);
   Fp2 v1 = fp2_mul(a.c1, b1);
   Fp2 c0 = fp2_add(fp2_mul_xi(fp2_mul(a.c2, b1)), v0);
@@ -1067,6 +1146,9 @@ DGH Fp6 fp6_mul_01(const Fp6& a, const Fp2& b0, const Fp2& b1) {
 }
 // (a0 + a1 v + a2 v^2) * (b1 v)
 DGI Fp6 fp6_mul_1(const Fp6& a, const Fp2& b1) {
+#if DG_FP6_DIG_ON
+  return fp6_mul_1_dig(a, b1);
+#endif
   return Fp6{fp2_mul_xi(fp2_mul(a.c2, b1)), fp2_mul(a.c0, b1), fp2_mul(a.c1, b1)};
 }
 

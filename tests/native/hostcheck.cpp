@@ -323,6 +323,37 @@ extern "C" int hc_fp2_mul_dig_check(uint64_t seed, uint32_t n) {
   return 1;
 }
 
+// field.h's Fp6 digit forms (DG_FP6_DIG) against fp6_mul / fp6_mul_01 / fp6_mul_1 on n pseudo-random operands (values
+// below p, including p - 1 limbs); 1 if all equal
+static bool fp6_same(const Fp6& x, const Fp6& y) { return fp2_eq(x.c0, y.c0) && fp2_eq(x.c1, y.c1) && fp2_eq(x.c2, y.c2); }
+extern "C" int hc_fp6_dig_check(uint64_t seed, uint32_t n) {
+  uint64_t s = seed | 1;
+  auto rnd = [&]() {
+    Fp a;
+    for (int i = 0; i < 12; ++i) {
+      s ^= s << 13;
+      s ^= s >> 7;
+      s ^= s << 17;
+      a.l[i] = (uint32_t)s;
+    }
+    a.l[11] &= 0x0fffffffu;
+    if ((s & 7) == 0) {  // the largest element, p - 1
+      a = fp_const(P_LIMBS);
+      a.l[0] -= 1;
+    }
+    return a;
+  };
+  auto r2 = [&]() { return Fp2{rnd(), rnd()}; };
+  for (uint32_t k = 0; k < n; ++k) {
+    const Fp6 a{r2(), r2(), r2()}, b{r2(), r2(), r2()};
+    const Fp2 b0 = r2(), b1 = r2();
+    if (!fp6_same(fp6_mul_dig(a, b), fp6_mul(a, b))) return 0;
+    if (!fp6_same(fp6_mul_01_dig(a, b0, b1), fp6_mul_01(a, b0, b1))) return 0;
+    if (!fp6_same(fp6_mul_1_dig(a, b1), fp6_mul_1(a, b1))) return 0;
+  }
+  return 1;
+}
+
 // [k]P with the accumulator as a memory slot (curve.h g2_mul_u256_psi_lds, LDS on the device) against the
 // register form; 1 if equal
 extern "C" int hc_g2_mul_lds_check(const uint8_t* sig96, const uint32_t* k8) {

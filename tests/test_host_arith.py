@@ -253,6 +253,12 @@ def test_fp2_mul_digit_form_matches(hc):
     assert hc.hc_fp2_mul_dig_check(ctypes.c_uint64(12345), 3000) == 1
 
 
+def test_fp6_digit_forms_match(hc):
+    """field.h's Fp6 products with each Fp2 operand unpacked once (DG_FP6_DIG: dense, 01-sparse and 1-sparse) equal
+    fp6_mul / fp6_mul_01 / fp6_mul_1 on random operands below p, p - 1 limbs included."""
+    assert hc.hc_fp6_dig_check(ctypes.c_uint64(777), 1500) == 1
+
+
 def test_wnaf_digits_host_build(hc):
     """recover.h rc_wnaf: width-5 signed digits (odd, |d| <= 15, >= 5 apart) that evaluate back to the scalar,
     including the 65th position a carry can reach."""
