@@ -290,3 +290,43 @@ def test_async_batches_consumed_on_the_batch_stream():
         exp = np.array(want if k == 2 else [0] * n, np.uint8)
         assert np.array_equal(got, exp), k
         assert np.array_equal(bits.cpu().numpy(), np.packbits(exp != 0, bitorder="little")), k
+
+
+_QUEUE_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from drand_amd import _lib as L
+from drand_amd import tbls
+from tests.fixtures import chain, chain_arrays, hx
+c = chain()
+pr, rr, ps, sigs, msgs = chain_arrays(c)
+bad = sigs.copy()
+bad[2] = sigs[3]
+bad[6, 0] ^= 0x20
+st = tbls.verify_beacons(hx(c["pk"]), pr, rr, ps, bad, seed=41)
+np.save(sys.argv[2], st)
+print(L.hw_queues())
+"""
+
+
+@pytest.mark.parametrize("queues", ["8", "16"])
+def test_dg_init_and_per_item_pass_at_other_queue_counts(tmp_path, queues):
+    """A process started with GPU_MAX_HW_QUEUES = 8 or 16 (child process: HIP reads it once) initialises -- round 4's
+    first plan put the per-item kernels' scratch on every set queue and failed dg_init at 8 queues with
+    HSA_STATUS_ERROR_OUT_OF_RESOURCES -- and a batch with two bad beacons gets the twin's statuses (the per-item pass on
+    the dedicated stream, dg_queue_plan)."""
+    out = tmp_path / "st.npy"
+    r = subprocess.run([sys.executable, "-c", _QUEUE_CHILD, ROOT, str(out)],
+                       env=dict(os.environ, GPU_MAX_HW_QUEUES=queues), capture_output=True, text=True, timeout=300,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == queues
+    c = chain()
+    pr, rr, ps, sigs, msgs = chain_arrays(c)
+    bad = sigs.copy()
+    bad[2] = sigs[3]
+    bad[6, 0] ^= 0x20
+    pk = hx(c["pk"])
+    want = [twin.verify(pk, bytes(msgs[i]), bytes(bad[i])) for i in range(len(rr))]
+    assert np.load(out).tolist() == want and sum(1 for w in want if w) == 2
