@@ -448,7 +448,7 @@ def recover_bench(L, tbls, shard, src, R_total, t, n, world, rank, peak, steps=2
     return out, (commits, msgs, parts), vp_line
 
 
-def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=256, frac=0.10, n_short=3):
+def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=256, frac=0.10, n_short=3, vp_neg=True):
     """BASELINE configs[4]: n = 256, t = 129, ~10% of the (round, share) cells corrupted with the six
     cycling modes of tools/corrupt.py, plus `n_short` rounds with more than n - t corrupted shares (-> "not
     enough shares"); each rank its contiguous range of R_total rounds through dg_recover_dev (inputs resident
@@ -522,6 +522,7 @@ def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=
     if roof is None:
         roof = roofline_of(kt, {"k_verify_groups": checks, "k_rs_sac": R}, peak, ext, "c5")
     rs_roof = roofline_of({k: v for k, v in kt.items() if k == "k_rs_sac"}, {"k_rs_sac": R}, peak, None, "c5")
+    vpn = vp_negative_bench(L, tbls, pub, d_msgs, d_parts, bad, world, peak) if vp_neg else None
     ncorrupt = np.array([len(items)], np.int64)
     if world > 1:
         import torch
@@ -543,7 +544,7 @@ def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=
                     "every round takes the per-item pass (group tests, then single checks); outputs all-gathered "
                     "(RCCL); host_api_value: the host-buffer dg_recover with the PCIe transfer of %d MB of partials "
                     "per GPU inside the call" % (R * n * 98 // 10**6)}, (commits, msgs, parts,
-                                                                                             ss, rs)
+                                                                                             ss, rs), vpn
 
 
 def c1_gpu(L, tbls, reps=3, rounds=1000):
@@ -618,6 +619,106 @@ def sync_bench(chain_sigs, R, batch=25000):
     return {"metric": "syncFrom catch-up rounds/s (bulk.sync_from, beacon/beacon.go:529-607)", "value": R / dt,
             "unit": "rounds/s", "rounds": R, "batch": batch, "s": dt,
             "note": "host Beacon objects -> dg_check_links + dg_verify_beacons per batch (host-buffer API, blocking)"}
+
+
+def negative_positions(G):
+    """Global 0-based positions of the corrupted rounds of the negative lines: 1% of G, the deterministic positions
+    of tests/test_gpu_round2.py::test_sharded_1m_chain_equals_one_batch."""
+    return np.unique((np.arange(G // 100, dtype=np.int64) * 7919 + 13) % G)
+
+
+def negative_bench(L, args, step, drain, sig_src, d_sts, nbuf, counter, n, a, G, world, peak, bounds):
+    """BASELINE configs[1] with SURVEY §8(d) C2's negative variant: the same overlapped, HBM-resident steps as the
+    headline, but 1% of the signatures replaced (at negative_positions) by the valid signature of the next round, so
+    every batch equation fails and each batch isolates its bad rounds (beacon/chain.go:65-71: kyber's verdict is per
+    beacon).  Every step's verdicts must flag exactly the replaced rounds (status 1, bad signature)."""
+    import torch
+
+    from drand_amd import shard
+
+    d_sig = sig_src[0]
+    bad = negative_positions(G)
+    loc = bad[(bad >= a) & (bad < a + n)] - a
+    neg = d_sig.clone()
+    src = torch.from_numpy(np.where(loc + 1 < n, loc + 1, loc - 1)).to(d_sig.device)
+    neg[torch.from_numpy(loc).to(d_sig.device)] = d_sig[src]
+    want = torch.zeros(n, dtype=torch.uint8, device=d_sig.device)
+    want[torch.from_numpy(loc).to(d_sig.device)] = L.ST_BAD_SIG
+    sig_src[0] = neg
+    try:
+        for w in range(max(1, args.warmup)):
+            step(2000 + w)
+        drain()
+        fb0 = L.fallback_count()
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+        c0 = counter[0]
+        t0 = time.perf_counter()
+        bits = [step(3000 + s) for s in range(args.neg_steps)]
+        drain()
+        if world > 1:
+            dist.barrier()
+        dt = max_over_ranks(time.perf_counter() - t0, world)
+        for i in sorted(set(c % nbuf for c in range(max(c0, counter[0] - nbuf), counter[0]))):
+            assert torch.equal(d_sts[i], want), "c2_negative: verdicts differ from the replaced rounds"
+        want_bits = shard.allgather_verdicts(want, world, m=(max(y - x for x, y in (shard.round_range(G, world, q)
+                                                                                    for q in range(world))) + 7) // 8)
+        assert all(torch.equal(b_, want_bits) for b_ in bits), "c2_negative: gathered bitmap"
+        fallbacks = L.fallback_count() - fb0
+        L.check(L.lib().dg_set_timing(1))
+        [step(3000 + s) for s in range(args.neg_steps)]
+        drain()
+        kt = L.timings()
+        L.check(L.lib().dg_set_timing(0))
+    finally:
+        sig_src[0] = d_sig
+    units = {"k_exp_pm3d4": 6 * n * args.neg_steps}
+    roof = roofline_of(kt, units, peak, {"timing": "HIP events, instrumented replay of the timed steps (overlapped)"})
+    iso = {k: v for k, v in kt.items() if k.startswith(("k_ck_", "k_xg_", "k_verify_", "k_clear_rounds"))}
+    tot = sum(u * c for u, c in kt.values()) or 1.0
+    return {"metric": "configs[1] negative: verified beacon rounds/s, 100k-round chain with 1%% of sigma replaced "
+                      "(%d rounds), exact bitmap" % len(bad),
+            "value": G * args.neg_steps / dt, "unit": "rounds/s", "steps": args.neg_steps,
+            "ms_per_step": dt / args.neg_steps * 1e3, "corrupted_rounds": int(len(bad)), "batch_fallbacks": fallbacks,
+            "isolation_kernel_share": round(sum(u * c for u, c in iso.values()) / tot, 4), "roofline": roof,
+            "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
+            "kernel_launches": {k: v[1] for k, v in kt.items()},
+            "note": "same overlapped HBM-resident steps as the headline; every batch equation fails and the batch "
+                    "isolates its bad rounds on the device; bitmap asserted exact every step"}
+
+
+def vp_negative_bench(L, tbls, pub, d_msgs, d_parts, bad, world, peak, steps=2):
+    """dg_verify_partials_dev (ProcessBeacon's VerifyPartial, beacon/beacon.go:148, of every partial) on C5's
+    corrupted set: n = 256, t = 129, ~10% of the partials corrupted (six modes) plus the short rounds.  The batch
+    equation fails, so every partial gets its own verdict by isolation; each must match the corruption map (corrupted:
+    rejected, clean: accepted)."""
+    import torch
+
+    tbls.verify_partial_batch_dev(pub, d_msgs, d_parts, seed=40)  # warmup
+    dts = []
+    for s in range(steps):
+        d_vst, dt = timed_ranks(lambda: tbls.verify_partial_batch_dev(pub, d_msgs, d_parts, seed=41 + s), world)
+        dts.append(dt)
+    st = d_vst.cpu().numpy().reshape(bad.shape)
+    assert (st[bad] != 0).all() and (st[~bad] == 0).all(), "vp_negative: statuses differ from the corruption map"
+    L.check(L.lib().dg_set_timing(1))
+    g0 = L.group_counts()
+    tbls.verify_partial_batch_dev(pub, d_msgs, d_parts, seed=49)
+    kt = L.timings()
+    g1 = L.group_counts()
+    L.check(L.lib().dg_set_timing(0))
+    dt = min(dts)
+    R = bad.shape[0]
+    roof = pipeline_roofline(kt, {m + 1: g1[m] - g0[m] for m in range(4)}, R, peak,
+                             {"timing": "HIP events on the launch stream, one call"}, "c5vp")
+    torch.cuda.synchronize()
+    return {"metric": "VerifyPartial of all n=256 partials per round, C5's 10%-corrupted set (partials/s)",
+            "value": bad.size * world / dt, "unit": "partials/s", "s_per_step": dt, "corrupted": int(bad.sum()),
+            "roofline": roof, "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
+            "kernel_launches": {k: v[1] for k, v in kt.items()},
+            "note": "HBM-resident partials; batch equation fails; statuses asserted against the corruption map"}
 
 
 def max_over_ranks(x, world):
@@ -698,7 +799,8 @@ def headline_roofline(kt, kt_iso, per, peak, G, steps, world, dt):
 SIDE_KEYS = ("kernel_avg_us", "kernel_launches", "kernel_avg_us_isolated", "kernel_time_share", "note", "sample", "partials_generated_s",
              "rs_sac_roofline",
              "setup_s", "checks_by_members", "timing", "allgather_s", "host_api_s_per_step", "rounds_per_gpu",
-             "partials_per_round", "recover_s", "recover_from_verdicts_s")
+             "partials_per_round", "recover_s", "recover_from_verdicts_s", "corrupted_rounds", "corrupted",
+             "steps", "isolation_kernel_share")
 
 
 # sub-lines print a short metric name (the full description is in the side file), and only these roofline and
@@ -708,7 +810,9 @@ SHORT_METRIC = {"recover": "configs[2] kyber Recover/s, n=64 t=33 (examined pref
                 "adversarial": "configs[4] adversarial Recover/s, n=256 t=129, 10% corrupted",
                 "c1": "configs[0] n=5 t=3: 5 Signs + Recover + VerifyRecovered, rounds/s",
                 "live_latency": "live round n=64 t=33, ms per call",
-                "sync": "syncFrom catch-up rounds/s"}
+                "sync": "syncFrom catch-up rounds/s",
+                "c2_negative": "configs[1] with 1% of sigma replaced: rounds/s, exact bitmap",
+                "vp_negative": "VerifyPartial on C5's 10%-corrupted set, partials/s"}
 SUB_ROOF = ("kernel", "achieved", "peak", "unit", "frac", "traffic", "issue_frac", "kernel_avg_us")
 SUB_CPU = ("value", "unit", "cores", "kind", "all_host_cpus_linear_est", "statuses_match_gpu")
 
@@ -807,6 +911,9 @@ def main():
     ap.add_argument("--c5-rounds", type=int, default=10000, help="C5 rounds (all GPUs); 0 disables")
     ap.add_argument("--sync-rounds", type=int, default=100000, help="0 disables the syncFrom catch-up line")
     ap.add_argument("--no-c1", action="store_true", help="no C1 / live-latency lines")
+    ap.add_argument("--neg-steps", type=int, default=10,
+                    help="steps of the c2_negative line (1%% of the signatures replaced); 0 disables")
+    ap.add_argument("--no-vp-negative", action="store_true", help="no vp_negative line (VerifyPartial on C5's set)")
     ap.add_argument("--status-bufs", type=int, default=int(os.environ.get("DG_SETS", "10")),
                     help="steps whose verdicts may be in flight (at least the library's workspace sets, DG_SETS = 10)")
     ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("BENCH_HW_QUEUES", "0")),
@@ -893,9 +1000,11 @@ def main():
     # workspace set stalls that set; several batches or ranks: a side stream waits for them all
     on_set = world == 1 and len(bounds) == 1 and not args.use_sync
 
+    sig_src = [d_sig]  # the signatures the steps verify (the c2_negative line swaps in a corrupted copy)
+
     def enqueue(lo, hi, d_st, seed, blocking):
-        args_ = (pkb, hi - lo, L.ptr(d_pr[lo:]), L.ptr(d_r[lo:]), L.ptr(d_ps), L.ptr(d_off[lo:]), L.ptr(d_sig[lo:]),
-                 L.ptr(d_st[lo:]), seed)
+        args_ = (pkb, hi - lo, L.ptr(d_pr[lo:]), L.ptr(d_r[lo:]), L.ptr(d_ps), L.ptr(d_off[lo:]),
+                 L.ptr(sig_src[0][lo:]), L.ptr(d_st[lo:]), seed)
         if blocking:
             L.check(lib.dg_verify_beacons_dev(*args_, None))
         else:
@@ -980,11 +1089,14 @@ def main():
     peak = measure_peak(shard, local, detail=(rank == 0 and not args.no_peak_detail))
     roof = headline_roofline(kt, kt_iso, bounds[0][1] - bounds[0][0], peak, G, args.steps, world, dt)
     share = {k: round(v[0] * v[1] / (dt * 1e6), 4) for k, v in kt.items()}
+    neg = None
+    if args.neg_steps > 0:
+        neg = negative_bench(L, args, step, drain, sig_src, d_sts, nbuf, counter, n, a, G, world, peak, bounds)
     del d_sts, d_sig, d_ps
     torch.cuda.empty_cache()
 
     # Recover lines (sharded like the headline; chain rounds 1..R)
-    rec = adv = syn = c1 = lat = c2 = None
+    rec = adv = syn = c1 = lat = c2 = vpn = None
     rec_in = adv_in = None
     src = None
     if args.recover_rounds or args.c5_rounds or args.sync_rounds:
@@ -993,7 +1105,8 @@ def main():
     if args.recover_rounds:
         rec, rec_in, c2 = recover_bench(L, tbls, shard, src, args.recover_rounds, 33, 64, world, rank, peak)
     if args.c5_rounds:
-        adv, adv_in = adversarial_bench(L, tbls, shard, src, args.c5_rounds, world, rank, peak)
+        adv, adv_in, vpn = adversarial_bench(L, tbls, shard, src, args.c5_rounds, world, rank, peak,
+                                             vp_neg=not args.no_vp_negative)
     if rank == 0:
         if args.sync_rounds and src.linked:
             syn = sync_bench(src.sigs, args.sync_rounds)
@@ -1039,7 +1152,8 @@ def main():
     tables = {"kernel_time_share": share, "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
               "kernel_avg_us_isolated": {k: round(v[0], 1) for k, v in kt_iso.items()}, "peak": peak}
     report(rank, world, head, roof, cpu, {"recover": rec, "adversarial": adv, "c1": c1, "live_latency": lat,
-                                          "sync": syn, "c2_verify_all": c2}, tables, args.tables_out)
+                                          "sync": syn, "c2_verify_all": c2, "c2_negative": neg,
+                                          "vp_negative": vpn}, tables, args.tables_out)
     if world > 1:
         dist.destroy_process_group()
 
