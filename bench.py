@@ -162,13 +162,12 @@ def pipeline_roofline(kt, checks, rounds, peak, extra=None, config="c5"):
     """Roofline of Recover's per-item pass as the pairing-check pipeline (checks.h): the algorithmic multiply-adds of
     every check the pass ran (profiles/opcounts.json: k_ck_prep[m] by member count m, the same rest per check) and of
     the per-round lines, over the summed HIP-event time of every k_ck_* launch of the call.  None when the call ran
-    no k_ck_* kernel (the round-3 single-lane kernel, DG_CK_OLD=1)."""
+    no k_ck_* kernel."""
     ck = {k: v for k, v in kt.items() if k.startswith("k_ck_")}
     if not ck:
         return None
     oc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["per_unit"]
-    rest = sum(oc[k]["macs"] for k in ("k_ck_lines2", "k_ck_miller", "k_ck_fe1", "k_ck_inv", "k_ck_mul (11 per check)",
-                                       "k_ck_expsq (5 per check)", "k_ck_expdec (5 per check)"))
+    rest = sum(oc[k]["macs"] for k in CK_REST)
     n = sum(checks.values())
     macs = sum(c * (oc["k_ck_prep[%d]" % m]["macs"] + rest) for m, c in checks.items()) + \
         rounds * oc["k_ck_round_lines (per round)"]["macs"]
@@ -180,6 +179,36 @@ def pipeline_roofline(kt, checks, rounds, peak, extra=None, config="c5"):
            "traffic": trf, "kernel": "k_ck_* pipeline", "kernel_avg_us": us, "units_per_launch": n,
            "macs_per_unit": macs / max(n, 1), "issue_frac": None, "peak_source": peak.get("source") if peak else None,
            "per_kernel_share": {k: round(a * l / us, 4) for k, (a, l) in ck.items()}}
+    if extra:
+        out.update(extra)
+    return out
+
+
+# the per-check kernels of the pipeline after the members' sums (profiles/opcounts.json keys)
+CK_REST = ("k_ck_lines2", "k_ck_miller", "k_ck_easy", "k_ck_expsq (5 per check)", "k_ck_expdec (5 per check)",
+           "k_ck_final")
+
+
+def xr_roofline(kt, counts, quads, peak, extra=None):
+    """Roofline of the cross-round isolation of failed single-key batches (xr.h) as a whole: the algorithmic
+    multiply-adds of its quad sums (2 sides per quad) and of the checks of each level (counts: dg_isolation_counts
+    deltas; level 1 groups of 4 quads, level 2 quads, level 3 single rounds; each check h_eff + lines of its hash side
+    and the pipeline's per-check rest), over the summed HIP-event time of every k_xg_* / k_xq_* / k_ck_* launch."""
+    ks = {k: v for k, v in kt.items() if k.startswith(("k_ck_", "k_xg_", "k_xq_"))}
+    if not ks or not sum(counts):
+        return None
+    oc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["per_unit"]
+    per_check = oc["k_xg_hlines"]["macs"] + sum(oc[k]["macs"] for k in CK_REST)
+    macs = (2 * quads * oc["k_xq_sum (per quad side)"]["macs"] + counts[0] * (oc["k_xg_prep[level 1, 4 quads]"]["macs"] +
+            per_check) + counts[1] * (oc["k_xg_prep[level 2]"]["macs"] + per_check) + counts[2] * per_check)
+    us = sum(a * l for a, l in ks.values())
+    achieved = macs / (us * 1e-6) / 1e12
+    pk = peak.get("tmac_s") if peak else None
+    out = {"bound": "valu-int", "achieved": achieved, "peak": pk, "unit": "TMAC/s", "frac": achieved / pk if pk else None,
+           "traffic": traffic_of("xr pipeline", "c2neg"), "kernel": "xr isolation (k_xq/k_xg/k_ck_*)",
+           "kernel_avg_us": us, "units_per_launch": sum(counts), "macs_per_unit": macs / max(sum(counts), 1),
+           "issue_frac": None, "checks_by_level": list(counts), "quads": quads,
+           "per_kernel_share": {k: round(a * l / us, 4) for k, (a, l) in ks.items()}}
     if extra:
         out.update(extra)
     return out
@@ -513,14 +542,11 @@ def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=
     kt = L.timings()
     g1 = L.group_counts()
     L.check(L.lib().dg_set_timing(0))
-    checks = {"k_verify_groups[%d]" % (m + 1): g1[m] - g0[m] for m in range(4)}
-    # the per-item pass as a whole (the pairing-check pipeline of checks.h), or the dominant kernel of the call when
-    # it ran the round-3 single-lane kernel (DG_CK_OLD=1); k_rs_sac: one unit = one round's joint column MSM (priced at
-    # t = 129 over a scattered index set)
+    checks = {"k_ck_prep[%d]" % (m + 1): g1[m] - g0[m] for m in range(4)}
+    # the per-item pass as a whole (the pairing-check pipeline of checks.h); k_rs_sac: one unit = one round's joint
+    # column MSM (priced at t = 129 over a scattered index set)
     ext = {"timing": "HIP events on the launch stream, one dg_recover call", "checks_by_members": checks}
     roof = pipeline_roofline(kt, {m + 1: g1[m] - g0[m] for m in range(4)}, R, peak, ext, "c5")
-    if roof is None:
-        roof = roofline_of(kt, {"k_verify_groups": checks, "k_rs_sac": R}, peak, ext, "c5")
     rs_roof = roofline_of({k: v for k, v in kt.items() if k == "k_rs_sac"}, {"k_rs_sac": R}, peak, None, "c5")
     vpn = vp_negative_bench(L, tbls, pub, d_msgs, d_parts, bad, world, peak) if vp_neg else None
     ncorrupt = np.array([len(items)], np.int64)
@@ -668,20 +694,28 @@ def negative_bench(L, args, step, drain, sig_src, d_sts, nbuf, counter, n, a, G,
         assert all(torch.equal(b_, want_bits) for b_ in bits), "c2_negative: gathered bitmap"
         fallbacks = L.fallback_count() - fb0
         L.check(L.lib().dg_set_timing(1))
+        x0 = L.isolation_counts()
         [step(3000 + s) for s in range(args.neg_steps)]
         drain()
         kt = L.timings()
+        x1 = L.isolation_counts()
         L.check(L.lib().dg_set_timing(0))
     finally:
         sig_src[0] = d_sig
-    units = {"k_exp_pm3d4": 6 * n * args.neg_steps}
-    roof = roofline_of(kt, units, peak, {"timing": "HIP events, instrumented replay of the timed steps (overlapped)"})
-    iso = {k: v for k, v in kt.items() if k.startswith(("k_ck_", "k_xg_", "k_verify_", "k_clear_rounds"))}
+    counts = [b_ - a_ for a_, b_ in zip(x0, x1)]
+    nb = len(bounds)
+    quads = sum((hi - lo + 3) // 4 for lo, hi in bounds) * args.neg_steps
+    ext = {"timing": "HIP events, instrumented replay of the timed steps (overlapped)"}
+    roof = xr_roofline(kt, counts, quads, peak, ext)
+    if roof is None:
+        roof = roofline_of(kt, {"k_exp_pm3d4": 6 * n * args.neg_steps}, peak, ext)
+    iso = {k: v for k, v in kt.items() if k.startswith(("k_ck_", "k_xg_", "k_xq_"))}
     tot = sum(u * c for u, c in kt.values()) or 1.0
     return {"metric": "configs[1] negative: verified beacon rounds/s, 100k-round chain with 1%% of sigma replaced "
                       "(%d rounds), exact bitmap" % len(bad),
             "value": G * args.neg_steps / dt, "unit": "rounds/s", "steps": args.neg_steps,
             "ms_per_step": dt / args.neg_steps * 1e3, "corrupted_rounds": int(len(bad)), "batch_fallbacks": fallbacks,
+            "checks_per_batch": [round(c / max(nb * args.neg_steps, 1), 1) for c in counts],
             "isolation_kernel_share": round(sum(u * c for u, c in iso.values()) / tot, 4), "roofline": roof,
             "kernel_avg_us": {k: round(v[0], 1) for k, v in kt.items()},
             "kernel_launches": {k: v[1] for k, v in kt.items()},

@@ -54,6 +54,7 @@ SIGNATURES = {
     "dg_last_batch_flags": ([_P], _I),
     "dg_fallback_count": ([_P], _I),
     "dg_group_counts": ([_P], _I),
+    "dg_isolation_counts": ([_P], _I),
     "dg_set_group_size": ([_U32], _I),
     "dg_recover_dev": ([_P, _U32, _U32, _SZ, _P, _SZ, _U32, _P, _P, _P, _P, _U64], _I),
     "dg_verify_partials_dev": ([_P, _U32, _SZ, _P, _SZ, _U32, _P, _P, _U64], _I),
@@ -164,6 +165,14 @@ def group_counts():
     """Recover's per-item pass since dg_init: [checks of 1, 2, 3, 4 shares of a round at once]."""
     out = np.zeros(4, dtype=np.uint64)
     check(lib().dg_group_counts(ptr(out)))
+    return [int(v) for v in out]
+
+
+def isolation_counts():
+    """The cross-round isolation of failed single-key batches since dg_init (xr.h): [group tests of 4 quads, tests
+    of one quad (4 rounds), single rounds]."""
+    out = np.zeros(3, dtype=np.uint64)
+    check(lib().dg_isolation_counts(ptr(out)))
     return [int(v) for v in out]
 
 

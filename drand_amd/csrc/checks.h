@@ -17,14 +17,15 @@
 //     k_ck_prep      the group's members: a = sum rho X, b = sum rho S (kernels.h group_combine)
 //     k_ck_lines2    the 68 lines of the pair (-g1, b) -> L2[s][g] (b's G2 state lives only here)
 //     k_ck_miller    f = the product of both pairs' lines at a and at -g1 (the Fp12 accumulator and one line)
-//     k_ck_fe1       the pieces of f^-1 down to one Fp norm per check  -> batch inversion (phases.h k_binv_*)
-//     k_ck_inv       f^-1;  k_ck_mul: f1 = f^-1 conj(f), f2 = f1 frob^2(f1)
+//     k_ck_easy      the easy part f2 = f1 frob^2(f1), f1 = f^-1 conj(f), with the one Fp inversion in the lane
 //     5 x [k_ck_expsq   63 compressed cyclotomic squarings (Karabina): the 6 powers, their denominators' norms
-//                       -> batch inversion of 6 G norms (Montgomery's trick across the chunk)
-//          k_ck_expdec  decompression and the product x^z  (k_ck_explain: the uncompressed chain where a
-//                       denominator is zero)
-//          k_ck_mul     the hard part's next factor]
-//     k_ck_verdict   == 1, the members' verdicts exactly as verify_group writes them.
+//          k_ck_expdec  the 6 norms inverted in the lane (Montgomery's trick, one Fp inversion), decompression, the
+//                       product x^z, times the hard part's next factor  (k_ck_explain: the uncompressed chain where
+//                       a denominator is zero, same next factor)]
+//     k_ck_final     the last factors and == 1 -> good[g];  k_ck_verdict: the members' verdicts.
+// Every kernel after the lines is one lane per check with no exchange between lanes (no batch inversion), so a launch
+// may be sized for more checks than it holds: `gcnt` (device) gates the lanes on the count a producer reached
+// (xr.h: the cross-round isolation of a failed single-key batch launches every level for its worst case).
 // Every value equals the one pair_check computes (pairing.h miller_loop, final_exp_cubed, cyc_exp_z): the same
 // formulas in the same order, only split across kernels (tests/test_host_arith.py runs the pipeline's pieces on the
 // host against pair_check).
@@ -50,7 +51,8 @@ namespace dg {
 #define DG_CK_SUB_WAVES 2
 #endif
 constexpr uint32_t CK_STEPS = 68;      // Miller steps over |z| = 0xd201000000010000: 63 doublings + 5 additions
-constexpr uint32_t CK_CHUNK = 524288;  // checks per pipeline launch (~15 GB of workspace: one chunk per pass at C5)
+constexpr uint32_t CK_CHUNK = 524288;  // checks per pipeline launch at most (~45 KB of workspace per check)
+constexpr uint32_t CK_NEXP = 5;        // x^z chains of the hard part (one k_ck_explain work list each)
 constexpr int CK_NPOW = 6;             // set bits of |z|: the powers a^(2^k) of the compressed chain
 constexpr uint32_t CK_GRP = 4;         // members per check at most (kernels.h GRP)
 
@@ -58,6 +60,8 @@ constexpr uint32_t CK_GRP = 4;         // members per check at most (kernels.h G
 struct CkLine {
   Fp2 c0, c1, c4;
 };
+// a lane past the checks of a launch: g >= G (the host's bound) or, when the device count gcnt is given, g >= *gcnt
+DGI bool ck_dead(uint32_t g, uint32_t G, const uint32_t* gcnt) { return g >= G || (gcnt && g >= *gcnt); }
 // one check: up to GRP shares of one round (or one share alone)
 struct CkState {
   G1AStore a;          // sum rho_i X_i (a single share: its key)
@@ -207,6 +211,22 @@ DGI Fp12 ck_expdec(Get get) {
   }
   return fp12_conj(acc);
 }
+// the six norms nv(i) (none zero) replaced by their inverses (Montgomery's trick: one Fp inversion, 15 products)
+template <class Ld, class St>
+DGI void ck_inv6(Ld ld, St st) {
+  Fp pre[CK_NPOW];
+  pre[0] = ld(0);
+#pragma unroll 1
+  for (int i = 1; i < CK_NPOW; ++i) pre[i] = fp_mul(pre[i - 1], ld(i));
+  Fp inv = fp_inv(pre[CK_NPOW - 1]);
+#pragma unroll 1
+  for (int i = CK_NPOW - 1; i > 0; --i) {
+    const Fp n = ld(i);
+    st(i, fp_mul(inv, pre[i - 1]));
+    inv = fp_mul(inv, n);
+  }
+  st(0, inv);
+}
 // x^z by the uncompressed chain (pairing.h cyc_exp_z's fallback)
 DGI Fp12 ck_exp_plain(const Fp12& a) {
   Fp12 acc = a;
@@ -328,7 +348,6 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_ck_sub(uint32_t G, uint3
 // the weighted sums (group_combine)
 // (g2m != null: the G2 sum of a group is left to k_ck_tab_* / k_ck_sac / k_ck_bfin -- g2m[g] = 1 and dig[g] its
 // column digits -- and so is np)
-template <bool kSplit>
 DGI void ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k, const uint64_t* seedp, const G1AStore* keys,
                  const uint32_t* item_slot, const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
                  uint32_t subgroup, unsigned long long* cnt, CkState* st, uint8_t* g2m, RsDigits* dig) {
@@ -342,7 +361,7 @@ DGI void ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k, co
   G2A b{fp2_zero(), fp2_zero(), true};
   CkState c;
   uint64_t rho[GRP];
-  const uint32_t nl = group_combine_t<!kSplit>(mem, n, *seedp, keys, item_slot, S, status, fin, subgroup, a, b, c.live, rho);
+  const uint32_t nl = group_combine(mem, n, *seedp, keys, item_slot, S, status, fin, subgroup, a, b, c.live, rho);
   c.round = mem[0] / k;
   c.n = n;
   c.nl = nl;
@@ -350,8 +369,8 @@ DGI void ck_prep(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k, co
     a = G1A{fp_zero(), fp_zero(), true};
     b = G2A{fp2_zero(), fp2_zero(), true};
   }
-  const bool later = kSplit && n > 1 && nl > 0;  // b from the table kernels
-  if (kSplit) {
+  const bool later = n > 1 && nl > 0;  // b from the table kernels
+  {
     g2m[g] = later ? 1 : 0;
     if (later) {
       const uint64_t d[4] = {rho[0], rho[1], rho[2], rho[3]};
@@ -368,47 +387,25 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep(uint32_t G, uint32_
                                                   const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
                                                   uint32_t subgroup, unsigned long long* cnt, CkState* st,
                                                   uint8_t* g2m, RsDigits* dig) {
-  ck_prep<true>(G, off, glist, k, seedp, keys, item_slot, hinf, S, status, fin, subgroup, cnt, st, g2m, dig);
-}
-// DG_CK_SPLIT=0 (A/B): the G2 sums in the lane as well (group_combine's Jacobian table in scratch)
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep_g2(uint32_t G, uint32_t off, const uint32_t* glist,
-                                                  uint32_t k, const uint64_t* seedp, const G1AStore* keys,
-                                                  const uint32_t* item_slot, const uint8_t* hinf, const G2AStore* S,
-                                                  uint8_t* status, uint8_t* fin, uint32_t subgroup,
-                                                  unsigned long long* cnt, CkState* st) {
-  ck_prep<false>(G, off, glist, k, seedp, keys, item_slot, hinf, S, status, fin, subgroup, cnt, st, nullptr, nullptr);
+  ck_prep(G, off, glist, k, seedp, keys, item_slot, hinf, S, status, fin, subgroup, cnt, st, g2m, dig);
 }
 // the lines of the pair (-g1, b): l2[s * G + g]
-DG_KERNEL void __launch_bounds__(64, DG_CK_L2_WAVES) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_L2_WAVES) k_ck_lines2(uint32_t G, const uint32_t* gcnt, const CkState* st,
+                                                                 CkLine* l2) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G || !(st[g].np & 2)) return;
+  if (ck_dead(g, G, gcnt) || !(st[g].np & 2)) return;
   const G2A b = load_g2a(st[g].b);
   ck_lines(b.x, b.y, [&](uint32_t s, const CkLine& l) { l2[(size_t)s * G + g] = l; });
 }
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
-  CkInv c;
-  nv[g] = ck_fe1(F[g], c);
-  inv[g] = c;
-}
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_inv(uint32_t G, const Fp12* F, const CkInv* inv, const Fp* nvinv,
-                                                 Fp12* out) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
-  out[g] = ck_inv(F[g], inv[g], nvinv[g]);
-}
 // the six compressed powers sn[i * G + g], their denominators' norms nv[i * G + g], zero[g]
 // (a lane with a zero denominator also appends itself to zl: zl[0] the count, zl[1..] the lanes; x = 1 -- the dead
-// checks, whose verdict k_ck_verdict ignores -- skips the chain: 1^z = 1, zero[g] = 2)
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero,
-                                                            uint32_t* zl) {
+// checks, whose verdict k_ck_final ignores -- skips the chain: 1^z = 1, zero[g] = 2)
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const uint32_t* gcnt, const Fp12* X, CycC* sn,
+                                                              Fp* nv, uint8_t* zero, uint32_t* zl) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
+  if (ck_dead(g, G, gcnt)) return;
   const Fp12 x = X[g];
-  if (fp12_is_one(x)) {  // 1^z = 1 (a check with no live member or no pair): zero = 2, norms 1 for the batch inversion
-#pragma unroll 1
-    for (int i = 0; i < CK_NPOW; ++i) nv[(size_t)i * G + g] = fp_one();
+  if (fp12_is_one(x)) {  // 1^z = 1 (a check with no live member or no pair)
     zero[g] = 2;
     return;
   }
@@ -419,14 +416,16 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const 
   zero[g] = z ? 1 : 0;
   if (z) zl[1 + atomicAdd(zl, 1u)] = g;
 }
-// the verdicts of the checks whose final exponentiation is res[g] (== 1: valid), written as verify_group writes them
-DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const Fp12* res, uint8_t* status,
+// the verdicts of the group / single checks of Recover's pass (good[g]: the check held, k_ck_final): a passed group
+// accepts its members (error probability <= 2^-63 each), a failed group sends them to their own checks (FIN_RECHECK),
+// a single check is kyber's bls.Verify verdict
+DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const uint8_t* good_, uint8_t* status,
                                                    uint8_t* fin) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   const CkState& c = st[g];
   if (c.nl == 0) return;
-  const bool good = c.np == 0 || fp12_is_one(res[g]);
+  const bool good = good_[g] != 0;
   if (c.n == 1) {
     status[c.live[0]] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
     fin[c.live[0]] = FIN_DONE;
@@ -444,28 +443,44 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep(uint32_t G, uint32_
                                                   const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
                                                   uint32_t subgroup, unsigned long long* cnt, CkState* st,
                                                   uint8_t* g2m, RsDigits* dig);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep_g2(uint32_t G, uint32_t off, const uint32_t* glist,
-                                                  uint32_t k, const uint64_t* seedp, const G1AStore* keys,
-                                                  const uint32_t* item_slot, const uint8_t* hinf, const G2AStore* S,
-                                                  uint8_t* status, uint8_t* fin, uint32_t subgroup,
-                                                  unsigned long long* cnt, CkState* st);
 DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_ck_sub(uint32_t G, uint32_t off, const uint32_t* glist,
                                                                 const G2AStore* S, uint8_t* status, uint8_t* fin);
-DG_KERNEL void __launch_bounds__(64, DG_CK_L2_WAVES) k_ck_lines2(uint32_t G, const CkState* st, CkLine* l2);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_fe1(uint32_t G, const Fp12* F, CkInv* inv, Fp* nv);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_inv(uint32_t G, const Fp12* F, const CkInv* inv, const Fp* nvinv,
-                                                 Fp12* out);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const Fp12* X, CycC* sn, Fp* nv, uint8_t* zero,
-                                                            uint32_t* zl);
-DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const Fp12* res, uint8_t* status,
+DG_KERNEL void __launch_bounds__(64, DG_CK_L2_WAVES) k_ck_lines2(uint32_t G, const uint32_t* gcnt, const CkState* st,
+                                                                 CkLine* l2);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const uint32_t* gcnt, const Fp12* X, CycC* sn,
+                                                              Fp* nv, uint8_t* zero, uint32_t* zl);
+DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const uint8_t* good_, uint8_t* status,
                                                    uint8_t* fin);
+#endif
+// (kernels_check_f.hip)
+#if DG_TU_CHECK == 6
+// the easy part of the final exponentiation: F2[g] = f1 frob^2(f1), f1 = f^-1 conj(f); f^-1 by ck_fe1 / ck_inv with the
+// one Fp inversion of the check in the lane (field.h fp_inv, safegcd) -- no batch inversion across the checks.  Lane 0
+// also empties the CK_NEXP work lists of k_ck_explain (zl + z (G + 1), z < CK_NEXP).
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_easy(uint32_t G, const uint32_t* gcnt, const Fp12* F, Fp12* F2,
+                                                            uint32_t* zl) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g == 0 && G)
+#pragma unroll 1
+    for (uint32_t z = 0; z < CK_NEXP; ++z) zl[(size_t)z * (G + 1)] = 0;
+  if (ck_dead(g, G, gcnt)) return;
+  const Fp12 f = F[g];
+  CkInv c;
+  const Fp n = ck_fe1(f, c);
+  const Fp12 f1 = ck_mul_op(ck_inv(f, c, fp_inv(n)), f, 0, 1);
+  F2[g] = ck_mul_op(f1, f1, 2, 0);
+}
+#else
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_easy(uint32_t G, const uint32_t* gcnt, const Fp12* F, Fp12* F2,
+                                                            uint32_t* zl);
 #endif
 // the Miller value of every check (kernels_check_b.hip)
 #if DG_TU_CHECK == 2
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, uint32_t R, const CkState* st, const CkLine* rl,
-                                                    const CkLine* l2, Fp12* F) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, const uint32_t* gcnt, uint32_t R,
+                                                              const CkState* st, const CkLine* rl, const CkLine* l2,
+                                                              Fp12* F) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
+  if (ck_dead(g, G, gcnt)) return;
   const uint32_t np = st[g].np, r = st[g].round;
   const Fp ax = st[g].a.x, ay = st[g].a.y;
   F[g] = ck_miller(np, ax, ay, [&](uint32_t s, uint32_t pair) {
@@ -473,40 +488,48 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, uint32
   });
 }
 #else
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, uint32_t R, const CkState* st, const CkLine* rl,
-                                                    const CkLine* l2, Fp12* F);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, const uint32_t* gcnt, uint32_t R,
+                                                              const CkState* st, const CkLine* rl, const CkLine* l2,
+                                                              Fp12* F);
 #endif
-// out = a * frob^nfrob(b), conjugated if `conj` (kernels_check_c.hip)
+// the end of final_exp_cubed and the check's verdict (kernels_check_c.hip): T = (a^z)^z frob^2(a) (k_ck_expdec's
+// product), b = T conj(a), c = f2^3, good[g] = (no pair, or b c == 1)
 #if DG_TU_CHECK == 3
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_mul(uint32_t G, const Fp12* A, const Fp12* B, uint32_t nfrob, uint32_t conj,
-                                                 Fp12* out) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_final(uint32_t G, const uint32_t* gcnt, const CkState* st,
+                                                             const Fp12* T, const Fp12* A, const Fp12* F2, uint8_t* good) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
-  out[g] = ck_mul_op(A[g], B[g], nfrob, conj);
+  if (ck_dead(g, G, gcnt)) return;
+  const Fp12 c = ck_mul_op(ck_mul_op(F2[g], F2[g], 0, 0), F2[g], 0, 0);
+  const Fp12 res = ck_mul_op(ck_mul_op(T[g], A[g], 0, 1), c, 0, 0);
+  good[g] = st[g].np == 0 || fp12_is_one(res) ? 1 : 0;
 }
 #else
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_mul(uint32_t G, const Fp12* A, const Fp12* B, uint32_t nfrob, uint32_t conj,
-                                                 Fp12* out);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_final(uint32_t G, const uint32_t* gcnt, const CkState* st,
+                                                             const Fp12* T, const Fp12* A, const Fp12* F2, uint8_t* good);
 #endif
-// x^z from the compressed powers (kernels_check_d.hip); lanes whose chain hit a zero denominator are left to
-// k_ck_explain
+// x^z from the compressed powers (kernels_check_d.hip): the six norms inverted in the lane (ck_inv6, in place), the
+// decompressed product, then out[g] = x^z op(Y[g]) when Y is given (op: frob^nfrob, then conj if `conj` -- the hard
+// part's next factor, ck_mul_op); lanes whose chain hit a zero denominator are left to k_ck_explain
 #if DG_TU_CHECK == 4
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expdec(uint32_t G, const CycC* sn, const Fp* nvinv, const uint8_t* zero,
-                                                    Fp12* XZ) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expdec(uint32_t G, const uint32_t* gcnt, const CycC* sn, Fp* nv,
+                                                              const uint8_t* zero, const Fp12* Y, uint32_t nfrob,
+                                                              uint32_t conj, Fp12* out) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G || zero[g] == 1) return;
-  if (zero[g] == 2) {  // x = 1 (k_ck_expsq)
-    XZ[g] = fp12_one();
-    return;
+  if (ck_dead(g, G, gcnt) || zero[g] == 1) return;
+  Fp12 x = fp12_one();  // x = 1 (zero[g] == 2, k_ck_expsq)
+  if (zero[g] == 0) {
+    ck_inv6([&](int i) { return nv[(size_t)i * G + g]; }, [&](int i, const Fp& v) { nv[(size_t)i * G + g] = v; });
+    x = ck_expdec([&](int i, CycC& c, Fp& n) {
+      c = sn[(size_t)i * G + g];
+      n = nv[(size_t)i * G + g];
+    });
   }
-  XZ[g] = ck_expdec([&](int i, CycC& c, Fp& n) {
-    c = sn[(size_t)i * G + g];
-    n = nvinv[(size_t)i * G + g];
-  });
+  out[g] = Y ? ck_mul_op(x, Y[g], nfrob, conj) : x;
 }
 #else
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expdec(uint32_t G, const CycC* sn, const Fp* nvinv, const uint8_t* zero,
-                                                    Fp12* XZ);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expdec(uint32_t G, const uint32_t* gcnt, const CycC* sn, Fp* nv,
+                                                              const uint8_t* zero, const Fp12* Y, uint32_t nfrob,
+                                                              uint32_t conj, Fp12* out);
 #endif
 // x^z by the uncompressed chain for the lanes with a zero Karabina denominator (kernels_check_e.hip)
 // over the work list zl (k_ck_expsq) with a fixed grid of CK_EXPLAIN_LANES lanes striding it; every lane exits when
@@ -578,11 +601,13 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_bfin(uint32_t G, const u
   const G1A a = load_g1a(st[g].a);
   st[g].np = ((!a.inf && !hinf[st[g].round]) ? 1u : 0u) | (!b.inf ? 2u : 0u);
 }
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(const uint32_t* zl, const Fp12* X, Fp12* XZ) {
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(const uint32_t* zl, const Fp12* X, const Fp12* Y,
+                                                               uint32_t nfrob, uint32_t conj, Fp12* out) {
   const uint32_t n = zl[0];
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
     const uint32_t g = zl[1 + j];
-    XZ[g] = ck_exp_plain(X[g]);
+    const Fp12 x = ck_exp_plain(X[g]);
+    out[g] = Y ? ck_mul_op(x, Y[g], nfrob, conj) : x;
   }
 }
 #else
@@ -596,7 +621,8 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_sac(uint32_t G, const ui
                                                            const uint4* T4, const uint8_t* tinf, G2JStore* bj, Fp* bn);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_bfin(uint32_t G, const uint8_t* g2m, const G2JStore* bj,
                                                             const Fp* bni, const uint8_t* hinf, CkState* st);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(const uint32_t* zl, const Fp12* X, Fp12* XZ);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(const uint32_t* zl, const Fp12* X, const Fp12* Y,
+                                                               uint32_t nfrob, uint32_t conj, Fp12* out);
 #endif
 #endif
 

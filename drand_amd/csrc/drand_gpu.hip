@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <mutex>
 #include <random>
 #include <string>
@@ -39,14 +40,12 @@ constexpr int kSets = DG_MAX_SETS;  // capacity; DG_SETS (environment) overrides
 // The workspace plan for a hardware queue count (GPU_MAX_HW_QUEUES; HIP's default 4).  HIP binds streams to queues as
 // they first dispatch (1, 2, 3, 4, 4, 3, 2, 1, 4, 3, ... on the box), a queue runs its streams' kernels one after
 // another, and a cross-stream wait queued on a shared queue stalls every stream behind it:
-//   >= 12 queues: 10 sets, the per-item kernels on their own stream (its queue alone reserves their ~15 KB scratch);
-//   5..11 queues: queues - 2 sets and the per-item stream, so no two library streams share a queue (the caller keeps
-//                 one); the per-item kernels cannot go on the set streams here -- every queue would reserve their
-//                 scratch, and 8 such queues failed dg_init with HSA_STATUS_ERROR_OUT_OF_RESOURCES;
-//   <= 4 queues:  a multiple of the queue count (8 at 4), each queue carrying the same share of batches, and the
-//                 per-item kernels on each set's own stream (no hand-over barriers; 4 queues reserve their scratch
-//                 fine).  Headline at 4 queues: 10 sets with the hop 8.7 M rounds/s, without it 11.1 M, 8 sets 12.0 M.
-void queue_plan(int hwq, int* sets, int* shared_fb) {
+//   >= 12 queues: 10 sets;  5..11 queues: queues - 2 sets (no two library streams share a queue, the caller keeps
+//   one);  <= 4 queues: a multiple of the queue count (8 at 4), each queue carrying the same share of batches.
+// The per-item passes (the check pipeline, checks.h / xr.h: every kernel under ~4 KB of private segment) run on the
+// batch's own stream at every queue count (*per_item_on_set = 1); only the fixture kernels k_sign / k_hash_to_g2
+// (~5.4 KB) keep a stream of their own, so no workspace queue reserves their scratch.
+void queue_plan(int hwq, int* sets, int* per_item_on_set) {
   if (hwq < 1) hwq = 4;
   int v;
   if (hwq >= 12)
@@ -57,7 +56,7 @@ void queue_plan(int hwq, int* sets, int* shared_fb) {
     v = (10 / hwq) * hwq;
   v = v < 1 ? 1 : (v > kSets ? kSets : v);
   *sets = v;
-  *shared_fb = hwq <= 4 && hwq < v + 2 ? 1 : 0;
+  *per_item_on_set = 1;
 }
 int env_hw_queues() {
   const char* q = getenv("GPU_MAX_HW_QUEUES");
@@ -88,7 +87,6 @@ struct Set {
   std::vector<void*> pool;  // indexed by Slot
   std::vector<size_t> pool_size;
   hipEvent_t done = nullptr;
-  hipEvent_t to_fb = nullptr, from_fb = nullptr;  // hand-over to / back from the per-item stream
   bool busy = false;
 };
 
@@ -108,19 +106,11 @@ struct Ctx {
   int device = -1;
   bool ready = false;
   Set sets[kSets];
-  // The per-item pairing kernels (k_verify_items, k_verify_groups: ~14.5 KB of private segment per lane) run on
-  // this one stream, whatever set the batch uses: a hardware queue reserves scratch for the largest private
-  // segment dispatched on it, so only this stream's queue holds that reservation and the workspace sets'
-  // queues stay at the ~5.7 KB of k_sign (with 8 hardware queues, every queue holding 14.5 KB failed
-  // with HSA_STATUS_ERROR_OUT_OF_RESOURCES).  Only failed or isolating batches reach it.
+  // the fixture kernels k_sign / k_hash_to_g2 (~5.4 KB of private segment per lane, the largest of the library) run
+  // on this stream of their own: a hardware queue reserves scratch for the largest private segment dispatched on it,
+  // for every wave the device can hold, so the workspace queues stay at the check pipeline's ~4 KB (12 workspace
+  // queues at 5.7 KB each failed dg_init with HSA_STATUS_ERROR_OUT_OF_RESOURCES)
   hipStream_t fb_stream = nullptr;
-  // shared_fb: the per-item kernels on the batch's own stream instead, every workspace queue prewarmed with their
-  // private segment.  Chosen in dg_init by the hardware queue count (GPU_MAX_HW_QUEUES, HIP's default 4): with fewer
-  // queues than the active sets' streams + the per-item stream + one for the caller, streams share queues, and the
-  // per-item stream's two cross-stream barriers per batch then stall whatever stream shares their queue (headline
-  // at 4 queues, 10 sets: 8.7 M rounds/s with the hop, 11.1 M without; at 16 queues the hop is free and keeps the
-  // large scratch reservation on one queue).  DG_SHARED_FB=0 / 1 forces either.
-  bool shared_fb = false;
   hipStream_t last_stream = nullptr;  // the set stream of the last asynchronous batch (dg_last_batch_stream)
   int cur = 0, next = 0;
   bool timing = false;
@@ -136,7 +126,8 @@ struct Ctx {
   uint8_t pk_bytes[48];
   bool pk_valid = false;
   unsigned long long* fallbacks = nullptr;  // device counter (k_count_fallback)
-  unsigned long long* gcount = nullptr;     // device counters: group checks by member count (k_verify_groups)
+  unsigned long long* gcount = nullptr;     // device counters: group checks by member count (checks.h k_ck_prep)
+  unsigned long long* xrcount = nullptr;    // device counters: cross-round isolation checks by level (xr.h)
   // share keys X_i = PubPoly.Eval(i) of the multi-key paths for the last (commits, distinct indices):
   // a drand group verifies every round against the same polynomial (the reference's build caches X_i
   // per group too), and decode + Horner are latency-bound single-lane jobs of ~15 ms
@@ -208,9 +199,9 @@ enum Slot {
   S_IDXCNT, S_IDXFIRST, S_SLOTOF, S_MSM_AFF, S_MSM_DEN, S_MSM_DINV, S_BINV_PRE, S_BINV_ROOTS, S_RC_UNI, S_RC_REF, S_RC_LIST, S_RS_DIG,
   S_RC_NAF, S_RC_EV, S_RC_TAB, S_RC_D, S_RC_PINF, S_RC_DEN, S_RC_A, S_PW, S_SLOTW, S_SFULL, S_STFULL, S_INC, S_PB, S_SLOTB,
   S_SEED2, S_SB, S_STB, S_ISOB, S_KMSM_GOFS, S_KMSM_BP, S_KMSM_BT2,
-  S_CK_RL, S_CK_HINF, S_CK_ST, S_CK_L2, S_CK_F, S_CK_T0, S_CK_T1, S_CK_T2, S_CK_F2, S_CK_A, S_CK_XZA, S_CK_XZB,
-  S_CK_INV, S_CK_NV, S_CK_NVI, S_CK_SN, S_CK_ZERO, S_CK_ZL, S_CK_T4, S_CK_TINF, S_CK_DIG, S_CK_TDEN, S_CK_BJ,
-  S_CK_BN, S_CK_G2M, S_KOK, S_COUNT
+  S_CK_RL, S_CK_HINF, S_CK_ST, S_CK_L2, S_CK_F, S_CK_T0, S_CK_T1, S_CK_F2, S_CK_A, S_CK_NV, S_CK_SN, S_CK_ZERO,
+  S_CK_ZL, S_CK_GOOD, S_CK_T4, S_CK_TINF, S_CK_DIG, S_CK_TDEN, S_CK_BJ, S_CK_BN, S_CK_G2M, S_KOK, S_XR_CNT, S_XR_CAND,
+  S_XR_QS, S_XR_T4, S_XR_TINF, S_XR_L2, S_XR_L3, S_XR_HS, S_XR_RL, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -420,11 +411,6 @@ struct BatchOut {
 // D = a SHA-256 tree over every (message, signature record) of the batch, left on the device.
 int bind_seed(const Batch& b, uint64_t seed, hipStream_t st, uint64_t** d_seed, Slot seed_slot = S_SEED) {
   const uint32_t N = b.R * b.k;
-  static const bool no_bind = getenv("DG_NO_BIND") != nullptr;  // A/B diagnostics of the binding's cost only
-  if (no_bind) {
-    RET(wsT(seed_slot, 16, d_seed));
-    return launch("k_store_seed", k_store_seed, 1, 64, st, seed, *d_seed);
-  }
   Sha256 h;
   sha256_init(h);
   for (int i = 7; i >= 0; --i) sha256_byte(h, (uint8_t)(seed >> (8 * i)));
@@ -454,6 +440,14 @@ int bind_seed(const Batch& b, uint64_t seed, hipStream_t st, uint64_t** d_seed, 
 // over the rounds with active[r] != 0.  With `test_windows` side A also gets the MSM_TWIN test windows of
 // the batched subgroup check; *win = its MSM_WT window sums (checked beside the Miller loops, k_pair_miller_coop).
 int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st);
+
+// the per-item passes after a batch equation (defined with the check pipeline below)
+constexpr uint32_t kXrSeg = 131072;  // items per cross-round isolation run at most (bounded per-check workspace)
+int xr_isolate(uint32_t i0, uint32_t n, const uint32_t* flag, const uint64_t* seed, const G1AStore* keys,
+               const G2JStore* Q, const G2AStore* S, uint8_t* status, hipStream_t st);
+int prefix_pass(uint32_t R, uint32_t k, uint32_t t, int passes, const uint64_t* seed, const G1AStore* keys,
+                const uint32_t* item_slot, const G2JStore* Q, const G2AStore* S, uint8_t* status, uint8_t* fin,
+                uint32_t subgroup, hipStream_t st);
 
 // `affine`: every point of PA and PB has Z = 1 or Z = 0, so the first levels are affine additions (msm.h).
 // `bad` (device, affine only): raised when an input breaks that precondition (msm.h aff_input_ok); the caller
@@ -723,25 +717,27 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
     out->batched_sub = batched_sub;
     return 0;
   }
-  // the per-item pass on the per-item stream (g_ctx.fb_stream), ordered after and before this set's stream, or on
-  // the set's own stream (shared_fb); the per-round H_r = h_eff(Q_r) there too (k_clear_rounds: ~5 KB of private
-  // segment, kept off the set streams unless shared_fb)
-  G2AStore* H;
-  RET(wsT(S_H, b.R, &H));
-  Set& set = cur_set();
-  const hipStream_t batch_st = st;
-  if (!g_ctx.shared_fb) {
-    HIPCHK(hipEventRecord(set.to_fb, batch_st));
-    st = g_ctx.fb_stream;
-    HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
-  }
-  RET(launch("k_clear_rounds", k_clear_rounds, b.R, 128, st, b.R, (const uint32_t*)flag, b.Q, H));
-  RET(launch_shm("k_verify_items", k_verify_items, N, 64, verify_lds(), st, N, b.k, (const uint32_t*)flag, b.keys, b.item_slot,
-             (const G2AStore*)H, (const G2AStore*)b.S, (const uint8_t*)iso, b.status, batched_sub));
-  if (!g_ctx.shared_fb) {
-    HIPCHK(hipEventRecord(set.from_fb, st));
-    st = batch_st;
-    HIPCHK(hipStreamWaitEvent(st, set.from_fb, 0));
+  if (b.nslots == 1 && b.k == 1 && !b.item_slot) {
+    // one key, one item per round (VerifyBeacon / VerifyRecovered): a failed batch isolates its bad rounds by group
+    // tests across rounds (xr.h), enqueued whole and decided on the device, so asynchronous batches stay asynchronous
+    for (uint32_t i0 = 0; i0 < N; i0 += kXrSeg)
+      RET(xr_isolate(i0, std::min(kXrSeg, N - i0), flag, seed, b.keys, b.Q, b.S, b.status, st));
+  } else {
+    // several keys (VerifyPartial, a blocking entry point): the items the equation did not decide -- every decoded
+    // item of a failed batch, the isolated ones of a passed batch -- take the group-test passes of checks.h (groups of
+    // up to GRP items of a round, then every failed group's members alone; t = k + 1: no round stops early)
+    uint8_t* fin;
+    uint32_t* inc;
+    RET(wsT(S_FIN, N, &fin));
+    RET(wsT(S_INC, 4, &inc));
+    HIPCHK(hipMemsetAsync(inc, 0, 4, st));
+    RET(launch("k_window_fin", k_window_fin, N, 256, st, b.R, b.k, 0u, b.k, (const uint32_t*)flag, (const uint8_t*)iso,
+               (const uint8_t*)b.status, b.status, fin, inc));
+    uint32_t inc_h = 0;
+    HIPCHK(hipMemcpyAsync(&inc_h, inc, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (inc_h)
+      RET(prefix_pass(b.R, b.k, b.k + 1, 1, seed, b.keys, b.item_slot, b.Q, b.S, b.status, fin, batched_sub, st));
   }
   RET(launch("k_count_fallback", k_count_fallback, 1, 64, st, (const uint32_t*)flag, g_ctx.fallbacks));
   return 0;
@@ -1016,49 +1012,37 @@ int verify_partials_dev(const uint8_t* commits48, uint32_t t, uint32_t R, const 
 // statuses Recover reads are exact.  Up to GRP fresh items of a round are checked together (kernels.h
 // verify_group); the members of a failed group, and everything in the last pass, are checked alone.  DG_GROUP=1
 // checks every item alone.  fin: FIN_DONE for the final verdicts, FIN_PENDING for the rest.
-// The pairing-check pipeline of checks.h over the G checks glist[4 + 4 (off + g)] of one pass (G <= CK_CHUNK):
-// members and weighted sums, the (-g1, b) lines, the Miller values against the per-round lines rl, the final
-// exponentiation in pieces (one batch inversion for the easy part, one per x^z for the compressed squarings'
-// denominators), the verdicts.  Every buffer is the current set's workspace, sized for CK_CHUNK checks.
+// The pairing-check pipeline of checks.h: per-check workspace of the current set, sized for the G checks of the launch
+// at hand (grow-only slots: a small call allocates little).
 struct CkBufs {
   CkState* st;
   CkLine* l2;
-  Fp12 *F, *T0, *T1, *T2, *F2, *A, *XZa, *XZb;
-  CkInv* inv;
-  Fp *nv, *nvi;
+  Fp12 *F, *F2, *T0, *T1, *A;
+  Fp* nv;
   CycC* sn;
-  uint8_t* zero;
-  uint32_t* zl;  // [0] = count, then the checks with a zero Karabina denominator (k_ck_explain's work list)
-  // the split G2 sums (checks.h k_ck_tab_* / k_ck_sac / k_ck_bfin)
+  uint8_t *zero, *good;
+  uint32_t* zl;  // CK_NEXP work lists of k_ck_explain, (G + 1) words each: [0] = count, then the checks
+  // the split G2 sums of Recover's group checks (checks.h k_ck_tab_* / k_ck_sac / k_ck_bfin)
   uint4* T4;
   uint8_t *tinf, *g2m;
   RsDigits* dig;
   Fp *tden, *bn;
   G2JStore* bj;
 };
-// DG_CK_SPLIT=0 (A/B only): the G2 sums of group checks inside k_ck_prep (group_combine, Jacobian table in scratch)
-bool ck_split() {
-  static const bool v = env_int("DG_CK_SPLIT", 1) != 0;
-  return v;
-}
-int ck_bufs(CkBufs& b) {
-  const size_t G = CK_CHUNK;
+int ck_bufs(CkBufs& b, size_t G, bool group_sums) {
   RET(wsT(S_CK_ST, G, &b.st));
   RET(wsT(S_CK_L2, (size_t)CK_STEPS * G, &b.l2));
   RET(wsT(S_CK_F, G, &b.F));
+  RET(wsT(S_CK_F2, G, &b.F2));
   RET(wsT(S_CK_T0, G, &b.T0));
   RET(wsT(S_CK_T1, G, &b.T1));
-  RET(wsT(S_CK_T2, G, &b.T2));
-  RET(wsT(S_CK_F2, G, &b.F2));
   RET(wsT(S_CK_A, G, &b.A));
-  RET(wsT(S_CK_XZA, G, &b.XZa));
-  RET(wsT(S_CK_XZB, G, &b.XZb));
-  RET(wsT(S_CK_INV, G, &b.inv));
   RET(wsT(S_CK_NV, CK_NPOW * G, &b.nv));
-  RET(wsT(S_CK_NVI, CK_NPOW * G, &b.nvi));
   RET(wsT(S_CK_SN, CK_NPOW * G, &b.sn));
-  RET(wsT(S_CK_ZL, G + 1, &b.zl));
-  if (ck_split()) {
+  RET(wsT(S_CK_ZERO, G, &b.zero));
+  RET(wsT(S_CK_GOOD, G, &b.good));
+  RET(wsT(S_CK_ZL, CK_NEXP * (G + 1), &b.zl));
+  if (group_sums) {
     RET(wsT(S_CK_T4, 8 * RC_Q * G, &b.T4));
     RET(wsT(S_CK_TINF, 8 * G, &b.tinf));
     RET(wsT(S_CK_DIG, G, &b.dig));
@@ -1067,77 +1051,104 @@ int ck_bufs(CkBufs& b) {
     RET(wsT(S_CK_BN, 2 * G, &b.bn));
     RET(wsT(S_CK_G2M, G, &b.g2m));
   }
-  return wsT(S_CK_ZERO, G, &b.zero);
+  return 0;
 }
-// XZ = X^z (pairing.h cyc_exp_z): the compressed chain, one batch inversion of the 6 G denominators' norms, the
-// decompressed product; the uncompressed chain for the lanes with a zero denominator
-// (the uncompressed chain runs over a device-built work list in CK_EXPLAIN_LANES lanes: it is rare, and a launch of G
-// lanes that mostly return cost ~1 ms at one wave per SIMD)
-int ck_expz(uint32_t G, const Fp12* X, Fp12* XZ, const CkBufs& b, hipStream_t st) {
-  HIPCHK(hipMemsetAsync(b.zl, 0, 4, st));
-  RET(launch("k_ck_expsq", k_ck_expsq, G, 64, st, G, X, b.sn, b.nv, b.zero, b.zl));
-  RET(batch_inv(CK_NPOW * G, b.nv, b.nvi, st));
-  RET(launch("k_ck_expdec", k_ck_expdec, G, 64, st, G, (const CycC*)b.sn, (const Fp*)b.nvi, (const uint8_t*)b.zero, XZ));
-  return launch("k_ck_explain", k_ck_explain, CK_EXPLAIN_LANES, 64, st, (const uint32_t*)b.zl, X, XZ);
+// X^z (pairing.h cyc_exp_z) times the hard part's next factor: the compressed chain (k_ck_expsq), the decompressed
+// product with the six norms inverted in the lane (k_ck_expdec), the uncompressed chain for the lanes with a zero
+// denominator (k_ck_explain over work list z, CK_EXPLAIN_LANES lanes: it is rare); out = X^z op(Y) (Y may be null)
+int ck_expz(uint32_t z, uint32_t G, const uint32_t* gcnt, const Fp12* X, const Fp12* Y, uint32_t nfrob, uint32_t conj,
+            Fp12* out, const CkBufs& b, hipStream_t st) {
+  uint32_t* zl = b.zl + (size_t)z * (G + 1);
+  RET(launch("k_ck_expsq", k_ck_expsq, G, 64, st, G, gcnt, X, b.sn, b.nv, b.zero, zl));
+  RET(launch("k_ck_expdec", k_ck_expdec, G, 64, st, G, gcnt, (const CycC*)b.sn, b.nv, (const uint8_t*)b.zero, Y, nfrob,
+             conj, out));
+  return launch("k_ck_explain", k_ck_explain, CK_EXPLAIN_LANES, 64, st, (const uint32_t*)zl, X, Y, nfrob, conj, out);
 }
-// out = a * frob^nfrob(b) (conjugated first if conj)
-int ck_mul(uint32_t G, const Fp12* a, const Fp12* b, uint32_t nfrob, uint32_t conj, Fp12* out, hipStream_t st) {
-  return launch("k_ck_mul", k_ck_mul, G, 64, st, G, a, b, nfrob, conj, out);
+// The checks b.st[0..G) (pair 0: (a, the lines rl[s R + round]), pair 1: (-g1, b)) -> b.good: the (-g1, b) lines, the
+// Miller values, the final exponentiation (k_ck_easy, five x^z with their next factors, k_ck_final).  Every kernel is
+// one lane per check without exchange, so gcnt (device, may be null) gates the lanes of a launch sized for G.
+int run_checks(uint32_t G, const uint32_t* gcnt, uint32_t R, const CkLine* rl, const CkBufs& b, hipStream_t st) {
+  RET(launch("k_ck_lines2", k_ck_lines2, G, 64, st, G, gcnt, (const CkState*)b.st, b.l2));
+  RET(launch("k_ck_miller", k_ck_miller, G, 64, st, G, gcnt, R, (const CkState*)b.st, rl, (const CkLine*)b.l2, b.F));
+  RET(launch("k_ck_easy", k_ck_easy, G, 64, st, G, gcnt, (const Fp12*)b.F, b.F2, b.zl));
+  // hard part (final_exp_cubed): t0 = f2^z conj(f2), t1 = t0^z conj(t0), a = t1^z frob(t1),
+  // b = (a^z)^z frob^2(a) conj(a), c = f2^3, result b c
+  RET(ck_expz(0, G, gcnt, b.F2, b.F2, 0, 1, b.T0, b, st));
+  RET(ck_expz(1, G, gcnt, b.T0, b.T0, 0, 1, b.T1, b, st));
+  RET(ck_expz(2, G, gcnt, b.T1, b.T1, 1, 0, b.A, b, st));
+  RET(ck_expz(3, G, gcnt, b.A, nullptr, 0, 0, b.T0, b, st));
+  RET(ck_expz(4, G, gcnt, b.T0, b.A, 2, 0, b.T1, b, st));
+  return launch("k_ck_final", k_ck_final, G, 64, st, G, gcnt, (const CkState*)b.st, (const Fp12*)b.T1,
+                (const Fp12*)b.A, (const Fp12*)b.F2, b.good);
 }
+// Recover's / VerifyPartial's group checks glist[4 + 4 (off + g)] of one pass (G <= CK_CHUNK): members and weighted
+// sums, the checks, the verdicts
 int check_chunk(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k, uint32_t R, const uint64_t* seed,
                 const G1AStore* keys, const uint32_t* item_slot, const uint8_t* hinf, const CkLine* rl, const G2AStore* S,
                 uint8_t* status, uint8_t* fin, uint32_t subgroup, hipStream_t st) {
   CkBufs b;
-  RET(ck_bufs(b));
-  static const bool sub_inline = getenv("DG_CK_SUB_INLINE") != nullptr;  // A/B: subgroup checks inside k_ck_prep
-  if (subgroup && !sub_inline)
-    RET(launch("k_ck_sub", k_ck_sub, 4 * G, 64, st, G, off, glist, (const G2AStore*)S, status, fin));
-  const bool split = ck_split();
-  if (split)
-    RET(launch("k_ck_prep", k_ck_prep, G, 64, st, G, off, glist, k, seed, keys, item_slot, hinf, S, status, fin,
-               sub_inline ? subgroup : 0u, g_ctx.gcount, b.st, b.g2m, b.dig));
-  else
-    RET(launch("k_ck_prep", k_ck_prep_g2, G, 64, st, G, off, glist, k, seed, keys, item_slot, hinf, S, status, fin,
-               sub_inline ? subgroup : 0u, g_ctx.gcount, b.st));
-  if (split) {
-    Fp *den = b.tden, *dinv = b.tden + 3 * (size_t)G;
-    for (uint32_t l = 0; l < 3; ++l) {
-      RET(launch("k_ck_tab_den", k_ck_tab_den, 3 * G, 64, st, l, G, (const CkState*)b.st, (const uint8_t*)b.g2m,
-                 S, b.T4, b.tinf, den));
-      RET(batch_inv(3 * G, den, dinv, st));
-      RET(launch("k_ck_tab_add", k_ck_tab_add, 3 * G, 64, st, l, G, (const CkState*)b.st, (const uint8_t*)b.g2m,
-                 S, b.T4, b.tinf, (const Fp*)dinv));
-    }
-    RET(launch("k_ck_sac", k_ck_sac, G, 64, st, G, (const uint8_t*)b.g2m, (const RsDigits*)b.dig, (const uint4*)b.T4,
-               (const uint8_t*)b.tinf, b.bj, b.bn));
-    RET(batch_inv(G, b.bn, b.bn + G, st));
-    RET(launch("k_ck_bfin", k_ck_bfin, G, 64, st, G, (const uint8_t*)b.g2m, (const G2JStore*)b.bj,
-               (const Fp*)(b.bn + G), hinf, b.st));
+  RET(ck_bufs(b, G, true));
+  if (subgroup) RET(launch("k_ck_sub", k_ck_sub, 4 * G, 64, st, G, off, glist, (const G2AStore*)S, status, fin));
+  RET(launch("k_ck_prep", k_ck_prep, G, 64, st, G, off, glist, k, seed, keys, item_slot, hinf, S, status, fin, 0u,
+             g_ctx.gcount, b.st, b.g2m, b.dig));
+  Fp *den = b.tden, *dinv = b.tden + 3 * (size_t)G;
+  for (uint32_t l = 0; l < 3; ++l) {
+    RET(launch("k_ck_tab_den", k_ck_tab_den, 3 * G, 64, st, l, G, (const CkState*)b.st, (const uint8_t*)b.g2m, S, b.T4,
+               b.tinf, den));
+    RET(batch_inv(3 * G, den, dinv, st));
+    RET(launch("k_ck_tab_add", k_ck_tab_add, 3 * G, 64, st, l, G, (const CkState*)b.st, (const uint8_t*)b.g2m, S, b.T4,
+               b.tinf, (const Fp*)dinv));
   }
-  RET(launch("k_ck_lines2", k_ck_lines2, G, 64, st, G, (const CkState*)b.st, b.l2));
-  RET(launch("k_ck_miller", k_ck_miller, G, 64, st, G, R, (const CkState*)b.st, rl, (const CkLine*)b.l2, b.F));
-  // easy part: f1 = f^-1 conj(f), f2 = f1 frob^2(f1)
-  RET(launch("k_ck_fe1", k_ck_fe1, G, 64, st, G, (const Fp12*)b.F, b.inv, b.nv));
-  RET(batch_inv(G, b.nv, b.nvi, st));
-  RET(launch("k_ck_inv", k_ck_inv, G, 64, st, G, (const Fp12*)b.F, (const CkInv*)b.inv, (const Fp*)b.nvi, b.T0));
-  RET(ck_mul(G, b.T0, b.F, 0, 1, b.T1, st));
-  RET(ck_mul(G, b.T1, b.T1, 2, 0, b.F2, st));
-  // hard part (final_exp_cubed): t0 = f2^z conj(f2), t1 = t0^z conj(t0), a = t1^z frob(t1),
-  // b = (a^z)^z frob^2(a) conj(a), c = f2^3, result b c
-  RET(ck_expz(G, b.F2, b.XZa, b, st));
-  RET(ck_mul(G, b.XZa, b.F2, 0, 1, b.T0, st));
-  RET(ck_expz(G, b.T0, b.XZa, b, st));
-  RET(ck_mul(G, b.XZa, b.T0, 0, 1, b.T1, st));
-  RET(ck_expz(G, b.T1, b.XZa, b, st));
-  RET(ck_mul(G, b.XZa, b.T1, 1, 0, b.A, st));
-  RET(ck_expz(G, b.A, b.XZa, b, st));
-  RET(ck_expz(G, b.XZa, b.XZb, b, st));
-  RET(ck_mul(G, b.XZb, b.A, 2, 0, b.T0, st));
-  RET(ck_mul(G, b.T0, b.A, 0, 1, b.T1, st));
-  RET(ck_mul(G, b.F2, b.F2, 0, 0, b.T0, st));
-  RET(ck_mul(G, b.T0, b.F2, 0, 0, b.T2, st));
-  RET(ck_mul(G, b.T1, b.T2, 0, 0, b.T0, st));
-  return launch("k_ck_verdict", k_ck_verdict, G, 128, st, G, (const CkState*)b.st, (const Fp12*)b.T0, status, fin);
+  RET(launch("k_ck_sac", k_ck_sac, G, 64, st, G, (const uint8_t*)b.g2m, (const RsDigits*)b.dig, (const uint4*)b.T4,
+             (const uint8_t*)b.tinf, b.bj, b.bn));
+  RET(batch_inv(G, b.bn, b.bn + G, st));
+  RET(launch("k_ck_bfin", k_ck_bfin, G, 64, st, G, (const uint8_t*)b.g2m, (const G2JStore*)b.bj, (const Fp*)(b.bn + G),
+             hinf, b.st));
+  RET(run_checks(G, nullptr, R, rl, b, st));
+  return launch("k_ck_verdict", k_ck_verdict, G, 128, st, G, (const CkState*)b.st, (const uint8_t*)b.good, status, fin);
+}
+
+// Cross-round isolation of a failed single-key batch (xr.h): items [i0, i0 + n) of the batch (its status, decoded S,
+// uncleared hashes Q, the group key keys[0]), levels of group tests on the device, no host round trip; after a passed
+// batch every launch returns at once.  At most kXrSeg items per run, so the per-check workspace stays bounded.
+uint32_t xr_qpg() {
+  static const uint32_t v = (uint32_t)std::max(1, std::min(64, env_int("DG_XR_QPG", (int)XR_QPG)));
+  return v;
+}
+int xr_isolate(uint32_t i0, uint32_t n, const uint32_t* flag, const uint64_t* seed, const G1AStore* keys,
+               const G2JStore* Q, const G2AStore* S, uint8_t* status, hipStream_t st) {
+  const uint32_t qpg = xr_qpg(), nqmax = (n + 3) / 4, G1 = (nqmax + qpg - 1) / qpg;
+  uint32_t *cnt, *cand, *l2, *l3;
+  G2JStore *QS, *HS;
+  uint4* T4;
+  uint8_t* tinf;
+  CkLine* rl;
+  CkBufs b;
+  RET(wsT(S_XR_CNT, XR_NCNT, &cnt));
+  RET(wsT(S_XR_CAND, n, &cand));
+  RET(wsT(S_XR_L2, nqmax, &l2));
+  RET(wsT(S_XR_L3, n, &l3));
+  RET(wsT(S_XR_QS, 2 * (size_t)nqmax, &QS));
+  RET(wsT(S_XR_T4, (size_t)8 * RC_Q * 2 * nqmax, &T4));
+  RET(wsT(S_XR_TINF, (size_t)8 * 2 * nqmax, &tinf));
+  RET(wsT(S_XR_HS, n, &HS));
+  RET(wsT(S_XR_RL, (size_t)CK_STEPS * n, &rl));
+  RET(ck_bufs(b, n, false));
+  RET(launch("k_xg_sub", k_xg_sub, n, 64, st, i0, n, flag, S, status, cnt));
+  RET(launch("k_xg_cand", k_xg_cand, n, 256, st, i0, n, flag, (const uint8_t*)status, cand, cnt));
+  RET(launch("k_xq_sum", k_xq_sum, 2 * nqmax, 64, st, nqmax, qpg, seed, cnt, (const uint32_t*)cand, Q, S, T4, tinf, l2,
+             QS));
+  for (uint32_t level = qpg > 1 ? 1u : 2u; level <= 3; ++level) {
+    const uint32_t G = level == 1 ? G1 : level == 2 ? nqmax : n;
+    const uint32_t* gcnt = cnt + level;
+    RET(launch("k_xg_prep", k_xg_prep, G, 64, st, level, G, (const uint32_t*)cnt, qpg, (const uint32_t*)l2,
+               (const uint32_t*)l3, (const G2JStore*)QS, Q, S, keys, b.st, HS));
+    RET(launch("k_xg_hlines", k_xg_hlines, G, 64, st, G, gcnt, (const G2JStore*)HS, rl, b.st));
+    RET(run_checks(G, gcnt, G, rl, b, st));
+    RET(launch("k_xg_verdict", k_xg_verdict, G, 128, st, level, G, qpg, cnt, (const uint8_t*)b.good,
+               (const uint32_t*)cand, l2, l3, status, g_ctx.xrcount));
+  }
+  return 0;
 }
 
 // The pass schedule of the pipeline: DG_CK_PASSES passes with speculative margins (DG_CK_MARGIN0 in the first,
@@ -1152,71 +1163,38 @@ uint32_t ck_margin(int which) {
   return (uint32_t)(which == 0 ? m0 : m);
 }
 
-// DG_CK_OLD=1 (A/B only): Recover's per-item pass as the round-3 single-lane kernel k_verify_groups instead of the
-// pipeline of checks.h
-bool ck_old() {
-  static const bool v = getenv("DG_CK_OLD") != nullptr;
-  return v;
-}
-
-int prefix_pass(uint32_t R, uint32_t k, uint32_t t, const uint64_t* seed, const G1AStore* keys, const uint32_t* item_slot,
-                const G2JStore* Q, const uint32_t* zero2, const G2AStore* S, uint8_t* status, uint8_t* fin,
-                uint32_t subgroup, hipStream_t batch_st) {
+// The per-item pass of a multi-key batch (Recover's examined prefix, VerifyPartial's isolated or failed items) on the
+// batch's own stream: H_r's lines once per round (k_ck_round_lines), then `passes` passes of group tests with
+// speculative margins and a final pass of single checks over every unverified item before the t-th valid one of its
+// round (t > k: every unverified item).  Per pass the group list is built on the device and its size read back, so
+// the pipeline runs over chunks of at most CK_CHUNK checks.  Statuses exact at the end; fin: FIN_DONE for the final
+// verdicts, FIN_PENDING for the rest (the seed's weights rho_i: kernels.h group_combine).
+int prefix_pass(uint32_t R, uint32_t k, uint32_t t, int passes, const uint64_t* seed, const G1AStore* keys,
+                const uint32_t* item_slot, const G2JStore* Q, const G2AStore* S, uint8_t* status, uint8_t* fin,
+                uint32_t subgroup, hipStream_t st) {
   const size_t N = (size_t)R * k;
-  Set& set = cur_set();
-  HIPCHK(hipEventRecord(set.to_fb, batch_st));
-  const hipStream_t st = g_ctx.shared_fb ? batch_st : g_ctx.fb_stream;
-  HIPCHK(hipStreamWaitEvent(st, set.to_fb, 0));
-  if (!ck_old()) {
-    // H_r's lines once per call; per pass the group list, its size to the host, the pipeline over chunks of checks
-    CkLine* rl;
-    uint8_t* hinf;
-    uint32_t* glist;
-    RET(wsT(S_CK_RL, (size_t)CK_STEPS * R, &rl));
-    RET(wsT(S_CK_HINF, R, &hinf));
-    RET(wsT(S_LIST, 4 * (N + 1), &glist));
-    RET(launch("k_ck_round_lines", k_ck_round_lines, R, 64, st, R, Q, rl, hinf));
-    const uint32_t grp = group_size();
-    const int kPasses = ck_passes();
-    for (int pass = 0; pass <= kPasses; ++pass) {
-      HIPCHK(hipMemsetAsync(glist, 0, 4, st));
-      const uint32_t margin = grp < 2 ? 0u : (pass == 0 ? ck_margin(0) : ck_margin(1));
-      RET(launch("k_prefix_groups", k_prefix_groups, R, 128, st, R, k, t, pass == kPasses ? 1u : 0u, grp, margin,
-                 (const uint8_t*)status, (const uint8_t*)fin, glist));
-      uint32_t G = 0;
-      HIPCHK(hipMemcpyAsync(&G, glist, 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      static const bool trace = getenv("DG_CK_TRACE") != nullptr;  // diagnostics: checks per pass
-      if (trace) fprintf(stderr, "[dg] prefix pass %d: %u checks\n", pass, G);
-      for (uint32_t off = 0; off < G; off += CK_CHUNK)
-        RET(check_chunk(std::min(G - off, CK_CHUNK), off, glist, k, R, seed, keys, item_slot, hinf, rl, S, status, fin,
-                        subgroup, st));
-    }
-    HIPCHK(hipEventRecord(set.from_fb, st));
-    HIPCHK(hipStreamWaitEvent(batch_st, set.from_fb, 0));
-    return 0;
-  }
-  // H_r = h_eff(Q_r) for every round (zero2: the flag pair {0, 0})
-  G2AStore* H;
-  RET(wsT(S_H, R, &H));
-  RET(launch("k_clear_rounds", k_clear_rounds, R, 128, st, R, zero2, Q, H));
+  CkLine* rl;
+  uint8_t* hinf;
   uint32_t* glist;
+  RET(wsT(S_CK_RL, (size_t)CK_STEPS * R, &rl));
+  RET(wsT(S_CK_HINF, R, &hinf));
   RET(wsT(S_LIST, 4 * (N + 1), &glist));
-  // An empty pass costs two launches of returning lanes; the speculative margins (k_prefix_groups) keep the
-  // non-empty ones to ~3 at 10% corruption (a pass model over the C5 pattern: 1.75 s of per-item checks alone ->
-  // ~1.05 s).
+  RET(launch("k_ck_round_lines", k_ck_round_lines, R, 64, st, R, Q, rl, hinf));
   const uint32_t grp = group_size();
-  constexpr int kPasses = 8;
-  for (int pass = 0; pass <= kPasses; ++pass) {
+  for (int pass = 0; pass <= passes; ++pass) {
     HIPCHK(hipMemsetAsync(glist, 0, 4, st));
-    const uint32_t margin = grp < 2 ? 0u : (pass == 0 ? 6u : 2u);
-    RET(launch("k_prefix_groups", k_prefix_groups, R, 128, st, R, k, t, pass == kPasses ? 1u : 0u, grp, margin,
+    const uint32_t margin = grp < 2 ? 0u : (pass == 0 ? ck_margin(0) : ck_margin(1));
+    RET(launch("k_prefix_groups", k_prefix_groups, R, 128, st, R, k, t, pass == passes ? 1u : 0u, grp, margin,
                (const uint8_t*)status, (const uint8_t*)fin, glist));
-    RET(launch_shm("k_verify_groups", k_verify_groups, (uint32_t)N, 64, verify_lds(), st, k, (const uint32_t*)glist, seed, keys, item_slot,
-               (const G2AStore*)H, S, status, fin, subgroup, g_ctx.gcount));
+    uint32_t G = 0;
+    HIPCHK(hipMemcpyAsync(&G, glist, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    static const bool trace = getenv("DG_CK_TRACE") != nullptr;  // diagnostics: checks per pass
+    if (trace) fprintf(stderr, "[dg] prefix pass %d: %u checks\n", pass, G);
+    for (uint32_t off = 0; off < G; off += CK_CHUNK)
+      RET(check_chunk(std::min(G - off, CK_CHUNK), off, glist, k, R, seed, keys, item_slot, hinf, rl, S, status, fin,
+                      subgroup, st));
   }
-  HIPCHK(hipEventRecord(set.from_fb, st));
-  HIPCHK(hipStreamWaitEvent(batch_st, set.from_fb, 0));
   return 0;
 }
 
@@ -1308,9 +1286,8 @@ int recover_windowed(const uint8_t* commits48, uint32_t t, uint32_t R, const uin
     RET(bind_seed(bf, seed ^ 0x77696e646f77ull, st, &s2, S_SEED2));
     pseed = s2;
   }
-  HIPCHK(hipMemsetAsync(inc + 2, 0, 8, st));  // k_clear_rounds: flag {0, 0} = clear every round
-  RET(prefix_pass(R, k, t, pseed, keys, d_itemslot, (const G2JStore*)Q, (const uint32_t*)(inc + 2), S, status, fin,
-                  bo.batched_sub, st));
+  RET(prefix_pass(R, k, t, ck_passes(), pseed, keys, d_itemslot, (const G2JStore*)Q, S, status, fin, bo.batched_sub,
+                  st));
   return launch("k_count_fallback", k_count_fallback, 1, 64, st, bo.flag, g_ctx.fallbacks);
 }
 
@@ -1458,8 +1435,6 @@ int dg_init(int device) {
   for (Set& x : g_ctx.sets) {
     if (!x.stream) HIPCHK(hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking));
     if (!x.done) HIPCHK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
-    if (!x.to_fb) HIPCHK(hipEventCreateWithFlags(&x.to_fb, hipEventDisableTiming));
-    if (!x.from_fb) HIPCHK(hipEventCreateWithFlags(&x.from_fb, hipEventDisableTiming));
   }
   if (!g_ctx.fb_stream) HIPCHK(hipStreamCreateWithFlags(&g_ctx.fb_stream, hipStreamNonBlocking));
   if (!g_ctx.fallbacks) {
@@ -1470,58 +1445,70 @@ int dg_init(int device) {
     HIPCHK(hipMalloc(&g_ctx.gcount, GRP * sizeof(unsigned long long)));
     HIPCHK(hipMemset(g_ctx.gcount, 0, GRP * sizeof(unsigned long long)));
   }
-  // A hardware queue's scratch (private segment) grows on the first dispatch that needs more.  On MI355X
-  // that growth, when it first happened inside an overlapped batch (the per-item kernels: ~14 KB per
-  // lane), stalled every queue for ~0.5 s (rocprofv3 trace).  Dispatch the largest-scratch kernels once here,
-  // with zero items (every lane returns at once), so the growth happens now -- the largest first: a dispatch
-  // that needs a larger private segment than the queue's current one, right behind it, failed with
-  // HSA_STATUS_ERROR_OUT_OF_RESOURCES on the box.  Each queue reserves its scratch for every wave the device can
-  // hold, so the kernels with the large private segments (the per-item pairing checks, k_clear_rounds, k_sign,
-  // k_hash_to_g2) all run on the per-item stream, and the workspace streams are prewarmed with the largest of the
-  // rest, k_rc_combine (~4 KB; tests/test_abi.py checks both orderings against the code-object metadata):
-  // with 12 workspace streams on 32 queues at k_sign's 5.7 KB, dg_init failed with that error.
-  if (const char* e = getenv("DG_SHARED_FB")) {
-    g_ctx.shared_fb = atoi(e) != 0;
-  } else {
-    const int hwq = env_hw_queues();
-    int sets, shared;
-    queue_plan(hwq, &sets, &shared);
-    g_ctx.shared_fb = shared != 0 && hwq < active_sets() + 2;  // (DG_SETS may leave every stream its own queue)
+  if (!g_ctx.xrcount) {
+    HIPCHK(hipMalloc(&g_ctx.xrcount, 4 * sizeof(unsigned long long)));  // (4 words: also the prewarm's zero counters)
+    HIPCHK(hipMemset(g_ctx.xrcount, 0, 4 * sizeof(unsigned long long)));
   }
-  hipFuncAttributes fa_items{}, fa_groups{};
-  HIPCHK(hipFuncGetAttributes(&fa_items, reinterpret_cast<const void*>(k_verify_items)));
-  HIPCHK(hipFuncGetAttributes(&fa_groups, reinterpret_cast<const void*>(k_verify_groups)));
-  const bool items_first = fa_items.localSizeBytes > fa_groups.localSizeBytes;
-  auto prewarm_items = [&](hipStream_t q) {
-    for (int pass = 0; pass < 2; ++pass) {
-      if ((pass == 0) == items_first) {
-        hipLaunchKernelGGL(k_verify_items, dim3(1), dim3(64), 0, q, 0u, 1u, (const uint32_t*)nullptr,
-                           (const G1AStore*)nullptr, (const uint32_t*)nullptr, (const G2AStore*)nullptr,
-                           (const G2AStore*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, 0u);
-      } else {
-        // glist[0] = 0 (the zeroed fallback counter): no groups
-        hipLaunchKernelGGL(k_verify_groups, dim3(1), dim3(64), 0, q, 1u, (const uint32_t*)g_ctx.fallbacks,
-                           (const uint64_t*)nullptr, (const G1AStore*)nullptr, (const uint32_t*)nullptr,
-                           (const G2AStore*)nullptr, (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr,
-                           0u, g_ctx.gcount);
+  // A hardware queue's scratch (private segment) grows on the first dispatch that needs more.  On MI355X that growth,
+  // when it first happened inside an overlapped batch (the round-1 per-item kernels: ~14 KB per lane), stalled every
+  // queue for ~0.5 s (rocprofv3 trace), and a dispatch needing more than the queue's current segment right behind
+  // another failed with HSA_STATUS_ERROR_OUT_OF_RESOURCES on the box.  So every kernel that may run on a stream is
+  // dispatched there once now with no work, largest private segment first (read from the code object): the queue's
+  // scratch has its final size before any batch runs.  Each queue reserves its scratch for every wave the device can
+  // hold, so the two fixture kernels with the library's largest segments (k_sign, k_hash_to_g2: ~5.4 KB) have the
+  // fb stream to themselves and the workspace queues hold the check pipeline's (tests/test_abi.py checks the split
+  // against the code-object metadata).  With no work every lane returns at once (zero counters: xrcount).
+  {
+    uint32_t* z = (uint32_t*)g_ctx.xrcount;
+    const uint32_t* cz = z;
+    struct Warm {
+      const void* fn;
+      std::function<void(hipStream_t)> go;
+    };
+    const dim3 g1(1), b64(64), b128(128);
+    const std::vector<Warm> on_sets = {
+        {(const void*)k_rc_combine, [&](hipStream_t q) { hipLaunchKernelGGL(k_rc_combine, g1, b128, 0, q, 0u, 0u, (const uint32_t*)nullptr, (const uint8_t*)nullptr, (const G2JStore*)nullptr, (G2JStore*)nullptr); }},
+        {(const void*)k_ck_prep, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_prep, g1, b64, 0, q, 0u, 0u, cz, 1u, (const uint64_t*)nullptr, (const G1AStore*)nullptr, cz, (const uint8_t*)nullptr, (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr, 0u, g_ctx.gcount, (CkState*)nullptr, (uint8_t*)nullptr, (RsDigits*)nullptr); }},
+        {(const void*)k_ck_round_lines, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_round_lines, g1, b64, 0, q, 0u, (const G2JStore*)nullptr, (CkLine*)nullptr, (uint8_t*)nullptr); }},
+        {(const void*)k_ck_lines2, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_lines2, g1, b64, 0, q, 0u, cz, (const CkState*)nullptr, (CkLine*)nullptr); }},
+        {(const void*)k_ck_miller, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_miller, g1, b64, 0, q, 0u, cz, 0u, (const CkState*)nullptr, (const CkLine*)nullptr, (const CkLine*)nullptr, (Fp12*)nullptr); }},
+        {(const void*)k_ck_easy, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_easy, g1, b64, 0, q, 0u, cz, (const Fp12*)nullptr, (Fp12*)nullptr, (uint32_t*)nullptr); }},
+        {(const void*)k_ck_expsq, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_expsq, g1, b64, 0, q, 0u, cz, (const Fp12*)nullptr, (CycC*)nullptr, (Fp*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr); }},
+        {(const void*)k_ck_expdec, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_expdec, g1, b64, 0, q, 0u, cz, (const CycC*)nullptr, (Fp*)nullptr, (const uint8_t*)nullptr, (const Fp12*)nullptr, 0u, 0u, (Fp12*)nullptr); }},
+        {(const void*)k_ck_explain, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_explain, g1, b64, 0, q, cz, (const Fp12*)nullptr, (const Fp12*)nullptr, 0u, 0u, (Fp12*)nullptr); }},
+        {(const void*)k_ck_final, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_final, g1, b64, 0, q, 0u, cz, (const CkState*)nullptr, (const Fp12*)nullptr, (const Fp12*)nullptr, (const Fp12*)nullptr, (uint8_t*)nullptr); }},
+        {(const void*)k_ck_sub, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_sub, g1, b64, 0, q, 0u, 0u, cz, (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr); }},
+        {(const void*)k_ck_sac, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_sac, g1, b64, 0, q, 0u, (const uint8_t*)nullptr, (const RsDigits*)nullptr, (const uint4*)nullptr, (const uint8_t*)nullptr, (G2JStore*)nullptr, (Fp*)nullptr); }},
+        {(const void*)k_xg_sub, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_sub, g1, b64, 0, q, 0u, 0u, cz, (const G2AStore*)nullptr, (uint8_t*)nullptr, z); }},
+        {(const void*)k_xq_sum, [&](hipStream_t q) { hipLaunchKernelGGL(k_xq_sum, g1, b64, 0, q, 0u, 1u, (const uint64_t*)nullptr, z, cz, (const G2JStore*)nullptr, (const G2AStore*)nullptr, (uint4*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr, (G2JStore*)nullptr); }},
+        {(const void*)k_xg_prep, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_prep, g1, b64, 0, q, 1u, 0u, cz, 1u, cz, cz, (const G2JStore*)nullptr, (const G2JStore*)nullptr, (const G2AStore*)nullptr, (const G1AStore*)nullptr, (CkState*)nullptr, (G2JStore*)nullptr); }},
+        {(const void*)k_xg_hlines, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_hlines, g1, b64, 0, q, 0u, cz, (const G2JStore*)nullptr, (CkLine*)nullptr, (CkState*)nullptr); }},
+    };
+    const std::vector<Warm> on_fb = {
+        {(const void*)k_sign, [&](hipStream_t q) { hipLaunchKernelGGL(k_sign, g1, b128, 0, q, 0u, (const uint8_t*)nullptr, (const uint16_t*)nullptr, (const uint8_t*)nullptr, 0u, (const uint8_t*)nullptr, 0u, (uint8_t*)nullptr); }},
+        {(const void*)k_hash_to_g2, [&](hipStream_t q) { hipLaunchKernelGGL(k_hash_to_g2, g1, b128, 0, q, 0u, (const uint8_t*)nullptr, 0u, (const uint8_t*)nullptr, 0u, (uint8_t*)nullptr); }},
+    };
+    // largest private segment first
+    auto order = [&](const std::vector<Warm>& ws, std::vector<size_t>& idx) -> int {
+      std::vector<size_t> sz(ws.size());
+      for (size_t i = 0; i < ws.size(); ++i) {
+        hipFuncAttributes fa{};
+        HIPCHK(hipFuncGetAttributes(&fa, ws[i].fn));
+        sz[i] = fa.localSizeBytes;
+        idx.push_back(i);
       }
-    }
-  };
-  // only the active sets' streams are dispatched to (a stream takes a hardware queue at its first dispatch), the
-  // per-item stream after them: with more streams than hardware queues (GPU_MAX_HW_QUEUES, default 4) streams
-  // share queues, and a cross-stream wait queued on a shared queue holds every stream behind it
-  for (int i = 0; i < active_sets(); ++i) {
-    Set& x = g_ctx.sets[i];
-    if (g_ctx.shared_fb) {
-      prewarm_items(x.stream);
-    } else {
-      // n = 0: every lane returns
-      hipLaunchKernelGGL(k_rc_combine, dim3(1), dim3(128), 0, x.stream, 0u, 0u, (const uint32_t*)nullptr,
-                         (const uint8_t*)nullptr, (const G2JStore*)nullptr, (G2JStore*)nullptr);
-    }
-    HIPCHK(hipGetLastError());
+      std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return sz[a] > sz[b]; });
+      return 0;
+    };
+    std::vector<size_t> oset, ofb;
+    RET(order(on_sets, oset));
+    RET(order(on_fb, ofb));
+    // only the active sets' streams are dispatched to (a stream takes a hardware queue at its first dispatch), the fb
+    // stream after them
+    for (int i = 0; i < active_sets(); ++i)
+      for (size_t w : oset) on_sets[w].go(g_ctx.sets[i].stream);
+    for (size_t w : ofb) on_fb[w].go(g_ctx.fb_stream);
   }
-  if (!g_ctx.shared_fb) prewarm_items(g_ctx.fb_stream);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   g_ctx.device = device;
@@ -1541,11 +1528,8 @@ void dg_shutdown(void) {
     x.busy = false;
     if (x.stream) (void)hipStreamDestroy(x.stream);
     if (x.done) (void)hipEventDestroy(x.done);
-    if (x.to_fb) (void)hipEventDestroy(x.to_fb);
-    if (x.from_fb) (void)hipEventDestroy(x.from_fb);
     x.stream = nullptr;
     x.done = nullptr;
-    x.to_fb = x.from_fb = nullptr;
   }
   if (g_ctx.fb_stream) {
     (void)hipStreamSynchronize(g_ctx.fb_stream);
@@ -1558,6 +1542,8 @@ void dg_shutdown(void) {
   if (g_ctx.pk_ready) (void)hipEventDestroy(g_ctx.pk_ready);
   if (g_ctx.fallbacks) (void)hipFree(g_ctx.fallbacks);
   if (g_ctx.gcount) (void)hipFree(g_ctx.gcount);
+  if (g_ctx.xrcount) (void)hipFree(g_ctx.xrcount);
+  g_ctx.xrcount = nullptr;
   if (g_ctx.d_dst) (void)hipFree(g_ctx.d_dst);
   if (g_ctx.d_xmd) (void)hipFree(g_ctx.d_xmd);
   g_ctx.d_dst = nullptr;
@@ -1838,6 +1824,17 @@ int dg_group_counts(uint64_t* out4) {
   unsigned long long v[GRP];
   HIPCHK(hipMemcpy(v, g_ctx.gcount, sizeof(v), hipMemcpyDeviceToHost));
   for (uint32_t m = 0; m < GRP; ++m) out4[m] = v[m];
+  return 0;
+}
+
+int dg_isolation_counts(uint64_t* out3) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  RET(require_ready());
+  if (!out3) return fail(DG_E_ARG, "bad arguments");
+  RET(wait_all());
+  unsigned long long v[3];
+  HIPCHK(hipMemcpy(v, g_ctx.xrcount, sizeof(v), hipMemcpyDeviceToHost));
+  for (int m = 0; m < 3; ++m) out3[m] = v[m];
   return 0;
 }
 

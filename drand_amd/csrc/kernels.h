@@ -16,22 +16,16 @@
 #ifndef DG_BULK_WAVES
 #define DG_BULK_WAVES 1  // min waves per SIMD for the other per-lane group-arithmetic kernels
 #endif
-#ifndef DG_VERIFY_WAVES
-#define DG_VERIFY_WAVES 1  // min waves per SIMD of the per-item pairing checks (k_verify_items / k_verify_groups)
-#endif
 #ifndef DG_COOP_WAVES
 #define DG_COOP_WAVES 1  // min waves per SIMD for the cooperative (latency-bound) kernels
 #endif
 #ifndef DG_TU_HOT
 #define DG_TU_HOT 0  // 1 in kernels_hot.hip: only the hot kernels are defined there (DESIGN.md §code generation)
 #endif
-#ifndef DG_TU_VERIFY
-#define DG_TU_VERIFY 0  // 1 in kernels_verify.hip: only the per-item pairing kernels are defined there
-#endif
 #ifndef DG_TU_CHECK
 #define DG_TU_CHECK 0  // 1 in kernels_check.hip: only the pairing-check pipeline of checks.h is defined there
 #endif
-#define DG_TU_LIB (!DG_TU_HOT && !DG_TU_VERIFY && !DG_TU_CHECK)  // the library translation unit (drand_gpu.hip)
+#define DG_TU_LIB (!DG_TU_HOT && !DG_TU_CHECK)  // the library translation unit (drand_gpu.hip)
 
 namespace dg {
 
@@ -485,23 +479,10 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_final_coop(uint32_t npair
 }
 #endif
 
-// H_r = h_eff(Q_r), affine (individual checks)
-// (skipped when the batch verified and nothing was isolated: flag[0] = batch ok, flag[1] = any isolated)
-#if DG_TU_LIB
-DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_clear_rounds(uint32_t R, const uint32_t* flag, const G2JStore* Q, G2AStore* H) {
-  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R || (flag[0] && !flag[1])) return;
-  store_g2a(H[r], g2_to_aff(g2_clear_cofactor(load_g2j(Q[r]))));
-}
-#endif
-
-// individual bls.Verify of item i: e(X_slot, H_{i/k}) == e(g1, S_i); with `subgroup` the decode skipped
-// the per-item G2 subgroup check (batched on the MSM windows), so it is done here: a sigma outside G2
-// is a decode error, as in g2_decompress
-// ---- Group tests over the examined prefix.  With a corrupted fraction f of the shares, one pairing check
+// ---- Group tests over the examined prefix (checks.h).  With a corrupted fraction f of the shares, one pairing check
 // per examined item is more than Recover needs: up to GRP consecutive unverified items of one round are
 // checked together, e(sum_i rho_i X_i, H_r) == e(g1, sum_i rho_i S_i) with independent 64-bit rho_i from the
-// batch's bound seed.  Every S_i is in G2 (subgroup-checked here as in verify_item) and H_r is in G2, so a
+// batch's bound seed.  Every S_i is in G2 (subgroup-checked by k_ck_sub) and H_r is in G2, so a
 // member with x_i H_r != S_i makes the sum vanish for at most one rho_i value mod r: a group with a bad
 // member passes with probability <= 2^-63 (rho_i is odd: 2^63 values).  A passed group gives every member kyber's nil verdict; the
 // members of a failed group are marked for their own check (fin = FIN_RECHECK) in the next pass, which
@@ -509,9 +490,8 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_clear_rounds(uint32_t R, 
 constexpr uint32_t GRP = 4;
 constexpr uint8_t FIN_PENDING = 0, FIN_DONE = 1, FIN_RECHECK = 2;
 constexpr uint64_t GROUP_TAG = 0x67726f7570746573ull;  // domain of rho_i, apart from alpha_r and beta_s
-#if DG_TU_VERIFY || DG_TU_CHECK
-// the Miller loop out of line, so its state and the final exponentiation's do not share one stack frame
-// (the per-item kernels' private segment must stay under the queue's scratch limit: ~14 KB per lane)
+#if DG_TU_CHECK || !defined(__HIP__)
+// the single-lane reference of the pipeline's checks (host builds: tests/native/hostcheck.cpp)
 DGN Fp12 miller_loop2(const G1A* P, const G2A* Q, int np) { return miller_loop<2>(P, Q, np); }
 // e(x, h) * e(-g1, s) == 1 (the identity's pairings dropped): kyber's bls.Verify equation
 DGN bool pair_check(const G1A& x, const G2A& h, const G2A& s) {
@@ -530,27 +510,13 @@ DGN bool pair_check(const G1A& x, const G2A& h, const G2A& s) {
   }
   return np == 0 ? true : fp12_is_one(final_exp_cubed(miller_loop2(P, Qa, np)));
 }
-DGN void verify_item(size_t i, uint32_t k, const G1AStore* keys, const uint32_t* item_slot, const G2AStore* H,
-                     const G2AStore* S, uint8_t* status, uint32_t subgroup) {
-  const G2A s = load_g2a(S[i]);
-  if (subgroup && !s.inf && !g2_in_subgroup_aff(s.x, s.y)) {
-    status[i] = DG_ST_SIG_DECODE_;
-    return;
-  }
-  const bool good = pair_check(load_g1a(keys[item_slot ? item_slot[i] : 0u]), load_g2a(H[i / k]), s);
-  status[i] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
-}
-
-// the members' weighted sums a = sum rho_i X_i, b = sum rho_i S_i; members failing the subgroup check are
-// decided here (decode error) and left out.  Returns the live members (their item indices in live[]).
-// With g2 = false (Recover's pipeline, checks.h) the G2 sum b is left to the table kernels (k_ck_tab_*, k_ck_sac),
-// except for a single share (b = its sigma); rho[] receives the live members' coefficients.
-template <bool g2>
-DGN uint32_t group_combine_t(const uint32_t* mem, uint32_t n, uint64_t seed, const G1AStore* keys,
+// the members' G1 weighted sum a = sum rho_i X_i (the G2 sum b = sum rho_i S_i is left to checks.h's table kernels,
+// k_ck_tab_*, k_ck_sac, except for a single share: b = its sigma); members failing the subgroup check are decided here
+// (decode error) and left out.  Returns the live members (their item indices in live[], coefficients in rho_out[]).
+DGN uint32_t group_combine(const uint32_t* mem, uint32_t n, uint64_t seed, const G1AStore* keys,
                              const uint32_t* item_slot, const G2AStore* S, uint8_t* status, uint8_t* fin,
                              uint32_t subgroup, G1A& a, G2A& b, uint32_t* live, uint64_t* rho_out) {
   G1J xp[GRP];
-  G2J sp[GRP];
   uint64_t rho[GRP];
   uint32_t nl = 0;
   for (uint32_t m = 0; m < n; ++m) {
@@ -570,83 +536,19 @@ DGN uint32_t group_combine_t(const uint32_t* mem, uint32_t n, uint64_t seed, con
       return 1;
     }
     xp[nl] = jac_from_aff(load_g1a(keys[item_slot ? item_slot[i] : 0u]));
-    if (g2) sp[nl] = jac_from_aff(s);
     rho[nl] = rlc_coeff(seed ^ GROUP_TAG, i);
     live[nl++] = i;
   }
   for (uint32_t m = nl; m < GRP; ++m) {
     xp[m] = jac_infinity<Fp>();
-    if (g2) sp[m] = jac_infinity<Fp2>();
     rho[m] = 0;
   }
   if (rho_out)
     for (uint32_t m = 0; m < GRP; ++m) rho_out[m] = rho[m];
-  if (nl) {
-    a = g1_to_aff(jac_msm4_sac(xp, rho));
-    if (g2) b = g2_to_aff(jac_msm4_sac(sp, rho));
-  }
+  if (nl) a = g1_to_aff(jac_msm4_sac(xp, rho));
+  (void)b;
   return nl;
 }
-DGI uint32_t group_combine(const uint32_t* mem, uint32_t n, uint64_t seed, const G1AStore* keys,
-                           const uint32_t* item_slot, const G2AStore* S, uint8_t* status, uint8_t* fin,
-                           uint32_t subgroup, G1A& a, G2A& b, uint32_t* live, uint64_t* rho_out = nullptr) {
-  return group_combine_t<true>(mem, n, seed, keys, item_slot, S, status, fin, subgroup, a, b, live, rho_out);
-}
-DGN void verify_group(const uint32_t* mem, uint32_t n, uint32_t k, uint64_t seed, const G1AStore* keys,
-                      const uint32_t* item_slot, const G2AStore* H, const G2AStore* S, uint8_t* status,
-                      uint8_t* fin, uint32_t subgroup) {
-  G1A a;
-  G2A b;
-  uint32_t live[GRP];
-  const uint32_t nl = group_combine(mem, n, seed, keys, item_slot, S, status, fin, subgroup, a, b, live);
-  if (nl == 0) return;
-  // one call site of the pairing check for singles and groups alike: a wave holding both runs it once
-  const bool good = pair_check(a, load_g2a(H[mem[0] / k]), b);
-  if (n == 1) {
-    status[live[0]] = good ? DG_ST_OK_ : DG_ST_BAD_SIG_;
-    fin[live[0]] = FIN_DONE;
-    return;
-  }
-  for (uint32_t m = 0; m < nl; ++m) {
-    if (good) status[live[m]] = DG_ST_OK_;
-    fin[live[m]] = good ? FIN_DONE : FIN_RECHECK;
-  }
-}
-#endif
-#if DG_TU_VERIFY
-// every decoded item after a failed batch (flag[0] == 0), only the isolated ones after a passed batch
-DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
-                                                    const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
-                                                    const uint8_t* isolate, uint8_t* status, uint32_t subgroup) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (status[i] != DG_ST_OK_) return;
-  if (flag[0] && !isolate[i]) return;
-  verify_item(i, k, keys, item_slot, H, S, status, subgroup);
-}
-
-// lane g < glist[0]: group g (one member: the item's own check)
-DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_groups(uint32_t k, const uint32_t* glist, const uint64_t* seedp,
-                                                    const G1AStore* keys, const uint32_t* item_slot,
-                                                    const G2AStore* H, const G2AStore* S, uint8_t* status,
-                                                    uint8_t* fin, uint32_t subgroup, unsigned long long* cnt) {
-  uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= glist[0]) return;
-  const uint32_t* mem = glist + 4 + 4 * (size_t)g;
-  uint32_t n = 0;
-  while (n < GRP && mem[n] != ~0u) ++n;
-  atomicAdd(&cnt[n - 1], 1ull);
-  verify_group(mem, n, k, *seedp, keys, item_slot, H, S, status, fin, subgroup);
-}
-#elif !DG_TU_CHECK
-// (defined in kernels_verify.hip)
-DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_items(uint32_t n, uint32_t k, const uint32_t* flag, const G1AStore* keys,
-                                                    const uint32_t* item_slot, const G2AStore* H, const G2AStore* S,
-                                                    const uint8_t* isolate, uint8_t* status, uint32_t subgroup);
-DG_KERNEL void __launch_bounds__(64, DG_VERIFY_WAVES) k_verify_groups(uint32_t k, const uint32_t* glist, const uint64_t* seedp,
-                                                    const G1AStore* keys, const uint32_t* item_slot,
-                                                    const G2AStore* H, const G2AStore* S, uint8_t* status,
-                                                    uint8_t* fin, uint32_t subgroup, unsigned long long* cnt);
 #endif
 #if DG_TU_LIB
 // ---- Recover's window (drand_gpu.hip recover_windowed).  kyber's tbls.Recover verifies the partials of a
@@ -761,10 +663,6 @@ DG_KERNEL void __launch_bounds__(64) k_count_fallback(const uint32_t* flag, unsi
 struct Seed0 {
   uint32_t w[8];
 };
-// diagnostics only (DG_NO_BIND=1): the caller's seed as is
-DG_KERNEL void __launch_bounds__(64) k_store_seed(uint64_t seed, uint64_t* out) {
-  if (threadIdx.x == 0) *out = seed;
-}
 // ---- Binding the batch coefficients to the batch (Fiat-Shamir).  alpha_r, beta_s and the test-window
 // digits of the batched subgroup check are keyed by seed' = SHA-256(seed0 || D)[0..8), where seed0 =
 // SHA-256(BE64 seed || key bytes) (host) and D is a SHA-256 tree over every item (message and signature
@@ -951,3 +849,4 @@ DG_KERNEL void __launch_bounds__(128) k_sign(uint32_t n, const uint8_t* sc32, co
 #include "msm.h"
 #include "recover.h"
 #include "checks.h"
+#include "xr.h"

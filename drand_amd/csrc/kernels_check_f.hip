@@ -1,0 +1,11 @@
+// Part 6 of Recover's pairing-check pipeline (checks.h), compiled in its own translation unit with every field
+// product inlined and serialised (DG_FP_CALL=3) and the Fp12 routines inlined (DG_INLINE12=1): each kernel of the
+// pipeline is short, so its formula fits the register file without calls or scratch.  The parts build in parallel.
+#define DG_TU_CHECK 6
+#define DG_FP_CALL 3
+#define DG_INLINE12 1
+#define DG_CYC_SQR 1
+#define DG_FP2_ILV 1
+#define DG_FP2_DIG 1  // Fp2 products in digit form: each operand unpacked once (field.h fp2_mul_dig, +3% C5 measured)
+#define DG_SEQ_DIG 1  // ... and the serialised forms (subgroup checks, column loops, compressed squarings: -1% C5)
+#include "kernels.h"

@@ -19,10 +19,12 @@
  *   - `msg_len` is the per-item message length (drand: 32 B SHA-256 outputs); all items of one call
  *     share it.  Messages are laid out back to back (n x msg_len bytes).
  *   - Verdicts of the batch paths are exact for every rejected item and probabilistic for accepted ones:
- *     a batch (or a Recover group test of up to 4 shares) that passes its random-linear-combination
- *     equation accepts all its members, and a bad member survives with probability <= 2^-63 (64-bit
- *     coefficients bound to the batch contents).  A failed equation sends every member to
- *     its own pairing check.  dg_set_group_size(1) makes Recover's per-item pass use single checks only.
+ *     a batch (or a group test: up to 4 shares of one Recover / VerifyPartial round, or 4..16 rounds of a
+ *     failed chain batch) that passes its random-linear-combination equation accepts all its members, and a
+ *     bad member survives with probability <= 2^-63 (64-bit coefficients bound to the batch contents,
+ *     DESIGN.md §4.4).  A failed equation splits its members into smaller group tests and, last, single
+ *     pairing checks: every rejection is a single check's.  dg_set_group_size(1) makes the multi-key per-item
+ *     pass (Recover, VerifyPartial) use single checks only.
  */
 #ifndef DRAND_GPU_H
 #define DRAND_GPU_H
@@ -168,8 +170,9 @@ int dg_verify_beacons_dev_async(const uint8_t* pk48_host, size_t n, const uint64
                                 const uint8_t* d_sigs96, uint8_t* d_status, uint64_t seed, void* in_stream,
                                 void* done_stream);
 /* The workspace plan dg_init uses for a hardware queue count (GPU_MAX_HW_QUEUES; HIP's default 4): *sets workspace
- * sets (batches in flight; DG_SETS overrides) and whether the per-item pass runs on each set's own stream (1) or on a
- * dedicated stream (0).  Host-only, no device needed.  (No reference counterpart.) */
+ * sets (batches in flight; DG_SETS overrides) and whether the per-item pass runs on each set's own stream (1, at
+ * every queue count since the check pipeline replaced the large-scratch per-item kernels).  Host-only, no device
+ * needed.  (No reference counterpart.) */
 int dg_queue_plan(int hw_queues, int* sets, int* per_item_on_set_streams);
 /* The HIP stream (hipStream_t) the most recent dg_verify_beacons_dev_async batch was enqueued on.  Work the caller
  * enqueues there runs after that batch with no cross-stream wait: with fewer hardware queues than streams
@@ -188,6 +191,10 @@ int dg_fallback_count(uint64_t* out);
 /* Recover's per-item pass since dg_init (waits for batches in flight): out4[m - 1] = checks of m shares of
  * one round at once (m = 1: a share's own bls.Verify; m = 2..4: a random-linear-combination group test). */
 int dg_group_counts(uint64_t* out4);
+/* The isolation of failed single-key batches (dg_verify, dg_verify_beacons*) since dg_init (waits for batches in
+ * flight): out3[0] = group tests of 4..64 rounds, out3[1] = tests of 4 rounds, out3[2] = single bls.Verify checks
+ * (beacon/chain.go:65-71 decides every round alone; a failed batch equation splits its rounds this way). */
+int dg_isolation_counts(uint64_t* out3);
 /* Shares per group test in Recover's per-item pass: 1..4 (default 4, or the DG_GROUP environment variable);
  * 1 = every examined share gets its own exact pairing check.  Process-wide. */
 int dg_set_group_size(uint32_t m);

@@ -43,6 +43,7 @@ EXPECT_TYPE(dg_last_batch_stream, int (*)(void**));
 EXPECT_TYPE(dg_last_batch_flags, int (*)(uint32_t*));
 EXPECT_TYPE(dg_fallback_count, int (*)(uint64_t*));
 EXPECT_TYPE(dg_group_counts, int (*)(uint64_t*));
+EXPECT_TYPE(dg_isolation_counts, int (*)(uint64_t*));
 EXPECT_TYPE(dg_set_group_size, int (*)(uint32_t));
 EXPECT_TYPE(dg_recover_dev, int (*)(const uint8_t*, uint32_t, uint32_t, size_t, const uint8_t*, size_t, uint32_t,
                                     const uint8_t*, uint8_t*, uint8_t*, uint8_t*, uint64_t));
@@ -97,6 +98,7 @@ int main() {
   expect("dg_fallback_count", dg_fallback_count(&u64), DG_E_NODEV);
   uint64_t u64x4[4];
   expect("dg_group_counts", dg_group_counts(u64x4), DG_E_NODEV);
+  expect("dg_isolation_counts", dg_isolation_counts(u64x4), DG_E_NODEV);
   expect("dg_wait_all", dg_wait_all(), DG_E_NODEV);
   // host-only state works without a device
   int plan_sets = 0, plan_shared = 0;

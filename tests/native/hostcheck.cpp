@@ -588,12 +588,20 @@ extern "C" int hc_cyc_exp_check(uint64_t seed, uint32_t n) {
 // Q2 at -g1, the easy part through ck_fe1 / ck_inv with the Fp inversion of the batch, the hard part through the
 // compressed chains (ck_expsq / ck_expdec, or ck_exp_plain where a denominator is zero) and ck_mul_op.  `np` drops
 // pairs as pair_check does (bit 0: (P1, Q1), bit 1: (-g1, Q2)).  Returns 1 when both Fp12 values are equal.
-static Fp12 hc_ck_expz(const Fp12& x) {
+static Fp12 hc_ck_expz(const Fp12& x, const Fp12* y, uint32_t nfrob, uint32_t conj) {
+  // k_ck_expsq, k_ck_expdec (norms inverted in the lane by ck_inv6), k_ck_explain; times op(y) when given
   CycC sn[CK_NPOW];
   Fp nv[CK_NPOW];
-  const bool zero = ck_expsq(x, [&](int i, const CycC& c, const Fp& n) { sn[i] = c; nv[i] = n; });
-  if (zero) return ck_exp_plain(x);
-  return ck_expdec([&](int i, CycC& c, Fp& n) { c = sn[i]; n = fp_inv(nv[i]); });
+  Fp12 xz;
+  if (fp12_is_one(x)) {
+    xz = fp12_one();
+  } else if (ck_expsq(x, [&](int i, const CycC& c, const Fp& n) { sn[i] = c; nv[i] = n; })) {
+    xz = ck_exp_plain(x);
+  } else {
+    ck_inv6([&](int i) { return nv[i]; }, [&](int i, const Fp& v) { nv[i] = v; });
+    xz = ck_expdec([&](int i, CycC& c, Fp& n) { c = sn[i]; n = nv[i]; });
+  }
+  return y ? ck_mul_op(xz, *y, nfrob, conj) : xz;
 }
 extern "C" int hc_ck_pipeline_check(const uint8_t* pk48, const uint8_t* q1_96, const uint8_t* q2_96, int np) {
   G1A p1;
@@ -609,20 +617,42 @@ extern "C" int hc_ck_pipeline_check(const uint8_t* pk48, const uint8_t* q1_96, c
   ck_lines(q1.x, q1.y, [&](uint32_t s, const CkLine& l) { l1[s] = l; });
   ck_lines(q2.x, q2.y, [&](uint32_t s, const CkLine& l) { l2[s] = l; });
   const Fp12 f = ck_miller((uint32_t)np, p1.x, p1.y, [&](uint32_t s, uint32_t pair) { return pair ? l2[s] : l1[s]; });
+  // k_ck_easy
   CkInv inv;
   const Fp nt = ck_fe1(f, inv);
-  const Fp12 finv = ck_inv(f, inv, fp_inv(nt));
-  const Fp12 f1 = ck_mul_op(finv, f, 0, 1);
+  const Fp12 f1 = ck_mul_op(ck_inv(f, inv, fp_inv(nt)), f, 0, 1);
   const Fp12 f2 = ck_mul_op(f1, f1, 2, 0);
-  const Fp12 t0 = ck_mul_op(hc_ck_expz(f2), f2, 0, 1);
-  const Fp12 t1 = ck_mul_op(hc_ck_expz(t0), t0, 0, 1);
-  const Fp12 a = ck_mul_op(hc_ck_expz(t1), t1, 1, 0);
-  const Fp12 b = ck_mul_op(ck_mul_op(hc_ck_expz(hc_ck_expz(a)), a, 2, 0), a, 0, 1);
+  // the five x^z with their next factors (drand_gpu.hip run_checks), k_ck_final
+  const Fp12 t0 = hc_ck_expz(f2, &f2, 0, 1);
+  const Fp12 t1 = hc_ck_expz(t0, &t0, 0, 1);
+  const Fp12 a = hc_ck_expz(t1, &t1, 1, 0);
+  const Fp12 t = hc_ck_expz(hc_ck_expz(a, nullptr, 0, 0), &a, 2, 0);
   const Fp12 c = ck_mul_op(ck_mul_op(f2, f2, 0, 0), f2, 0, 0);
-  const Fp12 res = n ? ck_mul_op(b, c, 0, 0) : fp12_one();
+  const Fp12 res = n ? ck_mul_op(ck_mul_op(t, a, 0, 1), c, 0, 0) : fp12_one();
   const Fp2* u[6] = {&res.c0.c0, &res.c0.c1, &res.c0.c2, &res.c1.c0, &res.c1.c1, &res.c1.c2};
   const Fp2* v[6] = {&ref.c0.c0, &ref.c0.c1, &ref.c0.c2, &ref.c1.c0, &ref.c1.c1, &ref.c1.c2};
   for (int i = 0; i < 6; ++i)
     if (!fp2_eq(*u[i], *v[i])) return 0;
   return 1;
+}
+
+// xr.h xq_sum4 (the cross-round quad sums of k_xq_sum: an affine 8-entry table built in three levels with one Fp
+// inversion per level, the column loop) against sum_i [rho_i] P_i by double-and-add.  sigs: 4 compressed G2 points
+// (repeats, negations and the identity allowed), rho: 4 coefficients, members past nl are the identity (rho 0).
+extern "C" int hc_xq_sum_check(const uint8_t* sigs384, const uint64_t* rho_in, uint32_t nl) {
+  G2A P[4];
+  uint64_t rho[4];
+  G2J ref = jac_infinity<Fp2>();
+  for (uint32_t m = 0; m < 4; ++m) {
+    if (!g2_decompress(P[m], sigs384 + 96 * m, false)) return -1;
+    if (m >= nl) P[m] = G2A{fp2_zero(), fp2_zero(), true};
+    rho[m] = m < nl ? rho_in[m] : 0;
+    ref = jac_add(ref, jac_mul_u64(jac_from_aff(P[m]), rho[m]));
+  }
+  G2A T[8];
+  for (auto& t : T) t = G2A{fp2_zero(), fp2_zero(), true};
+  G2J acc;
+  xq_sum4([&](uint32_t m) { return P[m]; }, rho, [&](uint32_t u) { return T[u]; },
+          [&](uint32_t u, const G2A& t) { T[u] = t; }, acc);
+  return jac_eq(acc, ref) ? 1 : 0;
 }

@@ -17,7 +17,9 @@ import bench
 KT = {"k_exp_pm3d4": (1260.0, 12), "k_h2c_p1a": (230.0, 2), "k_h2c_p3": (420.0, 2), "k_dec_p1": (410.0, 2),
       "k_pair_miller_coop": (4300.0, 2), "k_final_coop": (2400.0, 2), "k_msm_aff_add": (210.0, 6)}
 KT_REC = {"k_rc_straus": (150000.0, 1), "k_kmsm_chunks": (65000.0, 1), "k_exp_pm3d4": (6600.0, 6)}
-KT_ADV = {"k_verify_groups": (90000.0, 9), "k_rs_sac": (85000.0, 1)}
+KT_ADV = {"k_ck_miller": (56000.0, 3), "k_ck_expsq": (5300.0, 15), "k_ck_prep": (8300.0, 3), "k_rs_sac": (64000.0, 1)}
+KT_NEG = {"k_exp_pm3d4": (1500.0, 40), "k_xq_sum": (900.0, 10), "k_xg_hlines": (3000.0, 30), "k_ck_miller": (4000.0, 30),
+          "k_ck_expsq": (700.0, 150)}
 
 
 def _free_port():
@@ -40,10 +42,17 @@ def _worker(rank, world, port, peaks, tables_out, q):
                "roofline": bench.roofline_of(KT_REC, {"k_rc_straus": 50000}, peak, None, "c3"),
                "kernel_avg_us": {k: v[0] for k, v in KT_REC.items()}, "note": "x" * 500}
         adv = {"metric": "adversarial", "value": 7600.0, "unit": "recovers/s",
-               "roofline": bench.roofline_of(KT_ADV, {"k_verify_groups": {"k_verify_groups[1]": 100,
-                                                                           "k_verify_groups[4]": 300}}, peak, None,
-                                             "c5"),
+               "roofline": bench.pipeline_roofline(KT_ADV, {1: 345000, 4: 360000}, 10000, peak, None, "c5"),
                "kernel_avg_us": {k: v[0] for k, v in KT_ADV.items()}}
+        neg = {"metric": "negative " * 20, "value": 5.1e6, "unit": "rounds/s", "steps": 10, "ms_per_step": 19.6,
+               "corrupted_rounds": 1000, "batch_fallbacks": 10, "checks_per_batch": [6250.0, 3700.0, 4000.0],
+               "isolation_kernel_share": 0.41,
+               "roofline": bench.xr_roofline(KT_NEG, [62500, 37000, 40000], 250000, peak),
+               "kernel_avg_us": {k: v[0] for k, v in KT_NEG.items()}, "note": "n" * 300}
+        vpn = {"metric": "vp negative " * 10, "value": 3.1e6, "unit": "partials/s", "s_per_step": 0.8,
+               "corrupted": 262000, "roofline": bench.pipeline_roofline(KT_ADV, {1: 900000, 4: 640000}, 10000, peak,
+                                                                        None, "c5vp"),
+               "kernel_avg_us": {k: v[0] for k, v in KT_ADV.items()}, "note": "v" * 200}
         cpu = None
         if rank == 0:
             th, machine, quota = bench.host_cores()
@@ -73,7 +82,8 @@ def _worker(rank, world, port, peaks, tables_out, q):
                 x["cpu_baseline"] = bench.cpu_label({"value": v, "unit": "x/s", "kind": "port", "sample": "stub"}, th,
                                                     machine, quota)
         line = bench.report(rank, world, head, roof, cpu, {"recover": rec, "adversarial": adv, "c1": c1,
-                                                           "live_latency": lat, "sync": syn, "c2_verify_all": c2},
+                                                           "live_latency": lat, "sync": syn, "c2_verify_all": c2,
+                                                           "c2_negative": neg, "vp_negative": vpn},
                             tables, tables_out)
         q.put((rank, "ok", line))
     except Exception as e:  # noqa: BLE001 -- report any failure of any rank to the test
@@ -104,7 +114,7 @@ def test_bench_report_world2(tmp_path, peak1):
     assert res[1][1] is None  # only rank 0 prints
     line = res[0][1]
     print("line bytes", len(line))
-    assert len(line) < 4096, len(line)
+    assert len(line) < 4608, len(line)  # the driver keeps the last 8 KB of the output
     d = json.loads(line)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
@@ -115,6 +125,8 @@ def test_bench_report_world2(tmp_path, peak1):
     assert d["c2_verify_all"]["value"] == 150000.0 and d["c2_verify_all"]["cpu_baseline"]["value"] == 40.0
     assert "kernel_avg_us" not in d["recover"] and "note" not in d["recover"]
     assert d["cpu_baseline"]["cores"] >= 1 and d["recover"]["cpu_baseline"]["value"] == 30.0
+    assert d["c2_negative"]["value"] == 5.1e6 and d["c2_negative"]["roofline"]["frac"] > 0
+    assert d["vp_negative"]["roofline"]["frac"] > 0 and d["adversarial"]["roofline"]["frac"] > 0
     side = json.load(open(out))
     assert side["recover"]["kernel_avg_us"]["k_rc_straus"] == 150000.0
 

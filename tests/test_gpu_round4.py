@@ -9,9 +9,9 @@ statuses, every share status; bit-exact):
 - the exact per-item mode (DG_GROUP=1: every examined share gets its own pairing check, no group tests) at a C5
   shape (n = 256, t = 129, 30% corrupted) in a child process;
 - the HBM-resident VerifyPartial + Recover-from-verdicts pair that bench.py times as configs[2];
-- the per-item pass in its A/B forms (child processes: the G2 group sums inside k_ck_prep, DG_CK_SPLIT=0; the
-  subgroup checks inside k_ck_prep, DG_CK_SUB_INLINE=1; the per-item kernels on the batch's own stream or on the
-  dedicated one, DG_SHARED_FB=1 / 0) with repeated and cancelling members inside group tests;
+- the per-item pass in its schedule variants (child processes: no speculative passes, DG_CK_PASSES=0, so every
+  unverified share takes the final pass alone; no first-pass margin, DG_CK_MARGIN0=0) with repeated and cancelling
+  members inside group tests;
 - asynchronous beacon batches consumed on the batch's own stream (dg_last_batch_stream)."""
 import hashlib
 import json
@@ -210,7 +210,7 @@ def test_pipeline_forms_with_repeated_and_cancelling_members(tmp_path):
     """n = 256, t = 129, 8 rounds, 15% corrupted, plus members that repeat (a partial copied whole over its neighbour:
     the same sigma twice in one group test -- the affine table's tangent case) and cancel (a neighbour's sigma
     negated: P + (-P) = O in the table) inside the examined prefix.  The default library and child processes with
-    the A/B forms of the per-item pass all give the twin's signatures and statuses."""
+    the schedule variants of the per-item pass all give the twin's signatures and statuses."""
     t, n, R = 129, 256, 8
     coeffs, commits, shares = group(t, n)
     msgs = [hashlib.sha256(b"forms/%d" % r).digest() for r in range(R)]
@@ -233,8 +233,7 @@ def test_pipeline_forms_with_repeated_and_cancelling_members(tmp_path):
     inp = tmp_path / "in.npz"
     np.savez(inp, commits=np.array([list(c) for c in commits], np.uint8), msgs=np.array([list(m) for m in msgs],
              np.uint8), parts=parts, t=t, n=n)
-    for k, (var, val) in enumerate([("DG_CK_SPLIT", "0"), ("DG_CK_SUB_INLINE", "1"), ("DG_SHARED_FB", "1"),
-                                    ("DG_SHARED_FB", "0")]):
+    for k, (var, val) in enumerate([("DG_CK_PASSES", "0"), ("DG_CK_MARGIN0", "0")]):
         out = tmp_path / ("out%d.npz" % k)
         r = subprocess.run([sys.executable, "-c", _FORM_CHILD, ROOT, str(inp), str(out)],
                            env=dict(os.environ, **{var: val}), capture_output=True, text=True, timeout=300, cwd=ROOT)

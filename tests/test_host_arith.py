@@ -336,3 +336,25 @@ def test_check_pipeline_matches_pair_check(hc):
         h = out.raw
         for sig, np_ in ((bytes(sigs[i]), 3), (bytes(sigs[i + 1]), 3), (bytes(sigs[i]), 1), (bytes(sigs[i]), 2)):
             assert hc.hc_ck_pipeline_check(pk, h, sig, np_) == 1, (i, np_)
+
+
+def test_xr_quad_sum_matches_double_and_add(hc):
+    """xr.h xq_sum4 -- the cross-round isolation's quad sums sum rho_i P_i (k_xq_sum: the affine 8-entry table built in
+    the lane, one Fp inversion per level, the sign-aligned column loop) -- equals double-and-add per point: distinct
+    points, a repeated point, a point and its negation, the identity, 1..4 live members, edge coefficients."""
+    c = load("chain_t3n5.json")
+    sigs = [hx(r["sig"]) for r in c["rounds"][:8]]
+    neg = lambda s: bytes([s[0] ^ 0x20]) + s[1:]
+    ident = bytes([0xc0]) + bytes(95)
+    rng = random.Random(11)
+    groups = [sigs[0:4], sigs[4:8], [sigs[0], sigs[0], sigs[1], sigs[2]], [sigs[0], neg(sigs[0]), sigs[3], sigs[3]],
+              [ident, sigs[1], sigs[2], sigs[3]], [sigs[5], ident, ident, neg(sigs[5])], [sigs[6]] * 4]
+    rhos = [[rng.getrandbits(64) | 1 for _ in range(4)] for _ in range(3)]
+    rhos += [[1, 1, 1, 1], [(1 << 64) - 1, 1 << 63, 3, (1 << 64) - 1], [2, 4, 6, 8], [5, 5, (1 << 64) - 5, 5]]
+    hc.hc_xq_sum_check.restype = ctypes.c_int
+    for gi, g in enumerate(groups):
+        buf = b"".join(g)
+        for rho in rhos:
+            arr = (ctypes.c_uint64 * 4)(*rho)
+            for nl in (1, 2, 3, 4):
+                assert hc.hc_xq_sum_check(buf, arr, nl) == 1, (gi, rho, nl)

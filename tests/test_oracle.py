@@ -188,3 +188,41 @@ def test_torsion_fixture_decodes_outside_g2():
         assert B.G2C.on_curve(pt) and not B.g2_in_subgroup(pt)
         msg = hx(c["rounds"][case["round_index"]]["msg"])
         assert twin.verify(pk, msg, hx(case["sig"])) == 2
+
+
+def _ref_points():
+    t = load("reference_test_json_points.json")
+    return [hx(p["hex"]) for p in t["points"]]  # Public (G2), Previous (G1), Signature (G1)
+
+
+def _g2_variants(pub):
+    """Public's c0 <-> c1 swap (flags kept on the first half), the compression flag cleared, the infinity flag set
+    with a non-zero body, the sign flag flipped (the negated point: still valid)."""
+    swapped = bytes([pub[48] | (pub[0] & 0xE0)]) + pub[49:96] + bytes([pub[0] & 0x1F]) + pub[1:48]
+    return {"swapped": swapped, "uncompressed_flag": bytes([pub[0] & 0x7F]) + pub[1:],
+            "infinity_flag": bytes([pub[0] | 0x40]) + pub[1:], "sign_flipped": bytes([pub[0] ^ 0x20]) + pub[1:]}
+
+
+def test_reference_test_json_points_decode():
+    """The reference's only G2 encoding (test/test-integration/test.json:5, `Public` = x g2) and its two G1 signatures
+    (`Previous`, `Signature`; json_output.go:22,27) decode in pyref (on the curve, in the subgroup) and re-encode byte
+    for byte; the twin decodes them too: as (key, sigma) of a bls.Verify they give a pairing failure (status 1), not a
+    decode error (2, 4).  Swapping Public's c0 and c1 halves, clearing its compression flag or setting its infinity
+    flag makes it undecodable for both (status 2); flipping its sign flag gives the valid negated point (status 1).
+    This pins G2 decompression's c1 || c0 order and flag handling to data the reference holds."""
+    pub, prev, sig = _ref_points()
+    assert B.g2_compress(B.g2_decompress(pub)) == pub
+    for g1 in (prev, sig):
+        assert B.g1_compress(B.g1_decompress(g1)) == g1
+    msg = hashlib.sha256(b"test.json").digest()
+    for g1 in (prev, sig):
+        assert twin.verify(g1, msg, pub) == 1
+    want = {"swapped": 2, "uncompressed_flag": 2, "infinity_flag": 2, "sign_flipped": 1}
+    for name, v in _g2_variants(pub).items():
+        assert twin.verify(sig, msg, v) == want[name], name
+        try:
+            B.g2_decompress(v)
+            py = 1
+        except B.DecodeError:
+            py = 2
+        assert py == want[name], name

@@ -62,7 +62,7 @@ def main(dst):
         pc = product_counts(tmp)
         lines.append("# v_mad_u64_u32 per product (fp28.h, radix 2^28, 14 digits): %s" % pc)
         lines.append("# kernel  total  v_mad_u64_u32  share   (static instruction counts of the built objects)")
-        for tu in ("drand_gpu.o", "kernels_hot.o", "kernels_verify.o"):
+        for tu in ("drand_gpu.o", "kernels_hot.o"):
             m = mix(disasm(os.path.join(ROOT, "drand_amd", "csrc", tu), tmp))
             for k, v in sorted(m.items()):
                 if not k.startswith("k_"):

@@ -364,12 +364,13 @@ extern "C" void oc_recover_sac(const uint8_t* sigs96, const uint32_t* idx, uint3
   take(out + 6);
 }
 
-// Recover's pairing-check pipeline (checks.h) for one check of m shares of one round: per kernel, in the order of
-// out (3 counters each): 0 k_ck_prep (m subgroup checks, the weighted sums and their affine forms), 1 k_ck_lines2
-// (the 68 lines of the pair (-g1, b)), 2 k_ck_miller, 3 k_ck_fe1, 4 k_ck_inv (+ the batch inversion's ~3 products
-// per value), 5 k_ck_mul (all eleven launches of a check together), 6 k_ck_expsq (all five), 7 k_ck_expdec (all five,
-// + the batch inversion's 3 products per value for the 6 norms of each), 8 k_ck_round_lines (per ROUND: h_eff and
-// the 68 lines of H_r).  No zero Karabina denominator occurs on these inputs (k_ck_explain: none).
+// The pairing-check pipeline (checks.h) for one check of m shares of one round: per kernel, in the order of out (3
+// counters each): 0 k_ck_prep (m subgroup checks, the weighted sums and their affine forms), 1 k_ck_lines2 (the 68 lines
+// of the pair (-g1, b)), 2 k_ck_miller, 3 k_ck_easy (f^-1 with the lane's Fp inversion, f1, f2), 4 k_ck_expsq (all
+// five), 5 k_ck_expdec (all five: the lane's Montgomery trick over the 6 norms and its Fp inversion, decompression,
+// the fused next factor), 6 k_ck_final, 7 k_ck_round_lines (per ROUND: h_eff and the 68 lines of H_r; the cross-round
+// isolation's k_xg_hlines is the same per check).  No zero Karabina denominator occurs on these inputs (k_ck_explain:
+// none).
 extern "C" void oc_check_pipeline(const uint8_t* pk48s, const uint8_t* msg, const uint8_t* dst, uint32_t dl,
                                   const uint8_t* sigs96, uint32_t m, uint64_t* out) {
   G2J q = hash_to_g2_uncleared(msg, 32, dst, dl);
@@ -379,14 +380,11 @@ extern "C" void oc_check_pipeline(const uint8_t* pk48s, const uint8_t* msg, cons
     g1_decompress(pk[i], pk48s + 48 * i, false);
     g2_decompress(s[i], sigs96 + 96 * i, false);
   }
-  auto bump = [](uint64_t* o, uint32_t n) {  // Montgomery's trick of a batch inversion: ~3 products per value
-    o[0] += 3ull * n;
-  };
   reset();
   const G2A h = g2_to_aff(g2_clear_cofactor(q));
   std::vector<CkLine> l1(CK_STEPS), l2(CK_STEPS);
   ck_lines(h.x, h.y, [&](uint32_t st, const CkLine& l) { l1[st] = l; });
-  take(out + 24);
+  take(out + 21);
   reset();
   for (uint32_t i = 0; i < m; ++i) (void)g2_in_subgroup_aff(s[i].x, s[i].y);
   G1A a = pk[0];
@@ -413,22 +411,11 @@ extern "C" void oc_check_pipeline(const uint8_t* pk48s, const uint8_t* msg, cons
   reset();
   CkInv inv;
   const Fp nt = ck_fe1(f, inv);
+  const Fp12 f1 = ck_mul_op(ck_inv(f, inv, fp_inv(nt)), f, 0, 1);
+  const Fp12 f2 = ck_mul_op(f1, f1, 2, 0);
   take(out + 9);
-  const Fp nti = fp_inv(nt);
-  reset();
-  const Fp12 finv = ck_inv(f, inv, nti);
-  take(out + 12);
-  bump(out + 12, 1);
-  uint64_t mul[3] = {0, 0, 0}, sq[3] = {0, 0, 0}, dec[3] = {0, 0, 0};
-  auto mulop = [&](const Fp12& x, const Fp12& y, uint32_t nf, uint32_t cj) {
-    uint64_t t[3];
-    reset();
-    const Fp12 r = ck_mul_op(x, y, nf, cj);
-    take(t);
-    for (int k = 0; k < 3; ++k) mul[k] += t[k];
-    return r;
-  };
-  auto expz = [&](const Fp12& x) {
+  uint64_t sq[3] = {0, 0, 0}, dec[3] = {0, 0, 0};
+  auto expz = [&](const Fp12& x, const Fp12* y, uint32_t nf, uint32_t cj) {
     CycC sn[CK_NPOW];
     Fp nv[CK_NPOW];
     uint64_t t[3];
@@ -436,26 +423,60 @@ extern "C" void oc_check_pipeline(const uint8_t* pk48s, const uint8_t* msg, cons
     (void)ck_expsq(x, [&](int i, const CycC& c, const Fp& n) { sn[i] = c; nv[i] = n; });
     take(t);
     for (int k = 0; k < 3; ++k) sq[k] += t[k];
-    Fp ni[CK_NPOW];
-    for (int i = 0; i < CK_NPOW; ++i) ni[i] = fp_inv(nv[i]);
     reset();
-    const Fp12 r = ck_expdec([&](int i, CycC& c, Fp& n) { c = sn[i]; n = ni[i]; });
+    ck_inv6([&](int i) { return nv[i]; }, [&](int i, const Fp& v) { nv[i] = v; });
+    Fp12 r = ck_expdec([&](int i, CycC& c, Fp& n) { c = sn[i]; n = nv[i]; });
+    if (y) r = ck_mul_op(r, *y, nf, cj);
     take(t);
     for (int k = 0; k < 3; ++k) dec[k] += t[k];
-    dec[0] += 3ull * CK_NPOW;
     return r;
   };
-  const Fp12 f1 = mulop(finv, f, 0, 1);
-  const Fp12 f2 = mulop(f1, f1, 2, 0);
-  const Fp12 t0 = mulop(expz(f2), f2, 0, 1);
-  const Fp12 t1 = mulop(expz(t0), t0, 0, 1);
-  const Fp12 aa = mulop(expz(t1), t1, 1, 0);
-  const Fp12 bb = mulop(mulop(expz(expz(aa)), aa, 2, 0), aa, 0, 1);
-  const Fp12 cc = mulop(mulop(f2, f2, 0, 0), f2, 0, 0);
-  (void)mulop(bb, cc, 0, 0);
+  const Fp12 t0 = expz(f2, &f2, 0, 1);
+  const Fp12 t1 = expz(t0, &t0, 0, 1);
+  const Fp12 aa = expz(t1, &t1, 1, 0);
+  const Fp12 tt = expz(expz(aa, nullptr, 0, 0), &aa, 2, 0);
+  reset();
+  const Fp12 cc = ck_mul_op(ck_mul_op(f2, f2, 0, 0), f2, 0, 0);
+  (void)ck_mul_op(ck_mul_op(tt, aa, 0, 1), cc, 0, 0);
+  take(out + 18);
   for (int k = 0; k < 3; ++k) {
-    out[15 + k] = mul[k];
-    out[18 + k] = sq[k];
-    out[21 + k] = dec[k];
+    out[12 + k] = sq[k];
+    out[15 + k] = dec[k];
   }
+}
+
+// The cross-round isolation (xr.h) per unit: out[0..2] k_xq_sum (one quad side: four signatures with the coefficients
+// rho), out[3..5] k_xg_prep of a level-1 group of qpg quads (2 (qpg - 1) Jacobian additions, the affine sigma sum),
+// out[6..8] k_xg_prep of a level-2 quad (the affine sigma sum)
+extern "C" void oc_xr_units(const uint8_t* sigs96, uint32_t qpg, uint64_t* out) {
+  G2A P[4];
+  for (int i = 0; i < 4; ++i) g2_decompress(P[i], sigs96 + 96 * i, false);
+  uint64_t rho[4];
+  for (int i = 0; i < 4; ++i) rho[i] = rlc_coeff(0x5eed, (uint64_t)i);
+  G2A T[8];
+  G2J acc;
+  reset();
+  xq_sum4([&](uint32_t m) { return P[m]; }, rho, [&](uint32_t u) { return T[u]; },
+          [&](uint32_t u, const G2A& t) { T[u] = t; }, acc);
+  take(out);
+  // qpg distinct quad sums (other coefficients), uncounted
+  std::vector<G2J> qs;
+  for (uint32_t q = 0; q < qpg; ++q) {
+    for (int i = 0; i < 4; ++i) rho[i] = rlc_coeff(0x5eed + q, (uint64_t)i);
+    G2J a2;
+    xq_sum4([&](uint32_t m) { return P[m]; }, rho, [&](uint32_t u) { return T[u]; },
+            [&](uint32_t u, const G2A& t) { T[u] = t; }, a2);
+    qs.push_back(a2);
+  }
+  reset();
+  G2J h = qs[0], sg = qs[0];
+  for (uint32_t q = 1; q < qpg; ++q) {
+    h = jac_add(h, qs[q]);
+    sg = jac_add(sg, qs[q]);
+  }
+  (void)g2_to_aff(sg);
+  take(out + 3);
+  reset();
+  (void)g2_to_aff(acc);
+  take(out + 6);
 }

@@ -77,23 +77,26 @@ def main():
         add("k_recover_terms")
         if i < 8:
             L.oc_verify_item(pk, msg, 32, DST, len(DST), sig, o)
-            add("k_verify_items")
+            add("pair_check (one bls.Verify, single lane)")
             nxt4 = b"".join(bytes.fromhex(rounds[(i + q) % len(rounds)]["sig"]) for q in range(4))
-            for m in range(1, 5):
-                L.oc_verify_group(pk * m, msg, DST, len(DST), nxt4[:96 * m], m, o)
-                add("k_verify_groups[%d]" % m)
-            ck = (ctypes.c_uint64 * 27)()
+            ck = (ctypes.c_uint64 * 24)()
             for m in range(1, 5):
                 L.oc_check_pipeline(pk * m, msg, DST, len(DST), nxt4[:96 * m], m, ck)
-                for q, kname in ((0, "k_ck_prep[%d]" % m), (1, "k_ck_lines2"), (2, "k_ck_miller"), (3, "k_ck_fe1"),
-                                 (4, "k_ck_inv"), (5, "k_ck_mul (11 per check)"), (6, "k_ck_expsq (5 per check)"),
-                                 (7, "k_ck_expdec (5 per check)"), (8, "k_ck_round_lines (per round)")):
-                    if m > 1 and not kname.startswith("k_ck_prep") and q != 8:
+                for q, kname in ((0, "k_ck_prep[%d]" % m), (1, "k_ck_lines2"), (2, "k_ck_miller"), (3, "k_ck_easy"),
+                                 (4, "k_ck_expsq (5 per check)"), (5, "k_ck_expdec (5 per check)"), (6, "k_ck_final"),
+                                 (7, "k_ck_round_lines (per round)")):
+                    if m > 1 and not kname.startswith("k_ck_prep"):
                         continue  # the same per check whatever m (the Miller loop's G1 point only)
-                    if m > 1 and q == 8:
-                        continue
                     o[0], o[1], o[2] = ck[3 * q], ck[3 * q + 1], ck[3 * q + 2]
                     add(kname)
+                    if q == 7:
+                        add("k_xg_hlines")  # the same work per cross-round check (h_eff and 68 lines)
+            xr = (ctypes.c_uint64 * 9)()
+            L.oc_xr_units(nxt4, 4, xr)
+            for q, kname in ((0, "k_xq_sum (per quad side)"), (1, "k_xg_prep[level 1, 4 quads]"),
+                             (2, "k_xg_prep[level 2]")):
+                o[0], o[1], o[2] = xr[3 * q], xr[3 * q + 1], xr[3 * q + 2]
+                add(kname)
             L.oc_batch_final(pk, sig, nxt, o)
             add("k_pair_miller+k_final_check")
     # Recover's per-round MSM at n = 64, t = 33: the C3 index set (0..32: every share valid, input order) and a

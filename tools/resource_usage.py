@@ -45,7 +45,7 @@ def kernels_of(obj, tmp):
 def main(dst):
     rows = []
     with tempfile.TemporaryDirectory() as tmp:
-        for tu in ("drand_gpu.o", "kernels_hot.o", "kernels_verify.o") + tuple("kernels_check_%s.o" % p for p in "abcde"):
+        for tu in ("drand_gpu.o", "kernels_hot.o") + tuple("kernels_check_%s.o" % p for p in "abcdef"):
             for k in kernels_of(os.path.join(ROOT, "drand_amd", "csrc", tu), tmp):
                 rows.append([tu.replace(".o", ""), k[".name"]] + [k.get(f, "") for f in FIELDS])
     rows.sort(key=lambda r: (-int(r[7] or 0), r[1]))
