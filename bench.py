@@ -647,6 +647,27 @@ def sync_bench(chain_sigs, R, batch=25000):
             "note": "host Beacon objects -> dg_check_links + dg_verify_beacons per batch (host-buffer API, blocking)"}
 
 
+MAX_BATCH = 524288  # rounds per device batch by default at most (~6 GB of workspace per set at this size)
+
+
+def batch_bounds(n, batch=0):
+    """The device batches of a rank's n rounds: [(lo, hi)], contiguous and balanced.  batch = 0 (default): one batch
+    when n <= MAX_BATCH -- at N = 8 the 1M chain gives every rank 125k rounds, so each rank runs the N = 1 step (one
+    batch, its verdicts packed and all-gathered on the batch's own stream) instead of two batches and a side stream;
+    at N = 2 and 4 (500k, 250k rounds) one batch as well."""
+    cap = batch if batch > 0 else MAX_BATCH
+    nb = max(1, -(-n // cap))
+    return [(n * i // nb, n * (i + 1) // nb) for i in range(nb)]
+
+
+def consume_on_batch_stream(nbatches, use_sync=False):
+    """Whether a step's consumers (the bitmap pack and its RCCL all-gather) go on the batch's own stream
+    (dg_last_batch_stream) -- no cross-stream wait at all, which with HIP's default 4 hardware queues stalls whatever
+    shares the waiting queue (DESIGN.md §5.3) -- at every world size when the rank's step is one asynchronous batch;
+    several batches (or the blocking entry point) need a side stream that waits for them all."""
+    return nbatches == 1 and not use_sync
+
+
 def negative_positions(G):
     """Global 0-based positions of the corrupted rounds of the negative lines: 1% of G, the deterministic positions
     of tests/test_gpu_round2.py::test_sharded_1m_chain_equals_one_batch."""
@@ -927,7 +948,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--global-rounds", type=int, default=0,
                     help="rounds per step over all GPUs (default 100k at N = 1, the 1M chain at N > 1)")
-    ap.add_argument("--batch", type=int, default=100000, help="max rounds per device batch")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="max rounds per device batch (default: the rank's whole range in one batch up to %d rounds, "
+                         "so every rank runs the N = 1 step)" % MAX_BATCH)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--allow-unlinked", action="store_true",
                     help="without a digest-pinned chain file, measure GPU-signed unlinked rounds (labelled so in "
@@ -1007,8 +1030,8 @@ def main():
         prev, sigs = gpu_signed_rounds(tbls, a + 1, n, x)
         data = "synthetic rounds, GPU-signed (no chain file: prev_sig pseudo-random, links not checked)"
         linked = False
-    nb = max(1, -(-n // args.batch))
-    bounds = [(n * i // nb, n * (i + 1) // nb) for i in range(nb)]
+    bounds = batch_bounds(n, args.batch)
+    nb = len(bounds)
     mbytes = (max(y - x_ for x_, y in (shard.round_range(G, world, q) for q in range(world))) + 7) // 8
     rounds = np.arange(a + 1, b + 1, dtype=np.uint64)
     prev_sigs = [bytes(p) for p in prev]
@@ -1032,7 +1055,7 @@ def main():
     # one batch per step on one rank: the verdict bitmap is packed on the batch's own stream (dg_last_batch_stream), so
     # no cross-stream wait is queued -- with HIP's default 4 hardware queues a wait on a queue shared with another
     # workspace set stalls that set; several batches or ranks: a side stream waits for them all
-    on_set = world == 1 and len(bounds) == 1 and not args.use_sync
+    on_set = consume_on_batch_stream(len(bounds), args.use_sync)
 
     sig_src = [d_sig]  # the signatures the steps verify (the c2_negative line swaps in a corrupted copy)
 
@@ -1178,7 +1201,8 @@ def main():
             "config": {"workload": ("batch bls.Verify / beacon.VerifyBeacon of the %d-round linked chain per "
                                     "step, %d contiguous range(s) of <= %d rounds per GPU in batches of <= %d, "
                                     "one shared group key (BASELINE configs[%d])"
-                                    % (G, world, -(-G // world), args.batch, 1 if G <= 100000 else 3)),
+                                    % (G, world, -(-G // world), max(y - x_ for x_, y in bounds),
+                                       1 if G <= 100000 else 3)),
                        "global_rounds": G, "rounds_per_gpu": n, "batches_per_gpu": nb,
                        "hip_hw_queues": hw_queues,
                        "parallelism": "rounds sharded dp%d" % world},

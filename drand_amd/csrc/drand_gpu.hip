@@ -94,13 +94,6 @@ int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
-// a power of two in [1, hi] from the environment (rounded down), else dflt
-uint32_t env_pow2(const char* name, uint32_t dflt, uint32_t hi) {
-  const int v = env_int(name, (int)dflt);
-  uint32_t p = 1;
-  while (p * 2 <= (uint32_t)(v < 1 ? 1 : v) && p * 2 <= hi) p *= 2;
-  return p;
-}
 
 struct Ctx {
   int device = -1;
@@ -147,35 +140,32 @@ struct Ctx {
   uint8_t* d_dst = nullptr;
   XmdTail* d_xmd = nullptr;
   bool dst_dev_valid = false;
-  // hash-to-G2 and sigma decode as the phase kernels of phases.h (default) or the fused one-lane kernels
-  // (DG_FUSED=1: A/B only)
-  bool phased = getenv("DG_FUSED") == nullptr;
-  // single-key MSM first levels as mixed Jacobian chunk sums (DG_MSM_JAC=1: A/B only) instead of affine levels
-  bool msm_jac = getenv("DG_MSM_JAC") != nullptr;
-  // single-key MSM bucket stage (msm_run): lanes per bucket over the affine chunk sums (a power of two <= MSM_BSPLIT),
-  // and the row-sum fan-in of their partials and of the slice partials (2: pairwise levels; larger: fewer launches,
-  // longer chains per lane)
-  uint32_t msm_bsplit = env_pow2("DG_MSM_BSPLIT", MSM_BSPLIT, MSM_BSPLIT);
-  uint32_t msm_fold = env_pow2("DG_MSM_FOLD", 2, 64);
-  uint32_t slice_fold = env_pow2("DG_SLICE_FOLD", 2, 64);
-  // batch inversions by the chunked form only (DG_BINV_CHUNKED=1: A/B only) instead of the block tree
-  bool binv_chunked = getenv("DG_BINV_CHUNKED") != nullptr;
-  // batched subgroup check as its own launch after the final exponentiation (DG_SUB_SEPARATE=1: A/B only)
-  bool sub_separate = getenv("DG_SUB_SEPARATE") != nullptr;
+  // single-key MSM bucket stage (msm_run): lanes per bucket over the affine chunk sums, and the row-sum fan-in of
+  // their partials and of the slice partials (pairwise levels: each level is one dependent addition per lane, and
+  // longer chains on a nearly empty chip measured slower)
+  static constexpr uint32_t msm_bsplit = MSM_BSPLIT, msm_fold = 2, slice_fold = 2;
 };
 
 std::mutex g_mu;
 Ctx g_ctx;
 
 // HIP's hardware queues per process (GPU_MAX_HW_QUEUES, default 4) are read once, when the runtime starts (the
-// process's first HIP call).  The library keeps up to DG_SETS = 10 batches in flight on streams of their own plus the
-// per-item stream, and with 4 queues those streams share queues: a cross-stream wait queued on a shared queue holds
-// every stream behind it (7.9 M against 14 M verified rounds/s).  So when the library is loaded
-// and the process has not chosen a value, it asks for kDefaultHwQueues -- for a program linked against it (the cgo
-// drand binary) this runs before main, so before any HIP call.  An explicit GPU_MAX_HW_QUEUES (any value) is kept;
-// a process that started HIP before loading the library keeps the queues it has.
+// process's first HIP call).  The library keeps up to 10 batches in flight on streams of their own, and with 4 queues
+// those streams share queues: a cross-stream wait queued on a shared queue holds every stream behind it (DESIGN.md
+// §5.3).  So when the library is loaded and the process has not chosen a value, it asks for kDefaultHwQueues -- for a
+// program linked against it (the cgo drand binary) this runs before main, so before any HIP call.  An explicit
+// GPU_MAX_HW_QUEUES (any value) is kept.  A process that started HIP BEFORE loading the library (torch imported and
+// used first, with the variable unset) keeps HIP's 4 queues while the environment says 16: dg_init cannot query the
+// runtime's count, so it warns once when the value is the library's own (g_hwq_supplied) -- such a process should set
+// GPU_MAX_HW_QUEUES before its first HIP call (bench.py does).
 constexpr const char* kDefaultHwQueues = "16";
-__attribute__((constructor)) void dg_default_hw_queues() { setenv("GPU_MAX_HW_QUEUES", kDefaultHwQueues, 0); }
+bool g_hwq_supplied = false;
+__attribute__((constructor)) void dg_default_hw_queues() {
+  if (!getenv("GPU_MAX_HW_QUEUES")) {
+    setenv("GPU_MAX_HW_QUEUES", kDefaultHwQueues, 0);
+    g_hwq_supplied = true;
+  }
+}
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {
@@ -273,15 +263,6 @@ int launch_shm(const char* name, void (*k)(Args...), uint32_t n_threads, uint32_
 template <typename... Args>
 int launch(const char* name, void (*k)(Args...), uint32_t n_threads, uint32_t block, hipStream_t st, Args... args) {
   return launch_shm(name, k, n_threads, block, 0u, st, args...);
-}
-// DG_VERIFY_LDS=<bytes> (A/B only): dynamic LDS per workgroup of the per-item pairing kernels, which caps their
-// workgroups (one wave each) per CU and so the scratch they keep in flight
-uint32_t verify_lds() {
-  static const uint32_t v = [] {
-    const char* e = getenv("DG_VERIFY_LDS");
-    return e ? (uint32_t)atoi(e) : 0u;
-  }();
-  return v;
 }
 template <typename... Args>
 int launch_shm(const char* name, void (*k)(Args...), uint32_t n_threads, uint32_t block, uint32_t shm, hipStream_t st,
@@ -461,7 +442,7 @@ int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JSt
   uint32_t *offset = cnt + nbk, *cursor = offset + nbk, *chunk_off = cursor + nbk;
   RET(wsT(S_MSM_LIST, (size_t)nwin * R + 1, &list));
   if (affine && !bad) return fail(DG_E_ARG, "msm_run: the affine levels need a failure flag");
-  if (affine && !g_ctx.msm_jac) {
+  if (affine) {
     const size_t E = (size_t)nwin * R;
     if (E * nsides > 0x7fffffffull) return fail(DG_E_ARG, "batch too large for the MSM");
     uint32_t* gofs = chunk_off + nbk + 1;
@@ -550,7 +531,7 @@ int msm_run_keyed(const Batch& b, const uint64_t* seed, const uint8_t* iso, bool
   RET(launch("k_kmsm_count", k_kmsm_count, N, 256, st, N, b.k, nsets, nwin, seed, b.item_slot, (const uint8_t*)b.status,
              iso, cnt));
   const size_t E = (size_t)nwin * N;
-  const bool aff = !g_ctx.msm_jac && E + nkeys < 0x7fffffffull;  // affine first levels (DG_MSM_JAC=1: chunk sums)
+  const bool aff = E + nkeys < 0x7fffffffull;  // affine first levels (else: Jacobian chunk sums)
   auto scan = [&](uint32_t div, uint32_t* groups) -> int {
     RET(launch("k_kscan_local", k_kscan_local, nblocks * 256, 256, st, nkeys, div, (const uint32_t*)cnt, offset, groups,
                tot));
@@ -613,22 +594,18 @@ int msm_run_keyed(const Batch& b, const uint64_t* seed, const uint8_t* iso, bool
 int decode_items(uint32_t N, uint32_t k, uint32_t nslots, const uint8_t* sigs, uint32_t stride, uint32_t offset,
                  const uint32_t* item_slot, const uint8_t* key_status, G2AStore* S, uint8_t* status, uint32_t* cell,
                  uint8_t* iso, uint32_t sub, hipStream_t st) {
-  if (g_ctx.phased) {
-    // phases.h: flags / x, the two roots through k_exp_pm3d4, then y, sign and the cell claim
-    DecState* ds;
-    Fp *ein, *eout;
-    RET(wsT(S_DECST, N, &ds));
-    RET(wsT(S_DEIN, N, &ein));
-    RET(wsT(S_DEOUT, N, &eout));
-    RET(launch("k_dec_p1", k_dec_p1, N, 128, st, N, sigs, stride, offset, item_slot, key_status, ds, ein, status));
-    RET(launch("k_exp_pm3d4", k_exp_pm3d4, N, 128, st, N, (const Fp*)ein, eout));
-    RET(launch("k_dec_p2", k_dec_p2, N, 128, st, N, ds, ein, (const Fp*)eout, status));
-    RET(launch("k_exp_pm3d4", k_exp_pm3d4, N, 128, st, N, (const Fp*)ein, eout));
-    return launch("k_dec_p3", k_dec_p3, N, 128, st, N, k, nslots, item_slot, (const DecState*)ds, (const Fp*)ein,
-                  (const Fp*)eout, S, status, cell, iso, sub);
-  }
-  return launch("k_decode_items", k_decode_items, N, 128, st, N, k, nslots, sigs, stride, offset, item_slot, key_status, S,
-                status, cell, iso, sub);
+  // phases.h: flags / x, the two roots through k_exp_pm3d4, then y, sign and the cell claim
+  DecState* ds;
+  Fp *ein, *eout;
+  RET(wsT(S_DECST, N, &ds));
+  RET(wsT(S_DEIN, N, &ein));
+  RET(wsT(S_DEOUT, N, &eout));
+  RET(launch("k_dec_p1", k_dec_p1, N, 128, st, N, sigs, stride, offset, item_slot, key_status, ds, ein, status));
+  RET(launch("k_exp_pm3d4", k_exp_pm3d4, N, 128, st, N, (const Fp*)ein, eout));
+  RET(launch("k_dec_p2", k_dec_p2, N, 128, st, N, ds, ein, (const Fp*)eout, status));
+  RET(launch("k_exp_pm3d4", k_exp_pm3d4, N, 128, st, N, (const Fp*)ein, eout));
+  return launch("k_dec_p3", k_dec_p3, N, 128, st, N, k, nslots, item_slot, (const DecState*)ds, (const Fp*)ein,
+                (const Fp*)eout, S, status, cell, iso, sub);
 }
 
 int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out = nullptr) {
@@ -671,7 +648,7 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
   G2JStore* win = nullptr;
   if (b.nslots == 1) {
     // T = sum alpha_r V_r and K = sum alpha_r Q_r in one MSM (shared bucket sort)
-    RET(msm_run(b.R, seed, active, V, b.Q, batched_sub != 0, g_ctx.phased && b.k == 1, &msm, &win, st, flag + 2));
+    RET(msm_run(b.R, seed, active, V, b.Q, batched_sub != 0, b.k == 1, &msm, &win, st, flag + 2));
     T = msm;
     K = msm + 1;
   } else {
@@ -691,7 +668,7 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
     K = Kp;
     // Kc = sum over the active rounds of alpha_r Q_r (one MSM), Xc = sum_s beta_s X_s
     G2JStore* kmsm;
-    RET(msm_run(b.R, seed, active, b.Q, nullptr, false, g_ctx.phased, &kmsm, nullptr, st, flag + 2));
+    RET(msm_run(b.R, seed, active, b.Q, nullptr, false, true, &kmsm, nullptr, st, flag + 2));
     Kc = kmsm;
     RET(wsT(S_XC, 1, &Xc));
     RET(launch("k_key_combine", k_key_combine, 256, 256, st, b.nslots, seed, b.keys, b.key_status, Xc));
@@ -700,11 +677,8 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
   // the batched subgroup check's window sums ride in the Miller launch (extra workgroups); k_final_coop folds
   // their verdict (flag[2]) into the batch's
   const uint32_t nsub = batched_sub ? MSM_WT * (b.nslots > 1 ? b.nslots : 1u) : 0u;
-  const bool fuse_sub = !g_ctx.sub_separate;
-  RET(launch("k_pair_miller_coop", k_pair_miller_coop, 128 * (npairs + (fuse_sub ? nsub : 0u)), 128, st, b.nslots, seed,
+  RET(launch("k_pair_miller_coop", k_pair_miller_coop, 128 * (npairs + nsub), 128, st, b.nslots, seed,
              b.keys, K, T, (const G1AStore*)Xc, Kc, f, npairs, (const G2JStore*)win, flag + 2));
-  if (!fuse_sub && nsub)
-    RET(launch("k_msm_subgroup", k_msm_subgroup, 128 * nsub, 128, st, (const G2JStore*)win, flag + 2));
   RET(launch("k_final_coop", k_final_coop, 128, 128, st, npairs, (const Fp12*)f, flag, (const uint32_t*)flag + 2));
   // isolated items present?  The per-item pass decides on the device (no host round trip), so a batch
   // is one stream-ordered sequence of launches.
@@ -778,7 +752,6 @@ int decode_key(const uint8_t* pk48_host, hipStream_t st, G1AStore** keys, uint8_
 int batch_inv_chunked(uint32_t n, const Fp* vals, Fp* out, hipStream_t st, Slot slot);
 int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st) {
   constexpr uint32_t PER = BINV_T * BINV_K;
-  if (g_ctx.binv_chunked) return batch_inv_chunked(n, vals, out, st, S_BINV);
   if (n <= BINV_T * BINV_R) return launch("k_binv_blk_root", k_binv_blk_root, BINV_T, BINV_T, st, n, vals, out);
   // block tree (phases.h k_binv_blk_*): per block of PER values a root; the roots by the chunked form
   const uint32_t nb = (n + PER - 1) / PER;
@@ -848,9 +821,6 @@ int hash_rounds(uint32_t R, const uint8_t* d_msgs, uint32_t msg_len, hipStream_t
   RET(ensure_dst());
   d_dst = g_ctx.d_dst;
   RET(wsT(S_Q, R, Q));
-  if (!g_ctx.phased)
-    return launch("k_h2c_uncleared", k_h2c_uncleared, R, 128, st, R, d_msgs, msg_len, (const uint8_t*)d_dst,
-                  (uint32_t)g_ctx.dst.size(), (const XmdTail*)g_ctx.d_xmd, *Q);
   // phases.h: two maps per round, every exponentiation through k_exp_pm3d4
   const uint32_t M = 2 * R;
   H2cMap* hs;
@@ -1432,6 +1402,11 @@ int dg_init(int device) {
   if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
     return fail(DG_E_NODEV, std::string("not a gfx950 device: ") + prop.gcnArchName);
   HIPCHK(hipSetDevice(device));
+  if (g_hwq_supplied && !getenv("DG_QUIET"))
+    fprintf(stderr, "[drand_gpu] GPU_MAX_HW_QUEUES was unset: the library asked for %s hardware queues and plans %d "
+                    "workspace sets for them; a process that started HIP before loading the library has HIP's 4 -- set "
+                    "GPU_MAX_HW_QUEUES before the first HIP call (DG_QUIET=1 silences this)\n",
+            kDefaultHwQueues, active_sets());
   for (Set& x : g_ctx.sets) {
     if (!x.stream) HIPCHK(hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking));
     if (!x.done) HIPCHK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));

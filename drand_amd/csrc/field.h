@@ -660,27 +660,6 @@ DGI Fp2 fp2_conj(const Fp2& a) { return Fp2{a.c0, fp_neg(a.c1)}; }
 #ifndef DG_FP2_CALL
 #define DG_FP2_CALL 0
 #endif
-// DG_FP2_LAZY=1: every inlined Fp2 product (host builds, fp2_mul_r, fp2_mul_seq / fp2_mul_in) reduces lazily
-// (fp28.h fp28_fp2_mul_d: three digit products, two Montgomery reductions)
-#ifndef DG_FP2_LAZY
-#define DG_FP2_LAZY 0
-#endif
-DGI Fp2 fp2_mul_lazy(const Fp2& a, const Fp2& b) {
-  uint32_t x0[14], x1[14], y0[14], y1[14], r0[14], r1[14];
-  fp28_unpack(a.c0.l, x0);
-  fp28_unpack(a.c1.l, x1);
-  fp28_unpack(b.c0.l, y0);
-  fp28_unpack(b.c1.l, y1);
-  fp28_fp2_mul_d(x0, x1, y0, y1, r0, r1);
-  const uint32_t neg = 0u - (r0[13] >> 31);  // r0 in (-p, 0): add p (mod 2^384)
-  Fp2 r;
-  fp28_pack(r0, r.c0.l);
-  fp28_pack(r1, r.c1.l);
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) r.c0.l[i] = addc32(r.c0.l[i], P_LIMBS[i] & neg, c, &c);
-  return Fp2{fp_reduce_once(r.c0), fp_reduce_once(r.c1)};
-}
 #if DG_FP2_CALL && defined(__HIP_DEVICE_COMPILE__) && DG_FP_CALL == 1
 __device__ __noinline__ Fp2 fp2_mul_r(DG_P12(a), DG_P12(b), DG_P12(c), DG_P12(d));
 __device__ __noinline__ Fp2 fp2_sqr_r(DG_P12(a), DG_P12(b));
@@ -801,8 +780,6 @@ DGH Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
   DG_PIN_FP12(r.c0);
   DG_PIN_FP12(r.c1);
   return r;
-#elif DG_FP2_LAZY && !(defined(__HIP_DEVICE_COMPILE__) && DG_FP_CALL == 1)
-  return fp2_mul_lazy(a, b);
 #else
   Fp t0 = fp_mul(a.c0, b.c0);
   Fp t1 = fp_mul(a.c1, b.c1);
@@ -841,9 +818,6 @@ DGH Fp2 fp2_sqr(const Fp2& a) {
 #if defined(__HIP_DEVICE_COMPILE__) && DG_FP_CALL == 1
 __device__ __noinline__ Fp2 fp2_mul_r(DG_P12(a), DG_P12(b), DG_P12(c), DG_P12(d)) {
   const Fp x0{{DG_L12(a)}}, x1{{DG_L12(b)}}, y0{{DG_L12(c)}}, y1{{DG_L12(d)}};
-#if DG_FP2_LAZY
-  return fp2_mul_lazy(Fp2{x0, x1}, Fp2{y0, y1});
-#endif
   const Fp t0 = fp28_mul(x0, y0);
   const Fp t1 = fp28_mul(x1, y1);
   const Fp t2 = fp28_mul(fp_add(x0, x1), fp_add(y0, y1));
@@ -912,17 +886,6 @@ DGI Fp2 fp2_mul_seq(const Fp2& a, const Fp2& b) {
     return r;
   }
 #endif
-#if DG_FP2_LAZY
-  Fp2 x = a, y = b;
-  DG_PIN_FP(x.c0);
-  DG_PIN_FP(x.c1);
-  DG_PIN_FP(y.c0);
-  DG_PIN_FP(y.c1);
-  Fp2 r = fp2_mul_lazy(x, y);
-  DG_PIN_FP(r.c0);
-  DG_PIN_FP(r.c1);
-  return r;
-#endif
   const Fp t0 = fp_mul_seq(a.c0, b.c0);
   const Fp t1 = fp_mul_seq(a.c1, b.c1);
   const Fp t2 = fp_mul_seq(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
@@ -945,9 +908,6 @@ DGI Fp2 fp2_sqr_seq(const Fp2& a) {
 }
 // and inlined (the products' code at every call site)
 DGI Fp2 fp2_mul_in(const Fp2& a, const Fp2& b) {
-#if DG_FP2_LAZY
-  return fp2_mul_lazy(a, b);
-#endif
   const Fp t0 = fp_mul_inl(a.c0, b.c0);
   const Fp t1 = fp_mul_inl(a.c1, b.c1);
   const Fp t2 = fp_mul_inl(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
@@ -1025,83 +985,7 @@ DGI Fp6 fp6_add(const Fp6& a, const Fp6& b) { return Fp6{fp2_add(a.c0, b.c0), fp
 DGI Fp6 fp6_sub(const Fp6& a, const Fp6& b) { return Fp6{fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
 DGI Fp6 fp6_neg(const Fp6& a) { return Fp6{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
 DGI Fp6 fp6_mul_v(const Fp6& a) { return Fp6{fp2_mul_xi(a.c2), a.c0, a.c1}; }
-// ---- Fp6 products with each Fp2 operand unpacked to digit form once (DG_FP6_DIG, the one-wave pipeline kernels):
-// an operand feeding two or three Fp2 products is converted once, and the Karatsuba sums (a0 + a1 ...) are made
-// digit-wise.  Digits stay below 2^30 (a sum of sums), values below 4p: the SOS column sums stay below 2^64
-// (14 (2^30)^2 + 14 2^56 < 2^63.9) and (4p)^2 < p 2^392 keeps the output below 2p.  Same results as fp6_mul /
-// fp6_mul_01 / fp6_mul_1 (tests/test_host_arith.py::test_fp6_digit_forms_match).
-struct Fp2D {
-  uint32_t c0[14], c1[14];
-};
-DGI Fp2D fp2d_of(const Fp2& a) {
-  Fp2D d;
-  fp28_unpack(a.c0.l, d.c0);
-  fp28_unpack(a.c1.l, d.c1);
-  return d;
-}
-DGI Fp2D fp2d_add(const Fp2D& a, const Fp2D& b) {
-  Fp2D d;
-#pragma unroll
-  for (int i = 0; i < 14; ++i) {
-    d.c0[i] = a.c0[i] + b.c0[i];
-    d.c1[i] = a.c1[i] + b.c1[i];
-  }
-  return d;
-}
-DGI Fp2 fp2d_mul(Fp2D x, Fp2D y) {
-  DG_PIN_D14(x.c0);
-  DG_PIN_D14(y.c0);
-  Fp t0 = fp28_product_packed(x.c0, y.c0);
-  DG_PIN_T12(t0);
-  DG_PIN_D14(x.c1);
-  DG_PIN_D14(y.c1);
-  Fp t1 = fp28_product_packed(x.c1, y.c1);
-  DG_PIN_T12(t1);
-  uint32_t xs[14], ys[14];
-#pragma unroll
-  for (int i = 0; i < 14; ++i) {
-    xs[i] = x.c0[i] + x.c1[i];
-    ys[i] = y.c0[i] + y.c1[i];
-  }
-  DG_PIN_D14(xs);
-  DG_PIN_D14(ys);
-  Fp t2 = fp28_product_packed(xs, ys);
-  DG_PIN_T12(t2);
-  return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
-}
-DGI Fp6 fp6_mul_dig(const Fp6& a, const Fp6& b) {
-  const Fp2D A0 = fp2d_of(a.c0), A1 = fp2d_of(a.c1), A2 = fp2d_of(a.c2);
-  const Fp2D B0 = fp2d_of(b.c0), B1 = fp2d_of(b.c1), B2 = fp2d_of(b.c2);
-  const Fp2 v0 = fp2d_mul(A0, B0), v1 = fp2d_mul(A1, B1), v2 = fp2d_mul(A2, B2);
-  const Fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2d_mul(fp2d_add(A1, A2), fp2d_add(B1, B2)), v1), v2)), v0);
-  const Fp2 c1 = fp2_add(fp2_sub(fp2_sub(fp2d_mul(fp2d_add(A0, A1), fp2d_add(B0, B1)), v0), v1), fp2_mul_xi(v2));
-  const Fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2d_mul(fp2d_add(A0, A2), fp2d_add(B0, B2)), v0), v2), v1);
-  return Fp6{c0, c1, c2};
-}
-DGI Fp6 fp6_mul_01_dig(const Fp6& a, const Fp2& b0, const Fp2& b1) {
-  const Fp2D A0 = fp2d_of(a.c0), A1 = fp2d_of(a.c1), A2 = fp2d_of(a.c2), B0 = fp2d_of(b0), B1 = fp2d_of(b1);
-  const Fp2 v0 = fp2d_mul(A0, B0), v1 = fp2d_mul(A1, B1);
-  const Fp2 c0 = fp2_add(fp2_mul_xi(fp2d_mul(A2, B1)), v0);
-  const Fp2 c1 = fp2_sub(fp2_sub(fp2d_mul(fp2d_add(A0, A1), fp2d_add(B0, B1)), v0), v1);
-  const Fp2 c2 = fp2_add(fp2d_mul(A2, B0), v1);
-  return Fp6{c0, c1, c2};
-}
-DGI Fp6 fp6_mul_1_dig(const Fp6& a, const Fp2& b1) {
-  const Fp2D B1 = fp2d_of(b1);
-  return Fp6{fp2_mul_xi(fp2d_mul(fp2d_of(a.c2), B1)), fp2d_mul(fp2d_of(a.c0), B1), fp2d_mul(fp2d_of(a.c1), B1)};
-}
-#ifndef DG_FP6_DIG
-#define DG_FP6_DIG 0
-#endif
-#if DG_FP6_DIG && DG_FP_CALL == 3 && defined(__HIP_DEVICE_COMPILE__)
-#define DG_FP6_DIG_ON 1
-#else
-#define DG_FP6_DIG_ON 0
-#endif
 DGH Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
-#if DG_FP6_DIG_ON
-  return fp6_mul_dig(a, b);
-#endif
   Fp2 v0 = fp2_mul(a.c0, b.c0);
   Fp2 v1 = fp2_mul(a.c1, b.c1);
   Fp2 v2 = fp2_mul(a.c2, b.c2);
@@ -1134,9 +1018,6 @@ DG12 Fp6 fp6_inv(const Fp6& a) {
 }
 // (a0 + a1 v + a2 v^2) * (b0 + b1 v)
 DGH Fp6 fp6_mul_01(const Fp6& a, const Fp2& b0, const Fp2& b1) {
-#if DG_FP6_DIG_ON
-  return fp6_mul_01_dig(a, b0, b1);
-#endif
   Fp2 v0 = fp2_mul(a.c0, b0);
   Fp2 v1 = fp2_mul(a.c1, b1);
   Fp2 c0 = fp2_add(fp2_mul_xi(fp2_mul(a.c2, b1)), v0);
@@ -1146,9 +1027,6 @@ DGH Fp6 fp6_mul_01(const Fp6& a, const Fp2& b0, const Fp2& b1) {
 }
 // (a0 + a1 v + a2 v^2) * (b1 v)
 DGI Fp6 fp6_mul_1(const Fp6& a, const Fp2& b1) {
-#if DG_FP6_DIG_ON
-  return fp6_mul_1_dig(a, b1);
-#endif
   return Fp6{fp2_mul_xi(fp2_mul(a.c2, b1)), fp2_mul(a.c0, b1), fp2_mul(a.c1, b1)};
 }
 

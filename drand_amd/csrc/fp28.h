@@ -140,57 +140,6 @@ DGI void fp28_sos_sqr_d(const uint32_t (&x)[14], uint32_t (&r)[14]) {
   }
   fp28_sos_reduce(t, r);
 }
-
-// Fp2 product with lazy reduction (Karatsuba): r0 = x0 y0 - x1 y1, r1 = (x0 + x1)(y0 + y1) - x0 y0 - x1 y1, both
-// / 2^392 mod p (x*, y* < p in digit form; bounds below).  The three digit products are summed per column and
-// combined before reduction, so two Montgomery reductions run instead of three (196 of 1176 v_mad_u64_u32 saved).
-// Column k of r1 is the cross product x0 y1 + x1 y0 (non-negative, < 2^61); column k of r0 is signed (|.| < 2^60),
-// so its accumulator carries with arithmetic shifts.  r1 = (V1 + m p) / 2^392 < 2p as in the Fp product.  r0 is
-// (V0 + m p) / 2^392 with V0 = x0 y0 - x1 y1 in (-p^2, p^2): in (-p, 2p), negative (top digit < 0 as int32) when
-// V0 + m p < 0; field.h fp2_mul_lazy adds p back.
-DGI void fp28_tail_s(uint64_t& acc, int k, uint32_t (&m)[14], uint32_t (&r)[14]) {
-#pragma unroll
-  for (int i = 0; i < 14; ++i) {
-    const int j = k - i;
-    if (i < k && j >= 0 && j < 14) acc += (uint64_t)m[i] * P28[j];
-  }
-  if (k < 14) {
-    m[k] = ((uint32_t)acc * P_INV28) & FP28_MASK;
-    acc += (uint64_t)m[k] * P28[0];
-  } else {
-    r[k - 14] = (uint32_t)acc & FP28_MASK;
-  }
-  acc = (uint64_t)((int64_t)acc >> 28);
-}
-DGI void fp28_fp2_mul_d(const uint32_t (&x0)[14], const uint32_t (&x1)[14], const uint32_t (&y0)[14],
-                        const uint32_t (&y1)[14], uint32_t (&r0)[14], uint32_t (&r1)[14]) {
-  uint32_t s[14], u[14], m0[14], m1[14];
-#pragma unroll
-  for (int i = 0; i < 14; ++i) {
-    s[i] = x0[i] + x1[i];
-    u[i] = y0[i] + y1[i];
-  }
-  uint64_t acc0 = 0, acc1 = 0;
-#pragma unroll
-  for (int k = 0; k < 27; ++k) {
-    uint64_t p0 = 0, p1 = 0, p2 = 0;
-#pragma unroll
-    for (int i = 0; i < 14; ++i) {
-      const int j = k - i;
-      if (j >= 0 && j < 14) {
-        p0 += (uint64_t)x0[i] * y0[j];
-        p1 += (uint64_t)x1[i] * y1[j];
-        p2 += (uint64_t)s[i] * u[j];
-      }
-    }
-    acc0 += p0 - p1;
-    acc1 += p2 - p0 - p1;
-    fp28_tail_s(acc0, k, m0, r0);
-    fp28_mont_tail(acc1, k, m1, r1);
-  }
-  r0[13] = (uint32_t)acc0;
-  r1[13] = (uint32_t)acc1;
-}
 // r = a b / 2^392 mod p, r < 2p (a, b < p)
 DGI void fp28_mont_mul(const uint32_t (&a)[12], const uint32_t (&b)[12], uint32_t (&out)[12]) {
   uint32_t x[14], y[14], r[14];

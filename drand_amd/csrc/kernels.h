@@ -142,33 +142,6 @@ DG_KERNEL void __launch_bounds__(128) k_hash_to_g2(uint32_t n, const uint8_t* ms
 }
 #endif
 
-// hash-to-curve without cofactor clearing (RLC path); 32 B messages take the word-wise expand_message_xmd
-#if DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_h2c_uncleared(uint32_t n, const uint8_t* msgs, uint32_t msg_len,
-                                                      const uint8_t* dst, uint32_t dst_len, const XmdTail* xmd,
-                                                      G2JStore* outQ) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  Fp2 u[2];
-  if (msg_len == 32 && xmd)
-    hash_to_field_xmd32(u, msgs + 32ull * i, xmd);
-  else
-    hash_to_field_fp2x2(u, msgs + (size_t)msg_len * i, msg_len, dst, dst_len);
-  G2J q[2];
-  for (int h = 0; h < 2; ++h) {
-    Fp2 x, y;
-    sswu_g2(x, y, u[h], fp_zero(), false);
-    q[h] = iso_map_g2(x, y);
-  }
-  // normalised to Z = 1 (one safegcd inversion): the MSM and the scalar multiplications downstream
-  // then use mixed additions
-  store_g2j(outQ[i], jac_from_aff(g2_to_aff(jac_add(q[0], q[1]))));
-}
-#else
-DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_h2c_uncleared(uint32_t n, const uint8_t* msgs, uint32_t msg_len,
-                                                      const uint8_t* dst, uint32_t dst_len, const XmdTail* xmd,
-                                                      G2JStore* outQ);
-#endif
 
 
 // G1 decode (keys, commits), with subgroup check
@@ -232,40 +205,6 @@ DG_KERNEL void __launch_bounds__(64) k_pubpoly_eval(uint32_t n, uint32_t t, cons
 }
 #endif
 
-// decode sigma of every item (96 B at sigs + stride*i + offset), with the G2 subgroup check unless the
-// batch checks subgroup membership on the MSM window sums (`subgroup` == 0, msm.h); claim the item's
-// (round, slot) cell -- a taken cell sends the item to the individual check (`isolate`)
-#if DG_TU_HOT
-DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_decode_items(uint32_t n, uint32_t k, uint32_t nslots, const uint8_t* sigs,
-                                                     uint32_t stride, uint32_t offset, const uint32_t* item_slot,
-                                                     const uint8_t* key_status, G2AStore* S, uint8_t* status,
-                                                     uint32_t* cell, uint8_t* isolate, uint32_t subgroup) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t slot = item_slot ? item_slot[i] : 0u;
-  isolate[i] = 0;
-  if (key_status[slot] != DG_ST_OK_) {
-    store_g2a(S[i], G2A{fp2_zero(), fp2_zero(), true});
-    status[i] = DG_ST_PK_DECODE_;
-    return;
-  }
-  G2A a;
-  bool ok = g2_decompress(a, sigs + (size_t)stride * i + offset, subgroup != 0);
-  if (!ok) a = G2A{fp2_zero(), fp2_zero(), true};
-  store_g2a(S[i], a);
-  status[i] = ok ? DG_ST_OK_ : DG_ST_SIG_DECODE_;
-  if (ok) {
-    // a key outside the batch equation (a rare index, drand_gpu.hip verify_partials_dev) is checked alone
-    uint32_t old = slot < nslots ? atomicExch(&cell[(size_t)(i / k) * nslots + slot], 1u) : 1u;
-    isolate[i] = old ? 1 : 0;
-  }
-}
-#else
-DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_decode_items(uint32_t n, uint32_t k, uint32_t nslots, const uint8_t* sigs,
-                                                     uint32_t stride, uint32_t offset, const uint32_t* item_slot,
-                                                     const uint8_t* key_status, G2AStore* S, uint8_t* status,
-                                                     uint32_t* cell, uint8_t* isolate, uint32_t subgroup);
-#endif
 
 // U_i = beta_slot S_i for batch items, O otherwise
 #if DG_TU_LIB

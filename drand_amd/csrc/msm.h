@@ -399,7 +399,7 @@ DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_sum_rows(uint32_t rows, ui
 
 // the bucket sums from the affine chunk sums: lane (side, b, q < bsplit) adds chunks q, q + bsplit, ... of bucket b
 // (A[offset[b] + c 2^L]) with mixed additions, the running sum in LDS (g2_madd_lds); the bsplit partials
-// BP[sb * bsplit + q] are then row-summed (bsplit <= MSM_BSPLIT, a power of two: DG_MSM_BSPLIT)
+// BP[sb * bsplit + q] are then row-summed (bsplit <= MSM_BSPLIT, a power of two)
 #if defined(__HIP__) && DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_msm_buckets_aff(uint32_t nsides, uint32_t nbk, uint32_t bsplit,
                                                                       const uint32_t* count, const uint32_t* offset,
@@ -505,16 +505,9 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_final_coop(uint32_t n
   CO_SERIAL(store_g2j(out[side], G2J{acc.x, acc.y, acc.z}));
 }
 
-// batched subgroup check: one 128-lane workgroup per window sum W[w] (the first side's, or every key
-// set's in the keyed MSM) tests psi(P) == [z]P cooperatively (coop.h); any failure sets *fail, which
-// k_final_coop folds into the batch verdict, so the per-item pass runs.  The verify path runs these
-// workgroups inside the Miller launch (k_pair_miller_coop), beside the pairs; this standalone form is the
-// DG_SUB_SEPARATE=1 A/B.
-DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_subgroup(const G2JStore* W, uint32_t* fail) {
-  __shared__ CoG2Tmp tmp;
-  __shared__ CoG2 p, zp, pp;
-  co_subgroup_check(W + blockIdx.x, &p, &zp, &pp, &tmp, fail);
-}
+// (the batched subgroup check -- one 128-lane workgroup per window sum W[w] testing psi(P) == [z]P cooperatively,
+// coop.h co_subgroup_check -- runs as extra workgroups of the Miller launch, k_pair_miller_coop; a failure sets the
+// batch's flag[2], which k_final_coop folds into its verdict, so the isolation pass runs)
 
 // ---------------------------------------------------------------------------------------------------
 // Keyed MSM for the multi-key batch (VerifyPartial / Recover): T_s = sum over the batch items i of key

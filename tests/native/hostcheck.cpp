@@ -323,37 +323,6 @@ extern "C" int hc_fp2_mul_dig_check(uint64_t seed, uint32_t n) {
   return 1;
 }
 
-// field.h's Fp6 digit forms (DG_FP6_DIG) against fp6_mul / fp6_mul_01 / fp6_mul_1 on n pseudo-random operands (values
-// below p, including p - 1 limbs); 1 if all equal
-static bool fp6_same(const Fp6& x, const Fp6& y) { return fp2_eq(x.c0, y.c0) && fp2_eq(x.c1, y.c1) && fp2_eq(x.c2, y.c2); }
-extern "C" int hc_fp6_dig_check(uint64_t seed, uint32_t n) {
-  uint64_t s = seed | 1;
-  auto rnd = [&]() {
-    Fp a;
-    for (int i = 0; i < 12; ++i) {
-      s ^= s << 13;
-      s ^= s >> 7;
-      s ^= s << 17;
-      a.l[i] = (uint32_t)s;
-    }
-    a.l[11] &= 0x0fffffffu;
-    if ((s & 7) == 0) {  // the largest element, p - 1
-      a = fp_const(P_LIMBS);
-      a.l[0] -= 1;
-    }
-    return a;
-  };
-  auto r2 = [&]() { return Fp2{rnd(), rnd()}; };
-  for (uint32_t k = 0; k < n; ++k) {
-    const Fp6 a{r2(), r2(), r2()}, b{r2(), r2(), r2()};
-    const Fp2 b0 = r2(), b1 = r2();
-    if (!fp6_same(fp6_mul_dig(a, b), fp6_mul(a, b))) return 0;
-    if (!fp6_same(fp6_mul_01_dig(a, b0, b1), fp6_mul_01(a, b0, b1))) return 0;
-    if (!fp6_same(fp6_mul_1_dig(a, b1), fp6_mul_1(a, b1))) return 0;
-  }
-  return 1;
-}
-
 // [k]P with the accumulator as a memory slot (curve.h g2_mul_u256_psi_lds, LDS on the device) against the
 // register form; 1 if equal
 extern "C" int hc_g2_mul_lds_check(const uint8_t* sig96, const uint32_t* k8) {
@@ -495,46 +464,6 @@ extern "C" int hc_recover_sac_check(const uint8_t* sigs96, const uint32_t* idx, 
   return jac_eq(sum, want) ? 1 : 0;
 }
 
-
-// fp2_mul_lazy (the DG_FP2_LAZY A/B form: three digit products, two reductions) against the three-reduction
-// Karatsuba product, on n pseudo-random operand pairs below p plus the edge values 0, 1 and p - 1.  Returns the
-// number of mismatches.
-extern "C" int hc_fp2_mul_lazy_check(uint64_t seed, uint32_t n) {
-  uint64_t s = seed | 1;
-  auto next = [&s]() {
-    s ^= s << 13;
-    s ^= s >> 7;
-    s ^= s << 17;
-    return s;
-  };
-  Fp pm1 = fp_const(P_LIMBS);
-  uint32_t br = 0;
-  pm1.l[0] = subb32(pm1.l[0], 1, 0, &br);
-  const Fp edge[3] = {fp_zero(), fp_one(), pm1};
-  int bad = 0;
-  for (uint32_t it = 0; it < n; ++it) {
-    Fp v[4];
-    for (int k = 0; k < 4; ++k) {
-      if (it < 81) {
-        v[k] = edge[(it / (k == 0 ? 1 : k == 1 ? 3 : k == 2 ? 9 : 27)) % 3];
-        continue;
-      }
-      for (int i = 0; i < 12; i += 2) {
-        const uint64_t w = next();
-        v[k].l[i] = (uint32_t)w;
-        v[k].l[i + 1] = (uint32_t)(w >> 32);
-      }
-      v[k].l[11] &= 0x1fffffffu;
-      v[k] = fp_reduce_once(fp_reduce_once(fp_reduce_once(v[k])));
-    }
-    const Fp2 a{v[0], v[1]}, b{v[2], v[3]};
-    const Fp t0 = fp28_mul(a.c0, b.c0), t1 = fp28_mul(a.c1, b.c1);
-    const Fp t2 = fp28_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
-    const Fp2 ref{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
-    bad += !fp2_eq(ref, fp2_mul_lazy(a, b));
-  }
-  return bad;
-}
 
 // cyc_exp_z (Karabina compressed squarings, batched decompression) against the Granger-Scott square-and-multiply
 // chain, on n cyclotomic elements f^((p^6 - 1)(p^2 + 1)) of pseudo-random f, plus the element 1 (every

@@ -49,3 +49,22 @@ def test_pinned_chain_files_match(n):
     if not os.path.exists(p):
         pytest.skip("data/chain_v1_%d.bin not generated in this checkout" % n)
     assert S.find_chain(n) == (n, p)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_every_rank_runs_the_one_batch_step(world):
+    """BASELINE configs[3] at N = world (the 1M chain split N ways; configs[1] at N = 1): every rank's range is one
+    device batch, and its verdicts are packed and all-gathered on the batch's own stream (bench.py
+    consume_on_batch_stream: no side-stream wait) -- the N = 1 arrangement on every rank at world 2, 4, 8."""
+    from drand_amd import shard
+
+    G = 100000 if world == 1 else 1000000
+    for rank in range(world):
+        a, b = shard.round_range(G, world, rank)
+        bounds = bench.batch_bounds(b - a)
+        assert bounds == [(0, b - a)], (world, rank)
+        assert bench.consume_on_batch_stream(len(bounds))
+    # an explicit smaller --batch, or the blocking entry point, takes the side stream
+    assert len(bench.batch_bounds(125000, 50000)) == 3 and not bench.consume_on_batch_stream(3)
+    assert not bench.consume_on_batch_stream(1, use_sync=True)
+    assert bench.batch_bounds(1000000) == [(0, 500000), (500000, 1000000)]

@@ -356,10 +356,10 @@ print(json.dumps(tbls.verify_recovered_batch(hx(c["pk"]), msgs[:48], s, seed=5).
 
 
 def test_ab_switches_give_the_same_verdicts():
-    """The library's A/B switches (DG_MSM_JAC: Jacobian chunk sums instead of the affine MSM levels,
-    DG_BINV_CHUNKED: the chunk-of-32 batch inversion, DG_SUB_SEPARATE: the subgroup windows in their own
-    launch) select other kernels for the same computation: in a child process with all three set, the verdicts
-    of a corrupted batch equal the default library's and the CPU twin's."""
+    """The library's remaining run-time switches reshape the same computation: in a child process with one
+    workspace set (DG_SETS=1) and level-1 isolation groups of 2 quads (DG_XR_QPG=2), the verdicts of a corrupted
+    batch equal the default library's and the CPU twin's.  (The round-2/3 A/B switches DG_MSM_JAC,
+    DG_BINV_CHUNKED, DG_SUB_SEPARATE were removed with their code paths in round 5.)"""
     import json
     import subprocess
     import sys
@@ -374,7 +374,7 @@ def test_ab_switches_give_the_same_verdicts():
     here = tbls.verify_recovered_batch(pk, msgs[:48], s, seed=5).tolist()
     want = [twin.verify(pk, bytes(msgs[i]), bytes(s[i])) for i in range(48)]
     assert here == want and sum(1 for v in want if v) == 3
-    env = dict(os.environ, DG_MSM_JAC="1", DG_BINV_CHUNKED="1", DG_SUB_SEPARATE="1")
+    env = dict(os.environ, DG_SETS="1", DG_XR_QPG="2")
     r = subprocess.run([sys.executable, "-c", _AB_CHILD, ROOT], env=env, capture_output=True, text=True, timeout=240,
                        cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]

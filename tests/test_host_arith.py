@@ -253,12 +253,6 @@ def test_fp2_mul_digit_form_matches(hc):
     assert hc.hc_fp2_mul_dig_check(ctypes.c_uint64(12345), 3000) == 1
 
 
-def test_fp6_digit_forms_match(hc):
-    """field.h's Fp6 products with each Fp2 operand unpacked once (DG_FP6_DIG: dense, 01-sparse and 1-sparse) equal
-    fp6_mul / fp6_mul_01 / fp6_mul_1 on random operands below p, p - 1 limbs included."""
-    assert hc.hc_fp6_dig_check(ctypes.c_uint64(777), 1500) == 1
-
-
 def test_wnaf_digits_host_build(hc):
     """recover.h rc_wnaf: width-5 signed digits (odd, |d| <= 15, >= 5 apart) that evaluate back to the scalar,
     including the 65th position a carry can reach."""
@@ -299,14 +293,6 @@ def test_recover_sac_host_build(hc, t, seed):
     idx = list(range(t)) if seed < 0 else sorted(rng.sample(range(256), t))
     assert hc.hc_recover_sac_check(b"".join(sigs), (ctypes.c_uint32 * t)(*idx), t) == 1
 
-
-
-def test_fp2_lazy_product_matches_karatsuba(hc):
-    """DG_FP2_LAZY's product (fp28.h fp28_fp2_mul_d: signed column sums, two reductions, the negative c0 case
-    fixed up by + p) equals the three-reduction Karatsuba product, including all 81 combinations of 0, 1, p - 1."""
-    hc.hc_fp2_mul_lazy_check.restype = ctypes.c_int
-    hc.hc_fp2_mul_lazy_check.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
-    assert hc.hc_fp2_mul_lazy_check(0x9E3779B97F4A7C15, 20000) == 0
 
 
 def test_karabina_exponentiation_matches_granger_scott(hc):
