@@ -150,6 +150,21 @@ DGI Fp12 ck_miller(uint32_t np, const Fp& ax, const Fp& ay, Line line) {
   return fp12_conj(f);
 }
 
+// the Miller value of ONE pair of a check (pair 0: (a, H) at P = (px, py); pair 1: (-g1, b)), its own squarings included:
+// the two pairs' values multiply to ck_miller's (squaring is multiplicative), conjugated.  Two lanes per check halve the
+// lane's chain where the checks of a launch are too few to fill the chip (the cross-round isolation, xr.h).
+template <class Line>
+DGI Fp12 ck_miller1(const Fp& px, const Fp& py, Line line) {
+  Fp12 f = fp12_one();
+#pragma unroll 1
+  for (uint32_t s = 0; s < CK_STEPS; ++s) {
+    if (s != 0 && ck_step_is_dbl(s)) f = fp12_sqr(f);
+    const CkLine l = line(s);
+    f = fp12_mul_014(f, l.c0, fp2_mul_fp(l.c1, px), fp2_mul_fp(l.c4, py));
+  }
+  return fp12_conj(f);
+}
+
 // ---- final exponentiation in pieces (pairing.h final_exp_cubed)
 // f^-1 = (f0 t6^-1, -f1 t6^-1) with t6 = f0^2 - v f1^2 (field.h fp12_inv); t6^-1 by fp6_inv, whose one inversion
 // (of the Fp2 value t) becomes an inversion of N(t) in Fp, batched across the checks
@@ -320,6 +335,7 @@ static_assert(CK_GRP == GRP, "one group per check");
 // (kernels_check_a.hip)
 #if DG_TU_CHECK == 1
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_round_lines(uint32_t R, const G2JStore* Q, CkLine* rl, uint8_t* hinf) {
+  DG_HI();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   const G2A h = g2_to_aff(g2_clear_cofactor(load_g2j(Q[r])));
@@ -333,6 +349,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_round_lines(uint32_t R, c
 // subgroup-checked by its group.
 DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_ck_sub(uint32_t G, uint32_t off, const uint32_t* glist,
                                                                 const G2AStore* S, uint8_t* status, uint8_t* fin) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   __shared__ G2JStore s_acc[64];
   if (g >= 4 * G) return;
@@ -387,11 +404,13 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_prep(uint32_t G, uint32_
                                                   const uint8_t* hinf, const G2AStore* S, uint8_t* status, uint8_t* fin,
                                                   uint32_t subgroup, unsigned long long* cnt, CkState* st,
                                                   uint8_t* g2m, RsDigits* dig) {
+  DG_HI();
   ck_prep(G, off, glist, k, seedp, keys, item_slot, hinf, S, status, fin, subgroup, cnt, st, g2m, dig);
 }
 // the lines of the pair (-g1, b): l2[s * G + g]
 DG_KERNEL void __launch_bounds__(64, DG_CK_L2_WAVES) k_ck_lines2(uint32_t G, const uint32_t* gcnt, const CkState* st,
                                                                  CkLine* l2) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (ck_dead(g, G, gcnt) || !(st[g].np & 2)) return;
   const G2A b = load_g2a(st[g].b);
@@ -402,6 +421,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_L2_WAVES) k_ck_lines2(uint32_t G, con
 // checks, whose verdict k_ck_final ignores -- skips the chain: 1^z = 1, zero[g] = 2)
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const uint32_t* gcnt, const Fp12* X, CycC* sn,
                                                               Fp* nv, uint8_t* zero, uint32_t* zl) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (ck_dead(g, G, gcnt)) return;
   const Fp12 x = X[g];
@@ -421,6 +441,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const 
 // a single check is kyber's bls.Verify verdict
 DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const uint8_t* good_, uint8_t* status,
                                                    uint8_t* fin) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   const CkState& c = st[g];
@@ -457,28 +478,31 @@ DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st
 // the easy part of the final exponentiation: F2[g] = f1 frob^2(f1), f1 = f^-1 conj(f); f^-1 by ck_fe1 / ck_inv with the
 // one Fp inversion of the check in the lane (field.h fp_inv, safegcd) -- no batch inversion across the checks.  Lane 0
 // also empties the CK_NEXP work lists of k_ck_explain (zl + z (G + 1), z < CK_NEXP).
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_easy(uint32_t G, const uint32_t* gcnt, const Fp12* F, Fp12* F2,
-                                                            uint32_t* zl) {
+// (two != 0: F holds the two pairs' values of k_ck_miller2, F[g] and F[G + g]; f is their product)
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_easy(uint32_t G, const uint32_t* gcnt, uint32_t two, const Fp12* F,
+                                                            Fp12* F2, uint32_t* zl) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g == 0 && G)
 #pragma unroll 1
     for (uint32_t z = 0; z < CK_NEXP; ++z) zl[(size_t)z * (G + 1)] = 0;
   if (ck_dead(g, G, gcnt)) return;
-  const Fp12 f = F[g];
+  const Fp12 f = two ? fp12_mul(F[g], F[(size_t)G + g]) : F[g];
   CkInv c;
   const Fp n = ck_fe1(f, c);
   const Fp12 f1 = ck_mul_op(ck_inv(f, c, fp_inv(n)), f, 0, 1);
   F2[g] = ck_mul_op(f1, f1, 2, 0);
 }
 #else
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_easy(uint32_t G, const uint32_t* gcnt, const Fp12* F, Fp12* F2,
-                                                            uint32_t* zl);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_easy(uint32_t G, const uint32_t* gcnt, uint32_t two, const Fp12* F,
+                                                            Fp12* F2, uint32_t* zl);
 #endif
 // the Miller value of every check (kernels_check_b.hip)
 #if DG_TU_CHECK == 2
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, const uint32_t* gcnt, uint32_t R,
                                                               const CkState* st, const CkLine* rl, const CkLine* l2,
                                                               Fp12* F) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (ck_dead(g, G, gcnt)) return;
   const uint32_t np = st[g].np, r = st[g].round;
@@ -487,16 +511,38 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, const 
     return pair ? l2[(size_t)s * G + g] : rl[(size_t)s * R + r];
   });
 }
+// two lanes per check (lanes [0, Gp) pair 0, [Gp, 2 Gp) pair 1, Gp = G rounded up to whole waves): F[pair G + g]
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller2(uint32_t G, const uint32_t* gcnt, uint32_t R,
+                                                               const CkState* st, const CkLine* rl, const CkLine* l2,
+                                                               Fp12* F) {
+  DG_HI();
+  const uint32_t Gp = (G + 63) & ~63u, lane = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t pair = lane >= Gp ? 1u : 0u, g = lane - pair * Gp;
+  if (ck_dead(g, G, gcnt)) return;
+  const uint32_t np = st[g].np, r = st[g].round;
+  Fp12 f = fp12_one();
+  if ((np >> pair) & 1) {
+    if (pair)
+      f = ck_miller1(fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), [&](uint32_t s) { return l2[(size_t)s * G + g]; });
+    else
+      f = ck_miller1(st[g].a.x, st[g].a.y, [&](uint32_t s) { return rl[(size_t)s * R + r]; });
+  }
+  F[(size_t)pair * G + g] = f;
+}
 #else
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, const uint32_t* gcnt, uint32_t R,
                                                               const CkState* st, const CkLine* rl, const CkLine* l2,
                                                               Fp12* F);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller2(uint32_t G, const uint32_t* gcnt, uint32_t R,
+                                                               const CkState* st, const CkLine* rl, const CkLine* l2,
+                                                               Fp12* F);
 #endif
 // the end of final_exp_cubed and the check's verdict (kernels_check_c.hip): T = (a^z)^z frob^2(a) (k_ck_expdec's
 // product), b = T conj(a), c = f2^3, good[g] = (no pair, or b c == 1)
 #if DG_TU_CHECK == 3
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_final(uint32_t G, const uint32_t* gcnt, const CkState* st,
                                                              const Fp12* T, const Fp12* A, const Fp12* F2, uint8_t* good) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (ck_dead(g, G, gcnt)) return;
   const Fp12 c = ck_mul_op(ck_mul_op(F2[g], F2[g], 0, 0), F2[g], 0, 0);
@@ -514,6 +560,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_final(uint32_t G, const u
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expdec(uint32_t G, const uint32_t* gcnt, const CycC* sn, Fp* nv,
                                                               const uint8_t* zero, const Fp12* Y, uint32_t nfrob,
                                                               uint32_t conj, Fp12* out) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (ck_dead(g, G, gcnt) || zero[g] == 1) return;
   Fp12 x = fp12_one();  // x = 1 (zero[g] == 2, k_ck_expsq)
@@ -552,6 +599,7 @@ DGI void ck_tab_put(uint4* T4, uint8_t* tinf, uint32_t G, uint32_t g, uint32_t u
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_tab_den(uint32_t l, uint32_t G, const CkState* st,
                                                                const uint8_t* g2m, const G2AStore* S, uint4* T4,
                                                                uint8_t* tinf, Fp* den) {
+  DG_HI();
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= 3 * G) return;
   const uint32_t g = lane % G, e = lane / G;
@@ -567,6 +615,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_tab_den(uint32_t l, uint
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_tab_add(uint32_t l, uint32_t G, const CkState* st,
                                                                const uint8_t* g2m, const G2AStore* S, uint4* T4,
                                                                uint8_t* tinf, const Fp* dinv) {
+  DG_HI();
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= 3 * G) return;
   const uint32_t g = lane % G, e = lane / G;
@@ -579,6 +628,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_tab_add(uint32_t l, uint
 // the column loop: bj[g] = b (Jacobian), bn[g] = N(Z) (1 for the lanes not on this path)
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_sac(uint32_t G, const uint8_t* g2m, const RsDigits* dig,
                                                            const uint4* T4, const uint8_t* tinf, G2JStore* bj, Fp* bn) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   __shared__ G2JStore s_acc[64];
   if (g >= G) return;
@@ -594,6 +644,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_sac(uint32_t G, const ui
 // st[g].b = the affine b, and np
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_bfin(uint32_t G, const uint8_t* g2m, const G2JStore* bj,
                                                             const Fp* bni, const uint8_t* hinf, CkState* st) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G || !g2m[g]) return;
   const G2A b = ck_g2_affine(load_g2j(bj[g]), bni[g]);
@@ -603,6 +654,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_bfin(uint32_t G, const u
 }
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_explain(const uint32_t* zl, const Fp12* X, const Fp12* Y,
                                                                uint32_t nfrob, uint32_t conj, Fp12* out) {
+  DG_HI();
   const uint32_t n = zl[0];
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
     const uint32_t g = zl[1 + j];

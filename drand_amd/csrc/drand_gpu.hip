@@ -1002,7 +1002,7 @@ struct CkBufs {
 int ck_bufs(CkBufs& b, size_t G, bool group_sums) {
   RET(wsT(S_CK_ST, G, &b.st));
   RET(wsT(S_CK_L2, (size_t)CK_STEPS * G, &b.l2));
-  RET(wsT(S_CK_F, G, &b.F));
+  RET(wsT(S_CK_F, 2 * G, &b.F));  // (two pairs' values per check for k_ck_miller2)
   RET(wsT(S_CK_F2, G, &b.F2));
   RET(wsT(S_CK_T0, G, &b.T0));
   RET(wsT(S_CK_T1, G, &b.T1));
@@ -1037,10 +1037,19 @@ int ck_expz(uint32_t z, uint32_t G, const uint32_t* gcnt, const Fp12* X, const F
 // The checks b.st[0..G) (pair 0: (a, the lines rl[s R + round]), pair 1: (-g1, b)) -> b.good: the (-g1, b) lines, the
 // Miller values, the final exponentiation (k_ck_easy, five x^z with their next factors, k_ck_final).  Every kernel is
 // one lane per check without exchange, so gcnt (device, may be null) gates the lanes of a launch sized for G.
-int run_checks(uint32_t G, const uint32_t* gcnt, uint32_t R, const CkLine* rl, const CkBufs& b, hipStream_t st) {
-  RET(launch("k_ck_lines2", k_ck_lines2, G, 64, st, G, gcnt, (const CkState*)b.st, b.l2));
-  RET(launch("k_ck_miller", k_ck_miller, G, 64, st, G, gcnt, R, (const CkState*)b.st, rl, (const CkLine*)b.l2, b.F));
-  RET(launch("k_ck_easy", k_ck_easy, G, 64, st, G, gcnt, (const Fp12*)b.F, b.F2, b.zl));
+// latency (the cross-round isolation: few checks per launch): the lines are already in l2 (xr.h k_xg_lines) and each
+// check's two Miller pairs run in lanes of their own (k_ck_miller2)
+int run_checks(uint32_t G, const uint32_t* gcnt, uint32_t R, const CkLine* rl, const CkBufs& b, hipStream_t st,
+               bool latency = false) {
+  const uint32_t Gp = (G + 63) & ~63u;
+  if (latency) {
+    RET(launch("k_ck_miller2", k_ck_miller2, 2 * Gp, 64, st, G, gcnt, R, (const CkState*)b.st, rl, (const CkLine*)b.l2,
+               b.F));
+  } else {
+    RET(launch("k_ck_lines2", k_ck_lines2, G, 64, st, G, gcnt, (const CkState*)b.st, b.l2));
+    RET(launch("k_ck_miller", k_ck_miller, G, 64, st, G, gcnt, R, (const CkState*)b.st, rl, (const CkLine*)b.l2, b.F));
+  }
+  RET(launch("k_ck_easy", k_ck_easy, G, 64, st, G, gcnt, latency ? 1u : 0u, (const Fp12*)b.F, b.F2, b.zl));
   // hard part (final_exp_cubed): t0 = f2^z conj(f2), t1 = t0^z conj(t0), a = t1^z frob(t1),
   // b = (a^z)^z frob^2(a) conj(a), c = f2^3, result b c
   RET(ck_expz(0, G, gcnt, b.F2, b.F2, 0, 1, b.T0, b, st));
@@ -1085,9 +1094,14 @@ uint32_t xr_qpg() {
   static const uint32_t v = (uint32_t)std::max(1, std::min(64, env_int("DG_XR_QPG", (int)XR_QPG)));
   return v;
 }
+// DG_XR_SKIP=1: a failed level-1 group lists its rounds for the single checks directly (two levels)
+uint32_t xr_skip() {
+  static const uint32_t v = env_int("DG_XR_SKIP", (int)XR_SKIP) ? 1u : 0u;
+  return v;
+}
 int xr_isolate(uint32_t i0, uint32_t n, const uint32_t* flag, const uint64_t* seed, const G1AStore* keys,
                const G2JStore* Q, const G2AStore* S, uint8_t* status, hipStream_t st) {
-  const uint32_t qpg = xr_qpg(), nqmax = (n + 3) / 4, G1 = (nqmax + qpg - 1) / qpg;
+  const uint32_t qpg = xr_qpg(), skip = qpg > 1 ? xr_skip() : 0u, nqmax = (n + 3) / 4, G1 = (nqmax + qpg - 1) / qpg;
   uint32_t *cnt, *cand, *l2, *l3;
   G2JStore *QS, *HS;
   uint4* T4;
@@ -1109,13 +1123,14 @@ int xr_isolate(uint32_t i0, uint32_t n, const uint32_t* flag, const uint64_t* se
   RET(launch("k_xq_sum", k_xq_sum, 2 * nqmax, 64, st, nqmax, qpg, seed, cnt, (const uint32_t*)cand, Q, S, T4, tinf, l2,
              QS));
   for (uint32_t level = qpg > 1 ? 1u : 2u; level <= 3; ++level) {
-    const uint32_t G = level == 1 ? G1 : level == 2 ? nqmax : n;
+    if (level == 2 && skip) continue;
+    const uint32_t G = level == 1 ? G1 : level == 2 ? nqmax : n, Gp = (G + 63) & ~63u;
     const uint32_t* gcnt = cnt + level;
     RET(launch("k_xg_prep", k_xg_prep, G, 64, st, level, G, (const uint32_t*)cnt, qpg, (const uint32_t*)l2,
                (const uint32_t*)l3, (const G2JStore*)QS, Q, S, keys, b.st, HS));
-    RET(launch("k_xg_hlines", k_xg_hlines, G, 64, st, G, gcnt, (const G2JStore*)HS, rl, b.st));
-    RET(run_checks(G, gcnt, G, rl, b, st));
-    RET(launch("k_xg_verdict", k_xg_verdict, G, 128, st, level, G, qpg, cnt, (const uint8_t*)b.good,
+    RET(launch("k_xg_lines", k_xg_lines, 2 * Gp, 64, st, G, gcnt, (const G2JStore*)HS, rl, b.st, b.l2));
+    RET(run_checks(G, gcnt, G, rl, b, st, true));
+    RET(launch("k_xg_verdict", k_xg_verdict, G, 128, st, level, G, qpg, skip, cnt, (const uint8_t*)b.good,
                (const uint32_t*)cand, l2, l3, status, g_ctx.xrcount));
   }
   return 0;
@@ -1447,7 +1462,9 @@ int dg_init(int device) {
         {(const void*)k_ck_round_lines, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_round_lines, g1, b64, 0, q, 0u, (const G2JStore*)nullptr, (CkLine*)nullptr, (uint8_t*)nullptr); }},
         {(const void*)k_ck_lines2, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_lines2, g1, b64, 0, q, 0u, cz, (const CkState*)nullptr, (CkLine*)nullptr); }},
         {(const void*)k_ck_miller, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_miller, g1, b64, 0, q, 0u, cz, 0u, (const CkState*)nullptr, (const CkLine*)nullptr, (const CkLine*)nullptr, (Fp12*)nullptr); }},
-        {(const void*)k_ck_easy, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_easy, g1, b64, 0, q, 0u, cz, (const Fp12*)nullptr, (Fp12*)nullptr, (uint32_t*)nullptr); }},
+        {(const void*)k_ck_easy, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_easy, g1, b64, 0, q, 0u, cz, 0u, (const Fp12*)nullptr, (Fp12*)nullptr, (uint32_t*)nullptr); }},
+        {(const void*)k_ck_miller2, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_miller2, g1, b64, 0, q, 0u, cz, 0u, (const CkState*)nullptr, (const CkLine*)nullptr, (const CkLine*)nullptr, (Fp12*)nullptr); }},
+        {(const void*)k_xg_lines, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_lines, g1, b64, 0, q, 0u, cz, (const G2JStore*)nullptr, (CkLine*)nullptr, (CkState*)nullptr, (CkLine*)nullptr); }},
         {(const void*)k_ck_expsq, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_expsq, g1, b64, 0, q, 0u, cz, (const Fp12*)nullptr, (CycC*)nullptr, (Fp*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr); }},
         {(const void*)k_ck_expdec, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_expdec, g1, b64, 0, q, 0u, cz, (const CycC*)nullptr, (Fp*)nullptr, (const uint8_t*)nullptr, (const Fp12*)nullptr, 0u, 0u, (Fp12*)nullptr); }},
         {(const void*)k_ck_explain, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_explain, g1, b64, 0, q, cz, (const Fp12*)nullptr, (const Fp12*)nullptr, 0u, 0u, (Fp12*)nullptr); }},

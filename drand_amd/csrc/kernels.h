@@ -88,6 +88,17 @@ DGI uint64_t rlc_coeff(uint64_t seed, uint64_t i) {
 
 #if defined(__HIP__)
 #define DG_KERNEL extern "C" __global__
+// Latency-bound kernels (a few waves on a chip shared with other batches: the cooperative tail, the check pipeline of
+// the isolation passes) raise their waves' issue priority, so the throughput waves on the same SIMDs fill the gaps
+// instead of stretching the latency-bound chain (DG_PRIO=0: equal priority, A/B)
+#ifndef DG_PRIO
+#define DG_PRIO 1
+#endif
+#if DG_PRIO && defined(__HIP_DEVICE_COMPILE__)
+#define DG_HI() __builtin_amdgcn_s_setprio(3)
+#else
+#define DG_HI() ((void)0)
+#endif
 
 // A1: beacon messages
 #if DG_TU_LIB
@@ -338,6 +349,7 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_pair_miller_coop(uint32_t
                                                          const G2JStore* K, const G2JStore* T, const G1AStore* Xc,
                                                          const G2JStore* Kc, Fp12* f, uint32_t npairs,
                                                          const G2JStore* win, uint32_t* sub_fail) {
+  DG_HI();
   const uint64_t seed = *seedp;
   __shared__ CoGT gt;
   __shared__ CoML ml;
@@ -398,6 +410,7 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_pair_miller_coop(uint32_t
 // ok = (product of the Miller values, final-exponentiated, is 1) and no subgroup failure (*sub_fail == 0)
 DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_final_coop(uint32_t npairs, const Fp12* f, uint32_t* ok,
                                                                   const uint32_t* sub_fail) {
+  DG_HI();
   __shared__ CoGT gt;
   __shared__ Fp12W F, G, S[7];
   const int t = threadIdx.x;

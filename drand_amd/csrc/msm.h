@@ -379,6 +379,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_msm_aff_add(uint32_t l, ui
 #if defined(__HIP__) && DG_TU_HOT
 DG_KERNEL void __launch_bounds__(128, DG_MSM_WAVES) k_sum_rows(uint32_t rows, uint32_t cols, uint32_t chunk,
                                                                 const G2JStore* in, G2JStore* out, const uint8_t* skip) {
+  DG_HI();
   __shared__ G2JStore s_acc[128];
   uint32_t ocols = (cols + chunk - 1) / chunk;
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -465,6 +466,7 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_msm_slices(uint32_t nside
 // the first `tsides` sides)
 DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_horner_coop(uint32_t nwin, uint32_t tsides, const G2JStore* S,
                                                                        G2JStore* Wout) {
+  DG_HI();
   __shared__ CoG2Tmp tmp;
   __shared__ CoG2 acc, nxt;
   const uint32_t sw = blockIdx.x, w = sw % nwin;
@@ -488,6 +490,7 @@ DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_horner_coop(uint32_t 
 
 // one 128-lane workgroup per side: out[side] = sum_{w < MSM_WIN} W[side][w]
 DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_msm_final_coop(uint32_t nwin, const G2JStore* W, G2JStore* out) {
+  DG_HI();
   __shared__ CoG2Tmp tmp;
   __shared__ CoG2 acc, nxt;
   const uint32_t side = blockIdx.x;
@@ -764,6 +767,7 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_kmsm_slices(uint32_t nset
 // one 128-lane workgroup per set s: beta_s T_s by cooperative double-and-add (coop.h; beta is odd, so
 // non-zero)
 DG_KERNEL void __launch_bounds__(128, DG_COOP_WAVES) k_kmsm_beta(const uint64_t* seedp, const G2JStore* Tset, G2JStore* out) {
+  DG_HI();
   const uint64_t seed = *seedp;
   __shared__ CoG2Tmp tmp;
   __shared__ CoG2 acc, p;

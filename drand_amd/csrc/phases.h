@@ -422,6 +422,7 @@ DG_KERNEL void __launch_bounds__(128) k_binv_down(uint32_t n, const Fp* vals, co
 }
 // the top level (n <= BINV_C values), one lane: inverses of vals by one safegcd
 DG_KERNEL void __launch_bounds__(64) k_binv_root(uint32_t n, const Fp* vals, Fp* out) {
+  DG_HI();
   if (blockIdx.x * blockDim.x + threadIdx.x != 0) return;
   Fp pre[BINV_C];
   Fp acc = fp_one();
@@ -502,6 +503,7 @@ DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_down(uint32_t n, const Fp* v
 // BINV_R values per lane, the LDS tree, one safegcd on lane 0, back down -- one launch instead of the chunked
 // form's up / root / down chain
 DG_KERNEL void __launch_bounds__(BINV_T) k_binv_blk_root(uint32_t n, const Fp* vals, Fp* out) {
+  DG_HI();
   __shared__ Fp T[2 * BINV_T];
   const uint32_t l = threadIdx.x, a = l * BINV_R;
   // running products with compile-time indices (registers; a runtime-indexed array would live in scratch)

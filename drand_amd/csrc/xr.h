@@ -31,6 +31,7 @@ namespace dg {
 
 constexpr uint64_t XR_TAG = 0x63726f7373726e64ull;  // "crossrnd": domain of the cross-round weights rho_i
 constexpr uint32_t XR_QPG = 4;                       // quads per level-1 group (default; DG_XR_QPG, 1 = no level 1)
+constexpr uint32_t XR_SKIP = 0;                      // 1: no level 2, failed groups go to single checks (DG_XR_SKIP)
 // device counters: [0] candidates, [1] level-1 checks, [2] level-2 checks (quads), [3] level-3 checks (rounds)
 constexpr uint32_t XR_NCNT = 4;
 
@@ -89,6 +90,7 @@ DGI void xq_sum4(Member member, const uint64_t (&rho)[4], GetT getT, PutT putT, 
 // in G2 except with probability 2^-66 (msm.h) and the group tests need no per-item check.  Lane 0 clears the counters.
 DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_xg_sub(uint32_t i0, uint32_t n, const uint32_t* flag,
                                                                const G2AStore* S, uint8_t* status, uint32_t* cnt) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   __shared__ G2JStore s_acc[64];
   if (g == 0)
@@ -107,6 +109,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xg_prep(uint32_t level, uin
                                                              const uint32_t* l3list, const G2JStore* QS,
                                                              const G2JStore* Q, const G2AStore* S,
                                                              const G1AStore* keys, CkState* st, G2JStore* HS) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   __shared__ G2JStore s_h[64], s_s[64];
   if (ck_dead(g, G, cnt + level)) return;
@@ -145,6 +148,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xg_prep(uint32_t level, uin
 // (a, H) has no identity
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_hlines(uint32_t G, const uint32_t* gcnt, const G2JStore* HS,
                                                               CkLine* rl, CkState* st) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (ck_dead(g, G, gcnt)) return;
   const G2A h = g2_to_aff(g2_clear_cofactor(load_g2j(HS[g])));
@@ -152,7 +156,29 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_hlines(uint32_t G, const 
   st[g].np |= 1u;
   ck_lines(h.x, h.y, [&](uint32_t s, const CkLine& l) { rl[(size_t)s * G + g] = l; });
 }
+// k_xg_hlines and checks.h k_ck_lines2 in one launch, in waves of their own (lanes [0, Gp): the hash side, h_eff and
+// its lines into rl; [Gp, 2 Gp): the signature side's lines into l2, Gp = G rounded up to whole waves): the level's two
+// line chains run side by side instead of one after the other
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_lines(uint32_t G, const uint32_t* gcnt, const G2JStore* HS,
+                                                             CkLine* rl, CkState* st, CkLine* l2) {
+  DG_HI();
+  const uint32_t Gp = (G + 63) & ~63u, lane = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t side = lane >= Gp ? 1u : 0u, g = lane - side * Gp;
+  if (ck_dead(g, G, gcnt)) return;
+  if (side) {
+    if (!(st[g].np & 2)) return;
+    const G2A b = load_g2a(st[g].b);
+    ck_lines(b.x, b.y, [&](uint32_t s, const CkLine& l) { l2[(size_t)s * G + g] = l; });
+    return;
+  }
+  const G2A h = g2_to_aff(g2_clear_cofactor(load_g2j(HS[g])));
+  if (h.inf || st[g].a.inf) return;
+  atomicOr(&st[g].np, 1u);
+  ck_lines(h.x, h.y, [&](uint32_t s, const CkLine& l) { rl[(size_t)s * G + g] = l; });
+}
 #else
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_lines(uint32_t G, const uint32_t* gcnt, const G2JStore* HS,
+                                                             CkLine* rl, CkState* st, CkLine* l2);
 DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_xg_sub(uint32_t i0, uint32_t n, const uint32_t* flag,
                                                                const G2AStore* S, uint8_t* status, uint32_t* cnt);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xg_prep(uint32_t level, uint32_t G, const uint32_t* cnt,
@@ -171,6 +197,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xq_sum(uint32_t nqmax, uint
                                                             uint32_t* cnt, const uint32_t* cand, const G2JStore* Q,
                                                             const G2AStore* S, uint4* T4, uint8_t* tinf,
                                                             uint32_t* l2list, G2JStore* QS) {
+  DG_HI();
   const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
   __shared__ G2JStore s_acc[64];
   const uint32_t c = cnt[0], nq = (c + 3) / 4;
@@ -222,6 +249,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xq_sum(uint32_t nqmax, uint
 // order within a wave); none after a passed batch
 DG_KERNEL void __launch_bounds__(256) k_xg_cand(uint32_t i0, uint32_t n, const uint32_t* flag, const uint8_t* status,
                                                 uint32_t* cand, uint32_t* cnt) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const bool on = g < n && !flag[0] && status[i0 + g] == DG_ST_OK_;
   const uint64_t m = __ballot(on);
@@ -235,9 +263,11 @@ DG_KERNEL void __launch_bounds__(256) k_xg_cand(uint32_t i0, uint32_t n, const u
 // the verdicts of level `level` (good[g]: k_ck_final): a passed check leaves its rounds valid (their status is OK
 // already); a failed group lists its quads for level 2, a failed quad its rounds for level 3; a single check writes
 // kyber's verdict.  xrc[level - 1] counts the checks (dg_group_counts).
-DG_KERNEL void __launch_bounds__(128) k_xg_verdict(uint32_t level, uint32_t G, uint32_t qpg, uint32_t* cnt,
+// (skip != 0: a failed group lists its rounds for level 3 directly -- two levels, groups then single rounds)
+DG_KERNEL void __launch_bounds__(128) k_xg_verdict(uint32_t level, uint32_t G, uint32_t qpg, uint32_t skip, uint32_t* cnt,
                                                    const uint8_t* good, const uint32_t* cand, uint32_t* l2list,
                                                    uint32_t* l3list, uint8_t* status, unsigned long long* xrc) {
+  DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G || g >= cnt[level]) return;
   atomicAdd(&xrc[level - 1], 1ull);
@@ -248,7 +278,11 @@ DG_KERNEL void __launch_bounds__(128) k_xg_verdict(uint32_t level, uint32_t G, u
   }
   if (ok) return;
   const uint32_t c = cnt[0], nq = (c + 3) / 4;
-  if (level == 1) {
+  if (level == 1 && skip) {
+    const uint32_t j0 = 4 * g * qpg, j1 = j0 + 4 * qpg < c ? j0 + 4 * qpg : c;
+    const uint32_t pos = atomicAdd(&cnt[3], j1 - j0);
+    for (uint32_t j = j0; j < j1; ++j) l3list[pos + j - j0] = cand[j];
+  } else if (level == 1) {
     const uint32_t q0 = g * qpg, q1 = q0 + qpg < nq ? q0 + qpg : nq;
     const uint32_t pos = atomicAdd(&cnt[2], q1 - q0);
     for (uint32_t q = q0; q < q1; ++q) l2list[pos + q - q0] = q;

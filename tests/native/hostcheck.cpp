@@ -546,6 +546,17 @@ extern "C" int hc_ck_pipeline_check(const uint8_t* pk48, const uint8_t* q1_96, c
   ck_lines(q1.x, q1.y, [&](uint32_t s, const CkLine& l) { l1[s] = l; });
   ck_lines(q2.x, q2.y, [&](uint32_t s, const CkLine& l) { l2[s] = l; });
   const Fp12 f = ck_miller((uint32_t)np, p1.x, p1.y, [&](uint32_t s, uint32_t pair) { return pair ? l2[s] : l1[s]; });
+  // k_ck_miller2: each pair in a lane of its own (its own squarings), the two values multiplied by k_ck_easy
+  const Fp12 m0 = (np & 1) ? ck_miller1(p1.x, p1.y, [&](uint32_t s) { return l1[s]; }) : fp12_one();
+  const Fp12 m1 = (np & 2) ? ck_miller1(fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), [&](uint32_t s) { return l2[s]; })
+                           : fp12_one();
+  const Fp12 f01 = fp12_mul(m0, m1);
+  {
+    const Fp2* u[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+    const Fp2* v[6] = {&f01.c0.c0, &f01.c0.c1, &f01.c0.c2, &f01.c1.c0, &f01.c1.c1, &f01.c1.c2};
+    for (int i = 0; i < 6; ++i)
+      if (!fp2_eq(*u[i], *v[i])) return 3;
+  }
   // k_ck_easy
   CkInv inv;
   const Fp nt = ck_fe1(f, inv);
