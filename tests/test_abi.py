@@ -160,3 +160,12 @@ def test_queue_plan():
         assert got[q] == (10, 1)
     for q in range(1, 5):
         assert got[q][0] % q == 0
+
+
+def test_release_build_reads_no_retired_switches():
+    """Round-4 verdict (hygiene): DG_NO_BIND (and the removed A/B switches) have no effect on the release build -- the
+    library never reads them, so their names are absent from its strings (getenv takes the name as a literal)."""
+    blob = open(L.LIB_PATH, "rb").read()
+    for name in (b"DG_NO_BIND", b"DG_CK_OLD", b"DG_FUSED", b"DG_MSM_JAC", b"DG_FP2_LAZY", b"DG_FP6_DIG",
+                 b"DG_SUB_SEPARATE"):
+        assert name not in blob, name
