@@ -24,6 +24,7 @@ BASELINE.md) over its HIP-event launch time, against the v_mad_u64_u32 peak each
 GPU (tools/microbench/probe.hip).  The per-kernel timing tables go to a side file (--tables-out).
 """
 import argparse
+import collections
 import ctypes
 import json
 import os
@@ -1059,13 +1060,19 @@ def main():
 
     sig_src = [d_sig]  # the signatures the steps verify (the c2_negative line swaps in a corrupted copy)
 
+    hostprof = collections.defaultdict(float) if os.environ.get("DG_BENCH_HOSTPROF") else None
+
     def enqueue(lo, hi, d_st, seed, blocking):
         args_ = (pkb, hi - lo, L.ptr(d_pr[lo:]), L.ptr(d_r[lo:]), L.ptr(d_ps), L.ptr(d_off[lo:]),
                  L.ptr(sig_src[0][lo:]), L.ptr(d_st[lo:]), seed)
+        h0 = time.perf_counter()
         if blocking:
             L.check(lib.dg_verify_beacons_dev(*args_, None))
         else:
             L.check(lib.dg_verify_beacons_dev_async(*args_, None, None if on_set else ctypes.c_void_p(side.cuda_stream)))
+        if hostprof is not None:
+            hostprof["enqueue_s"] += time.perf_counter() - h0
+            hostprof["enqueues"] += 1
 
     def step(seed):
         """Enqueue this rank's batches (asynchronously: consecutive batches overlap) and the all-gather of the
@@ -1073,7 +1080,10 @@ def main():
         i = counter[0] % nbuf
         counter[0] += 1
         if gathered[i] is not None:
+            h0 = time.perf_counter()
             gathered[i][1].synchronize()  # the all-gather that read this status buffer has finished
+            if hostprof is not None:
+                hostprof["bufwait_s"] += time.perf_counter() - h0
         d_st = d_sts[i]
         for j, (lo, hi) in enumerate(bounds):
             enqueue(lo, hi, d_st, seed * 64 + j, args.use_sync)
@@ -1115,11 +1125,18 @@ def main():
         dist.barrier()
     fb0 = L.fallback_count()
     t0 = time.perf_counter()
+    if hostprof is not None:
+        hostprof.clear()
     bits = [step(17 + s) for s in range(args.steps)]
+    if hostprof is not None:
+        hostprof["steps_enqueued_s"] = time.perf_counter() - t0
     drain()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if hostprof is not None:
+        hostprof["timed_s"] = dt
+        print("[hostprof]", json.dumps({k: round(v, 5) for k, v in hostprof.items()}), file=sys.stderr, flush=True)
     assert all(int(bt.sum().item()) == 0 for bt in bits)
     assert all(int(d.max().item()) == 0 for d in d_sts[:min(counter[0], nbuf)])  # (buffers no step used hold 99)
     fallbacks = L.fallback_count() - fb0  # timed batches that ran the per-item pass (0 for valid chains)

@@ -1,6 +1,7 @@
 // libdrandgpu.so: the C-ABI of include/drand_gpu.h over the HIP kernels of kernels.h (gfx950 only).
 // Host code here only moves bytes, sizes launches and sequences kernels; every group/field operation
 // runs on the device.  No CPU fallback exists: without a gfx950 device the API returns DG_E_NODEV.
+#include <chrono>
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
@@ -88,6 +89,13 @@ struct Set {
   std::vector<size_t> pool_size;
   hipEvent_t done = nullptr;
   bool busy = false;
+  // the latency-bound end of this set's beacon batches (MSM row sums and Horner, the Miller loops and final
+  // exponentiation of the batch equation, the cross-round isolation) runs on a high-priority stream: HIP gives those
+  // hardware queues of their own beside the GPU_MAX_HW_QUEUES normal ones (tools/microbench/queue_prio.hip), so a
+  // batch's few-workgroup tail no longer holds one of the 4 queues the bulk kernels share.  hop: the set stream's
+  // bulk part done (the tail stream waits for it).
+  hipStream_t tail = nullptr;
+  hipEvent_t hop = nullptr;
 };
 
 int env_int(const char* name, int dflt) {
@@ -104,6 +112,8 @@ struct Ctx {
   // for every wave the device can hold, so the workspace queues stay at the check pipeline's ~4 KB (12 workspace
   // queues at 5.7 KB each failed dg_init with HSA_STATUS_ERROR_OUT_OF_RESOURCES)
   hipStream_t fb_stream = nullptr;
+  static constexpr int kTails = 4;
+  hipStream_t tails[kTails] = {};  // high-priority streams, set i -> tails[i % kTails] (DG_TAIL=0: none)
   hipStream_t last_stream = nullptr;  // the set stream of the last asynchronous batch (dg_last_batch_stream)
   int cur = 0, next = 0;
   bool timing = false;
@@ -196,6 +206,17 @@ enum Slot {
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
 
+// DG_HOSTPROF=1 (diagnostics): host time inside kernel launches and inside the set waits of acquire_set, printed and
+// reset by dg_wait_all
+struct HostProf {
+  bool on = getenv("DG_HOSTPROF") != nullptr;
+  double launch_us = 0, wait_us = 0;
+  uint64_t launches = 0, waits = 0;
+} g_hp;
+inline double hp_now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int ws(Slot s, size_t bytes, void** out) {
   Set& c = cur_set();
   if (c.pool.size() < S_COUNT) {
@@ -221,7 +242,12 @@ int acquire_set(hipStream_t* st) {
   c.next = (c.next + 1) % active_sets();
   Set& s = c.sets[i];
   if (s.busy) {
+    const double h0 = g_hp.on ? hp_now_us() : 0.0;
     HIPCHK(hipEventSynchronize(s.done));
+    if (g_hp.on) {
+      g_hp.wait_us += hp_now_us() - h0;
+      ++g_hp.waits;
+    }
     s.busy = false;
   }
   c.cur = i;
@@ -276,7 +302,12 @@ int launch_shm(const char* name, void (*k)(Args...), uint32_t n_threads, uint32_
     e1 = get_event();
     (void)hipEventRecord(e0, st);
   }
+  const double h0 = g_hp.on ? hp_now_us() : 0.0;
   hipLaunchKernelGGL(k, dim3(grid), dim3(block), shm, st, args...);
+  if (g_hp.on) {
+    g_hp.launch_us += hp_now_us() - h0;
+    ++g_hp.launches;
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(DG_E_HIP, std::string("launch ") + name + ": " + hipGetErrorString(e));
   if (c.timing) {
@@ -434,7 +465,7 @@ int prefix_pass(uint32_t R, uint32_t k, uint32_t t, int passes, const uint64_t* 
 // `bad` (device, affine only): raised when an input breaks that precondition (msm.h aff_input_ok); the caller
 // passes its batch-failure flag, so such a batch falls back to exact per-item checks.
 int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JStore* PA, const G2JStore* PB, bool test_windows,
-            bool affine, G2JStore** out, G2JStore** win, hipStream_t st, uint32_t* bad = nullptr) {
+            bool affine, G2JStore** out, G2JStore** win, hipStream_t st, uint32_t* bad = nullptr, hipStream_t tst = nullptr) {
   const uint32_t nsides = PB ? 2 : 1, nwin = test_windows ? MSM_WT : MSM_WIN, nbk = nwin * MSM_NB;
   uint32_t *cnt, *list;
   G2JStore *chunks, *BP, *tmp, *P1, *W;
@@ -494,6 +525,12 @@ int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JSt
   RET(reduce_rows(BP, tmp, nbk * nsides, MSM_BSPLIT, st));  // B[side][b] = BP[side * nbk + b]
   }
   RET(launch("k_msm_slices", k_msm_slices, nsides * nwin * MSM_C * MSM_SLICE_LANES, 128, st, nsides, nwin, (const G2JStore*)BP, P1));
+  if (tst) {
+    // the rest is latency-bound: it moves to the batch's tail stream (Set::tail)
+    HIPCHK(hipEventRecord(cur_set().hop, st));
+    HIPCHK(hipStreamWaitEvent(tst, cur_set().hop, 0));
+    st = tst;
+  }
   RET(reduce_rows(P1, tmp, nsides * nwin * MSM_C, MSM_SLICE_LANES, st, g_ctx.slice_fold));  // S[side][w][k] = P1[...]
   RET(launch("k_msm_horner_coop", k_msm_horner_coop, 128 * nwin * nsides, 128, st, nwin, 1u, (const G2JStore*)P1, W));
   RET(launch("k_msm_final_coop", k_msm_final_coop, 128 * nsides, 128, st, nwin, (const G2JStore*)W, *out));
@@ -608,7 +645,9 @@ int decode_items(uint32_t N, uint32_t k, uint32_t nslots, const uint8_t* sigs, u
                 (const Fp*)eout, S, status, cell, iso, sub);
 }
 
-int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out = nullptr) {
+// tst (single key only, may be null): the stream the batch's latency-bound end runs on (Set::tail); the batch is
+// complete in tst's order then
+int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out = nullptr, hipStream_t tst = nullptr) {
   const uint32_t N = b.R * b.k;
   uint64_t* d_seed;
   RET(bind_seed(b, seed_in, st, &d_seed));
@@ -648,7 +687,8 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
   G2JStore* win = nullptr;
   if (b.nslots == 1) {
     // T = sum alpha_r V_r and K = sum alpha_r Q_r in one MSM (shared bucket sort)
-    RET(msm_run(b.R, seed, active, V, b.Q, batched_sub != 0, b.k == 1, &msm, &win, st, flag + 2));
+    RET(msm_run(b.R, seed, active, V, b.Q, batched_sub != 0, b.k == 1, &msm, &win, st, flag + 2, tst));
+    if (tst) st = tst;
     T = msm;
     K = msm + 1;
   } else {
@@ -730,7 +770,10 @@ int decode_key(const uint8_t* pk48_host, hipStream_t st, G1AStore** keys, uint8_
   *keys = c.pk_dev;
   *key_status = c.pk_status;
   if (c.pk_valid && memcmp(c.pk_bytes, pk48_host, 48) == 0) {
-    HIPCHK(hipStreamWaitEvent(st, c.pk_ready, 0));
+    // a cross-stream wait puts a barrier in the stream's hardware queue: only while the decode is still running
+    const hipError_t q = hipEventQuery(c.pk_ready);
+    if (q == hipErrorNotReady) HIPCHK(hipStreamWaitEvent(st, c.pk_ready, 0));
+    else HIPCHK(q);
     return 0;
   }
   // a previous key may still be in use by batches in flight on other sets
@@ -848,7 +891,7 @@ int hash_rounds(uint32_t R, const uint8_t* d_msgs, uint32_t msg_len, hipStream_t
 
 // bls.Verify batch against one key, everything device-resident
 int verify_single_key(const uint8_t* pk48_host, uint32_t n, const uint8_t* d_msgs, uint32_t msg_len,
-                      const uint8_t* d_sigs, uint8_t* d_status, uint64_t seed, hipStream_t st) {
+                      const uint8_t* d_sigs, uint8_t* d_status, uint64_t seed, hipStream_t st, hipStream_t tst = nullptr) {
   G1AStore* keys;
   uint8_t* kst;
   G2JStore* Q;
@@ -857,7 +900,7 @@ int verify_single_key(const uint8_t* pk48_host, uint32_t n, const uint8_t* d_msg
   RET(hash_rounds(n, d_msgs, msg_len, st, &Q));
   RET(wsT(S_S, n, &S));
   Batch b{n, 1, 1, Q, keys, kst, nullptr, d_sigs, 96, 0, S, d_status, d_msgs, msg_len, pk48_host, 48};
-  RET(batch_verify(b, seed, st));
+  RET(batch_verify(b, seed, st, nullptr, tst));
   return 0;
 }
 
@@ -1425,7 +1468,14 @@ int dg_init(int device) {
   for (Set& x : g_ctx.sets) {
     if (!x.stream) HIPCHK(hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking));
     if (!x.done) HIPCHK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
+    if (!x.hop) HIPCHK(hipEventCreateWithFlags(&x.hop, hipEventDisableTiming));
   }
+  if (env_int("DG_TAIL", 1) && !g_ctx.tails[0]) {
+    int least = 0, greatest = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    for (hipStream_t& t : g_ctx.tails) HIPCHK(hipStreamCreateWithPriority(&t, hipStreamNonBlocking, greatest));
+  }
+  for (int i = 0; i < kSets; ++i) g_ctx.sets[i].tail = g_ctx.tails[i % Ctx::kTails];
   if (!g_ctx.fb_stream) HIPCHK(hipStreamCreateWithFlags(&g_ctx.fb_stream, hipStreamNonBlocking));
   if (!g_ctx.fallbacks) {
     HIPCHK(hipMalloc(&g_ctx.fallbacks, sizeof(unsigned long long)));
@@ -1500,6 +1550,9 @@ int dg_init(int device) {
     for (int i = 0; i < active_sets(); ++i)
       for (size_t w : oset) on_sets[w].go(g_ctx.sets[i].stream);
     for (size_t w : ofb) on_fb[w].go(g_ctx.fb_stream);
+    for (hipStream_t t : g_ctx.tails)  // the tail streams' queues (high priority) run the check pipeline too
+      if (t)
+        for (size_t w : oset) on_sets[w].go(t);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
@@ -1520,8 +1573,18 @@ void dg_shutdown(void) {
     x.busy = false;
     if (x.stream) (void)hipStreamDestroy(x.stream);
     if (x.done) (void)hipEventDestroy(x.done);
+    if (x.hop) (void)hipEventDestroy(x.hop);
     x.stream = nullptr;
     x.done = nullptr;
+    x.hop = nullptr;
+    x.tail = nullptr;
+  }
+  for (hipStream_t& t : g_ctx.tails) {
+    if (t) {
+      (void)hipStreamSynchronize(t);
+      (void)hipStreamDestroy(t);
+    }
+    t = nullptr;
   }
   if (g_ctx.fb_stream) {
     (void)hipStreamSynchronize(g_ctx.fb_stream);
@@ -1700,7 +1763,8 @@ static int enqueue_beacons_dev(const uint8_t* pk48_host, size_t n, const uint64_
   }
   uint8_t* d_msgs;
   RET(beacons_to_msgs(n, d_pr, d_r, d_ps, d_off, &d_msgs, st));
-  RET(verify_single_key(pk48_host, (uint32_t)n, d_msgs, 32, d_sigs, d_status, fresh_seed(seed), st));
+  RET(verify_single_key(pk48_host, (uint32_t)n, d_msgs, 32, d_sigs, d_status, fresh_seed(seed), st, set.tail));
+  if (set.tail) st = set.tail;  // the batch ends on its tail stream
   HIPCHK(hipEventRecord(set.done, st));
   set.busy = true;
   g_ctx.last_stream = st;
@@ -1709,6 +1773,13 @@ static int enqueue_beacons_dev(const uint8_t* pk48_host, size_t n, const uint64_
 }
 
 static int wait_all() {
+  if (g_hp.on) {
+    fprintf(stderr, "[dg hostprof] launches %llu: %.1f us each, %.1f ms total; set waits %llu: %.1f ms total\n",
+            (unsigned long long)g_hp.launches, g_hp.launches ? g_hp.launch_us / g_hp.launches : 0.0, g_hp.launch_us / 1e3,
+            (unsigned long long)g_hp.waits, g_hp.wait_us / 1e3);
+    g_hp = HostProf{};
+    g_hp.on = true;
+  }
   for (Set& x : g_ctx.sets)
     if (x.busy) {
       HIPCHK(hipEventSynchronize(x.done));

@@ -487,6 +487,15 @@ DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_rs_combine(uint32_t R, ui
 #endif
 
 #if defined(__HIP__) && DG_TU_HOT
+// table entry e of share j in divergent round u: a lane's eight entries are contiguous (8 x 192 B), so the column
+// loop's data-dependent pick reads 192 consecutive bytes per lane (the round-4 layout, entry-major with the rounds
+// innermost, coalesced only lanes that picked the same entry: ~8x the bytes fetched)
+DGI const uint4* rs_entry(const uint4* T4, uint32_t j, uint32_t u, uint32_t e, uint32_t Rn) {
+  return T4 + (((size_t)j * Rn + u) * 8 + e) * RC_Q;
+}
+DGI uint4* rs_entry(uint4* T4, uint32_t j, uint32_t u, uint32_t e, uint32_t Rn) {
+  return T4 + (((size_t)j * Rn + u) * 8 + e) * RC_Q;
+}
 DGI bool rs_lane(uint32_t g, uint32_t t, uint32_t R, uint32_t Rn, const uint32_t* nl, const uint8_t* rst,
                  uint32_t& j, uint32_t& u, uint32_t& r) {
   if (g >= t * Rn) return false;
@@ -511,7 +520,7 @@ DG_KERNEL void __launch_bounds__(128) k_rs_tab_den(uint32_t l, uint32_t R, uint3
       Fp2 px[4], py[4];
       rs_points(p, px, py);
       Fp2 ax = px[0], ay;
-      if (src) rc_ld(T4 + ((size_t)j * 8 + src) * RC_Q * Rn + u, Rn, ax, ay);
+      if (src) rc_ld(rs_entry(T4, j, u, src, Rn), 1, ax, ay);
       v = fp2_norm(fp2_sub(px[pb], ax));
     }
   }
@@ -530,10 +539,10 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_rs_tab_add(uint32_t l, uin
   Fp2 px[4], py[4];
   rs_points(p, px, py);
   G2A a{px[0], py[0], false};
-  if (src) rc_ld(T4 + ((size_t)j * 8 + src) * RC_Q * Rn + u, Rn, a.x, a.y);
-  else if (e == 0) rc_st(T4 + (size_t)j * 8 * RC_Q * Rn + u, Rn, px[0], py[0]);  // T0 = P0 (level 0, once)
+  if (src) rc_ld(rs_entry(T4, j, u, src, Rn), 1, a.x, a.y);
+  else if (e == 0) rc_st(rs_entry(T4, j, u, 0, Rn), 1, px[0], py[0]);  // T0 = P0 (level 0, once)
   const G2A s = g2_aff_sum(a, G2A{px[pb], py[pb], false}, 1, ninv[g]);
-  rc_st(T4 + ((size_t)j * 8 + dst) * RC_Q * Rn + u, Rn, s.x, s.y);
+  rc_st(rs_entry(T4, j, u, dst, Rn), 1, s.x, s.y);
 }
 
 // lane (share group q, divergent round u), grid RS lanes = ngroups * Rn padded to whole waves: the columns of
@@ -567,14 +576,14 @@ DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rs_sac(uint32_t R, uint32
         pos = (d.sgn >> c) & 1u;
       }
       Fp2 x, y;
-      rc_ld(T4 + ((size_t)j * 8 + e) * RC_Q * Rn + u, Rn, x, y);
+      rc_ld(rs_entry(T4, j, u, e, Rn), 1, x, y);
       g2_madd_lds(acc, x, pos ? y : fp2_neg(y));
     }
   }
   for (uint32_t j = j0; j < j1; ++j) {
     if (pinf[(size_t)j * Rn + u] || !dig[(size_t)j * Rn + u].even) continue;
     Fp2 x, y;
-    rc_ld(T4 + (size_t)j * 8 * RC_Q * Rn + u, Rn, x, y);
+    rc_ld(rs_entry(T4, j, u, 0, Rn), 1, x, y);
     g2_madd_lds(acc, x, fp2_neg(y));
   }
   Aps[(size_t)q * Rn + u] = acc;

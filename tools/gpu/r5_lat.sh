@@ -22,3 +22,12 @@ for cfg in ${CONFIGS:-base: skip:DG_XR_SKIP=1 q1:DG_XR_QPG=1 noprio:lib=tools/va
     || { echo "bench $name failed"; tail -20 gpurun_out/lat_$name.err; exit 1; }
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); n=d['c2_negative']; print(sys.argv[2], 'head', d['value'], 'neg', n['value'], n['ms_per_step'])" gpurun_out/lat_$name.json $name
 done
+if [ -n "$TRACE" ]; then
+  # kernel timeline of the headline (start/end per dispatch with its queue) for the overlap analysis
+  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lat_trace -o run -- \
+    python3 -u bench.py --steps 10 --recover-rounds 0 --c5-rounds 0 --sync-rounds 0 --no-c1 --no-cpu-baseline \
+    --no-peak-detail --no-vp-negative --neg-steps 0 > gpurun_out/lat_trace.json 2> gpurun_out/lat_trace.err \
+    || { echo "trace failed"; tail -20 gpurun_out/lat_trace.err; exit 1; }
+  find gpurun_out/lat_trace -name "*.csv"
+fi
