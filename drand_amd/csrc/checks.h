@@ -211,6 +211,24 @@ DGI bool ck_expsq(const Fp12& x, Put put) {
   }
   return zero;
 }
+// One Karabina squaring (pairing.h cyc_sqr_c) split over the two lanes of a check (k_ck_expsq2, the latency form of
+// the isolation): lane half 0 owns (u, v) = (g2, g3) and has received (x, y) = (g4, g5); half 1 owns (g4, g5) and has
+// received (g2, g3).  Each lane squares the received pair (three Fp2 squarings instead of six per lane) and outputs
+// its own next pair: half 0 (h2, h3), half 1 (h4, h5); the lanes then swap their outputs.
+DGI void ck_cyc_half(uint32_t half, const Fp2& u, const Fp2& v, const Fp2& x, const Fp2& y, Fp2& o1, Fp2& o2) {
+  const Fp2 sx = DG_FP4_SQR2(x), sy = DG_FP4_SQR2(y);
+  const Fp2 b = fp2_sub(fp2_sub(DG_FP4_SQR2(fp2_add(x, y)), sx), sy);  // 2 x y
+  const Fp2 a = fp2_add(sx, fp2_mul_xi(sy));
+  const Fp2 a3 = fp2_add(fp2_dbl(a), a);
+  if (half == 0) {  // h2 = 2 g2 + 3 xi b45, h3 = 3 a45 - 2 g3
+    const Fp2 t = fp2_mul_xi(b);
+    o1 = fp2_add(fp2_dbl(u), fp2_add(fp2_dbl(t), t));
+    o2 = fp2_sub(a3, fp2_dbl(v));
+  } else {  // h4 = 3 a23 - 2 g4, h5 = 2 g5 + 3 b23
+    o1 = fp2_sub(a3, fp2_dbl(u));
+    o2 = fp2_add(fp2_dbl(v), fp2_add(fp2_dbl(b), b));
+  }
+}
 // x^z from the six compressed powers and the inverses of their denominators' norms (get(i, c, nv))
 template <class Get>
 DGI Fp12 ck_expdec(Get get) {
@@ -436,6 +454,61 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const 
   zero[g] = z ? 1 : 0;
   if (z) zl[1 + atomicAdd(zl, 1u)] = g;
 }
+// k_ck_expsq with two lanes per check (lanes 2g, 2g + 1 of a wave: ck_cyc_half, the outputs swapped by a DPP quad
+// permutation): the same sn / nv / zero / zl, half the dependent products per squaring -- the cross-round isolation's
+// checks are few and latency-bound (drand_gpu.hip run_checks(latency))
+__device__ __forceinline__ uint32_t ck_xpair(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1, 0, 3, 2]
+}
+__device__ __forceinline__ Fp2 ck_xpair(const Fp2& a) {
+  Fp2 r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    r.c0.l[i] = ck_xpair(a.c0.l[i]);
+    r.c1.l[i] = ck_xpair(a.c1.l[i]);
+  }
+  return r;
+}
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq2(uint32_t G, const uint32_t* gcnt, const Fp12* X, CycC* sn,
+                                                               Fp* nv, uint8_t* zero, uint32_t* zl) {
+  DG_HI();
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x, g = lane >> 1, half = lane & 1;
+  if (ck_dead(g, G, gcnt)) return;  // (both lanes of a check alike)
+  const Fp12 x = X[g];
+  if (fp12_is_one(x)) {
+    if (!half) zero[g] = 2;
+    return;
+  }
+  // CycC{g2, g3, g4, g5} = {x.c1.c0, x.c0.c2, x.c0.c1, x.c1.c2}
+  Fp2 u = half ? x.c0.c1 : x.c1.c0, v = half ? x.c1.c2 : x.c0.c2;
+  Fp2 p = half ? x.c1.c0 : x.c0.c1, q = half ? x.c0.c2 : x.c1.c2;
+  bool z = false;
+  int n = 0;
+#pragma unroll 1
+  for (int k = 1; k <= 63; ++k) {
+    ck_cyc_half(half, u, v, p, q, u, v);
+    p = ck_xpair(u);
+    q = ck_xpair(v);
+    if ((Z_ABS >> k) & 1) {
+      CycC* c = sn + (size_t)n * G + g;
+      if (!half) {
+        c->g2 = u;
+        c->g3 = v;
+        const Fp2 d = fp2_dbl(fp2_dbl(u));
+        z |= fp2_is_zero(d);
+        nv[(size_t)n * G + g] = fp2_norm(d);
+      } else {
+        c->g4 = u;
+        c->g5 = v;
+      }
+      ++n;
+    }
+  }
+  if (!half) {
+    zero[g] = z ? 1 : 0;
+    if (z) zl[1 + atomicAdd(zl, 1u)] = g;
+  }
+}
 // the verdicts of the group / single checks of Recover's pass (good[g]: the check held, k_ck_final): a passed group
 // accepts its members (error probability <= 2^-63 each), a failed group sends them to their own checks (FIN_RECHECK),
 // a single check is kyber's bls.Verify verdict
@@ -470,6 +543,8 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_L2_WAVES) k_ck_lines2(uint32_t G, con
                                                                  CkLine* l2);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const uint32_t* gcnt, const Fp12* X, CycC* sn,
                                                               Fp* nv, uint8_t* zero, uint32_t* zl);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq2(uint32_t G, const uint32_t* gcnt, const Fp12* X, CycC* sn,
+                                                               Fp* nv, uint8_t* zero, uint32_t* zl);
 DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const uint8_t* good_, uint8_t* status,
                                                    uint8_t* fin);
 #endif

@@ -1070,9 +1070,12 @@ int ck_bufs(CkBufs& b, size_t G, bool group_sums) {
 // product with the six norms inverted in the lane (k_ck_expdec), the uncompressed chain for the lanes with a zero
 // denominator (k_ck_explain over work list z, CK_EXPLAIN_LANES lanes: it is rare); out = X^z op(Y) (Y may be null)
 int ck_expz(uint32_t z, uint32_t G, const uint32_t* gcnt, const Fp12* X, const Fp12* Y, uint32_t nfrob, uint32_t conj,
-            Fp12* out, const CkBufs& b, hipStream_t st) {
+            Fp12* out, const CkBufs& b, hipStream_t st, bool latency) {
   uint32_t* zl = b.zl + (size_t)z * (G + 1);
-  RET(launch("k_ck_expsq", k_ck_expsq, G, 64, st, G, gcnt, X, b.sn, b.nv, b.zero, zl));
+  if (latency)  // two lanes per check
+    RET(launch("k_ck_expsq2", k_ck_expsq2, 2 * G, 64, st, G, gcnt, X, b.sn, b.nv, b.zero, zl));
+  else
+    RET(launch("k_ck_expsq", k_ck_expsq, G, 64, st, G, gcnt, X, b.sn, b.nv, b.zero, zl));
   RET(launch("k_ck_expdec", k_ck_expdec, G, 64, st, G, gcnt, (const CycC*)b.sn, b.nv, (const uint8_t*)b.zero, Y, nfrob,
              conj, out));
   return launch("k_ck_explain", k_ck_explain, CK_EXPLAIN_LANES, 64, st, (const uint32_t*)zl, X, Y, nfrob, conj, out);
@@ -1095,11 +1098,11 @@ int run_checks(uint32_t G, const uint32_t* gcnt, uint32_t R, const CkLine* rl, c
   RET(launch("k_ck_easy", k_ck_easy, G, 64, st, G, gcnt, latency ? 1u : 0u, (const Fp12*)b.F, b.F2, b.zl));
   // hard part (final_exp_cubed): t0 = f2^z conj(f2), t1 = t0^z conj(t0), a = t1^z frob(t1),
   // b = (a^z)^z frob^2(a) conj(a), c = f2^3, result b c
-  RET(ck_expz(0, G, gcnt, b.F2, b.F2, 0, 1, b.T0, b, st));
-  RET(ck_expz(1, G, gcnt, b.T0, b.T0, 0, 1, b.T1, b, st));
-  RET(ck_expz(2, G, gcnt, b.T1, b.T1, 1, 0, b.A, b, st));
-  RET(ck_expz(3, G, gcnt, b.A, nullptr, 0, 0, b.T0, b, st));
-  RET(ck_expz(4, G, gcnt, b.T0, b.A, 2, 0, b.T1, b, st));
+  RET(ck_expz(0, G, gcnt, b.F2, b.F2, 0, 1, b.T0, b, st, latency));
+  RET(ck_expz(1, G, gcnt, b.T0, b.T0, 0, 1, b.T1, b, st, latency));
+  RET(ck_expz(2, G, gcnt, b.T1, b.T1, 1, 0, b.A, b, st, latency));
+  RET(ck_expz(3, G, gcnt, b.A, nullptr, 0, 0, b.T0, b, st, latency));
+  RET(ck_expz(4, G, gcnt, b.T0, b.A, 2, 0, b.T1, b, st, latency));
   return launch("k_ck_final", k_ck_final, G, 64, st, G, gcnt, (const CkState*)b.st, (const Fp12*)b.T1,
                 (const Fp12*)b.A, (const Fp12*)b.F2, b.good);
 }
@@ -1465,16 +1468,37 @@ int dg_init(int device) {
                     "workspace sets for them; a process that started HIP before loading the library has HIP's 4 -- set "
                     "GPU_MAX_HW_QUEUES before the first HIP call (DG_QUIET=1 silences this)\n",
             kDefaultHwQueues, active_sets());
-  for (Set& x : g_ctx.sets) {
-    if (!x.stream) HIPCHK(hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking));
+  int least_prio = 0, greatest_prio = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&least_prio, &greatest_prio));
+  // (the odd sets on low-priority streams, queues of their own: 13.1 -> 12.2 M rounds/s, dropped -- DESIGN.md §5.3)
+  // A/B (DG_TAIL_CUS=k): k CUs, spread over the chip, reserved for the tail streams (the set streams masked off
+  // them), so the latency-bound waves never share a SIMD with the bulk kernels'
+  const int tail_cus = env_int("DG_TAIL_CUS", 0);
+  std::vector<uint32_t> set_mask, tail_mask;
+  if (tail_cus > 0 && tail_cus < prop.multiProcessorCount) {
+    const int ncu = prop.multiProcessorCount, every = ncu / tail_cus;
+    set_mask.assign((ncu + 31) / 32, 0u);
+    tail_mask.assign((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; ++c) ((c % every == every - 1) ? tail_mask : set_mask)[c / 32] |= 1u << (c % 32);
+  }
+  for (int i = 0; i < kSets; ++i) {
+    Set& x = g_ctx.sets[i];
+    if (!x.stream) {
+      if (!set_mask.empty())
+        HIPCHK(hipExtStreamCreateWithCUMask(&x.stream, (uint32_t)set_mask.size(), set_mask.data()));
+      else
+        HIPCHK(hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking));
+    }
     if (!x.done) HIPCHK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
     if (!x.hop) HIPCHK(hipEventCreateWithFlags(&x.hop, hipEventDisableTiming));
   }
-  if (env_int("DG_TAIL", 1) && !g_ctx.tails[0]) {
-    int least = 0, greatest = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    for (hipStream_t& t : g_ctx.tails) HIPCHK(hipStreamCreateWithPriority(&t, hipStreamNonBlocking, greatest));
-  }
+  if (env_int("DG_TAIL", 1) && !g_ctx.tails[0])
+    for (hipStream_t& t : g_ctx.tails) {
+      if (!tail_mask.empty())
+        HIPCHK(hipExtStreamCreateWithCUMask(&t, (uint32_t)tail_mask.size(), tail_mask.data()));
+      else
+        HIPCHK(hipStreamCreateWithPriority(&t, hipStreamNonBlocking, greatest_prio));
+    }
   for (int i = 0; i < kSets; ++i) g_ctx.sets[i].tail = g_ctx.tails[i % Ctx::kTails];
   if (!g_ctx.fb_stream) HIPCHK(hipStreamCreateWithFlags(&g_ctx.fb_stream, hipStreamNonBlocking));
   if (!g_ctx.fallbacks) {
@@ -1516,6 +1540,7 @@ int dg_init(int device) {
         {(const void*)k_ck_miller2, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_miller2, g1, b64, 0, q, 0u, cz, 0u, (const CkState*)nullptr, (const CkLine*)nullptr, (const CkLine*)nullptr, (Fp12*)nullptr); }},
         {(const void*)k_xg_lines, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_lines, g1, b64, 0, q, 0u, cz, (const G2JStore*)nullptr, (CkLine*)nullptr, (CkState*)nullptr, (CkLine*)nullptr); }},
         {(const void*)k_ck_expsq, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_expsq, g1, b64, 0, q, 0u, cz, (const Fp12*)nullptr, (CycC*)nullptr, (Fp*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr); }},
+        {(const void*)k_ck_expsq2, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_expsq2, g1, b64, 0, q, 0u, cz, (const Fp12*)nullptr, (CycC*)nullptr, (Fp*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr); }},
         {(const void*)k_ck_expdec, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_expdec, g1, b64, 0, q, 0u, cz, (const CycC*)nullptr, (Fp*)nullptr, (const uint8_t*)nullptr, (const Fp12*)nullptr, 0u, 0u, (Fp12*)nullptr); }},
         {(const void*)k_ck_explain, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_explain, g1, b64, 0, q, cz, (const Fp12*)nullptr, (const Fp12*)nullptr, 0u, 0u, (Fp12*)nullptr); }},
         {(const void*)k_ck_final, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_final, g1, b64, 0, q, 0u, cz, (const CkState*)nullptr, (const Fp12*)nullptr, (const Fp12*)nullptr, (const Fp12*)nullptr, (uint8_t*)nullptr); }},

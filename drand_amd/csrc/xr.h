@@ -9,13 +9,16 @@
 //     e(X, h_eff(sum rho_i Q_i)) == e(g1, sum rho_i S_i)          (Q_i the uncleared hash of round i: h_eff is linear)
 // holds for a set of valid rounds, and a set holding a bad round passes with probability <= 2^-63 (every S_i in G2 --
 // the batch's windowed subgroup check, or k_xg_sub after it failed -- and E_i = x h(Q_i) - S_i != 0 vanishes in the
-// weighted sum for at most one rho_i mod r).  Three levels, each one run of the pipeline with its checks listed on the
+// weighted sum for at most one rho_i mod r).  Levels, each one run of the pipeline with its checks listed on the
 // device:
-//     level 1  groups of qpg quads (4 qpg rounds; default 16)          -> a failed group lists its quads
-//     level 2  quads (4 rounds)                                        -> a failed quad lists its rounds
+//     level 1  groups of qpg quads (4 qpg rounds; default 16)          -> a failed group lists its rounds (default) or
+//                                                                         its quads (DG_XR_SKIP=0)
+//     level 2  quads (4 rounds; DG_XR_SKIP=0 only)                     -> a failed quad lists its rounds
 //     level 3  single rounds: e(X, h(Q_i)) == e(g1, S_i), kyber's bls.Verify verdict, exact
 // Every round of a passed group or quad keeps its OK status (error <= 2^-63); every rejected round was rejected by its
-// own exact check.  At 1% bad rounds a 100k-round batch takes ~6.3 k + ~3.7 k + ~4 k checks instead of 100 k.
+// own exact check.  At 1% bad rounds a 100k-round batch takes ~6.3 k + ~15 k checks (three levels: ~6.3 k + ~3.7 k +
+// ~4 k) instead of 100 k.  Each level costs the latency of one check, so two levels beat three (c2_negative 3.3 vs
+// 2.8 M rounds/s).
 //
 //   k_xg_sub    (after a failed windowed subgroup check only) the G2 subgroup check of every decoded signature
 //   k_xg_cand   the decoded rounds of a failed batch, compacted (nothing after a passed batch)
@@ -31,7 +34,7 @@ namespace dg {
 
 constexpr uint64_t XR_TAG = 0x63726f7373726e64ull;  // "crossrnd": domain of the cross-round weights rho_i
 constexpr uint32_t XR_QPG = 4;                       // quads per level-1 group (default; DG_XR_QPG, 1 = no level 1)
-constexpr uint32_t XR_SKIP = 0;                      // 1: no level 2, failed groups go to single checks (DG_XR_SKIP)
+constexpr uint32_t XR_SKIP = 1;                      // 1: no level 2, failed groups go to single checks (DG_XR_SKIP)
 // device counters: [0] candidates, [1] level-1 checks, [2] level-2 checks (quads), [3] level-3 checks (rounds)
 constexpr uint32_t XR_NCNT = 4;
 

@@ -517,6 +517,7 @@ extern "C" int hc_cyc_exp_check(uint64_t seed, uint32_t n) {
 // Q2 at -g1, the easy part through ck_fe1 / ck_inv with the Fp inversion of the batch, the hard part through the
 // compressed chains (ck_expsq / ck_expdec, or ck_exp_plain where a denominator is zero) and ck_mul_op.  `np` drops
 // pairs as pair_check does (bit 0: (P1, Q1), bit 1: (-g1, Q2)).  Returns 1 when both Fp12 values are equal.
+static bool g_split_bad = false;  // ck_cyc_half disagreed with cyc_sqr_c (hc_ck_pipeline_check returns 4)
 static Fp12 hc_ck_expz(const Fp12& x, const Fp12* y, uint32_t nfrob, uint32_t conj) {
   // k_ck_expsq, k_ck_expdec (norms inverted in the lane by ck_inv6), k_ck_explain; times op(y) when given
   CycC sn[CK_NPOW];
@@ -527,6 +528,20 @@ static Fp12 hc_ck_expz(const Fp12& x, const Fp12* y, uint32_t nfrob, uint32_t co
   } else if (ck_expsq(x, [&](int i, const CycC& c, const Fp& n) { sn[i] = c; nv[i] = n; })) {
     xz = ck_exp_plain(x);
   } else {
+    // k_ck_expsq2: the two halves of the split squaring (ck_cyc_half), outputs swapped after every step
+    Fp2 u0 = x.c1.c0, v0 = x.c0.c2, u1 = x.c0.c1, v1 = x.c1.c2;
+    int n = 0;
+    for (int k = 1; k <= 63; ++k) {
+      Fp2 a0, b0, a1, b1;
+      ck_cyc_half(0, u0, v0, u1, v1, a0, b0);
+      ck_cyc_half(1, u1, v1, u0, v0, a1, b1);
+      u0 = a0, v0 = b0, u1 = a1, v1 = b1;
+      if ((Z_ABS >> k) & 1) {
+        if (!fp2_eq(u0, sn[n].g2) || !fp2_eq(v0, sn[n].g3) || !fp2_eq(u1, sn[n].g4) || !fp2_eq(v1, sn[n].g5))
+          g_split_bad = true;
+        ++n;
+      }
+    }
     ck_inv6([&](int i) { return nv[i]; }, [&](int i, const Fp& v) { nv[i] = v; });
     xz = ck_expdec([&](int i, CycC& c, Fp& n) { c = sn[i]; n = nv[i]; });
   }
@@ -569,6 +584,7 @@ extern "C" int hc_ck_pipeline_check(const uint8_t* pk48, const uint8_t* q1_96, c
   const Fp12 t = hc_ck_expz(hc_ck_expz(a, nullptr, 0, 0), &a, 2, 0);
   const Fp12 c = ck_mul_op(ck_mul_op(f2, f2, 0, 0), f2, 0, 0);
   const Fp12 res = n ? ck_mul_op(ck_mul_op(t, a, 0, 1), c, 0, 0) : fp12_one();
+  if (g_split_bad) return 4;
   const Fp2* u[6] = {&res.c0.c0, &res.c0.c1, &res.c0.c2, &res.c1.c0, &res.c1.c1, &res.c1.c2};
   const Fp2* v[6] = {&ref.c0.c0, &ref.c0.c1, &ref.c0.c2, &ref.c1.c0, &ref.c1.c1, &ref.c1.c2};
   for (int i = 0; i < 6; ++i)

@@ -91,7 +91,7 @@ def test_chain_100k_one_percent_replaced_vs_twin():
     """configs[1] negative: the 100k-round linked chain with 1% of the signatures replaced by the
     next round's (the positions of bench.py's c2_negative line) as one dg_verify_beacons_dev batch: exactly those
     rounds rejected as bad signatures, the rest valid; the twin agrees on every replaced round and on 4000 others;
-    the isolation ran its three levels (dg_isolation_counts) far below one check per round."""
+    the isolation ran its levels (dg_isolation_counts) far below one check per round."""
     import torch
 
     N = 100000
@@ -149,15 +149,17 @@ np.save(sys.argv[3], st)
 """
 
 
-@pytest.mark.parametrize("qpg", ["1", "16"])
-def test_level_shapes_vs_twin(tmp_path, qpg):
-    """The isolation's level shapes (DG_XR_QPG: 1 = quads then single rounds, no level 1; 16 = groups of 64 rounds)
-    in a child process: the same statuses as the twin on a mixed batch."""
-    pk, msgs, bad, want = _mixed(2048, b"qpg" + qpg.encode())
+@pytest.mark.parametrize("shape", [{"DG_XR_QPG": "1"}, {"DG_XR_QPG": "16"}, {"DG_XR_SKIP": "0"}],
+                         ids=["quads", "qpg16", "three-levels"])
+def test_level_shapes_vs_twin(tmp_path, shape):
+    """The isolation's level shapes in a child process (DG_XR_QPG: 1 = quads then single rounds, no level 1; 16 =
+    groups of 64 rounds; DG_XR_SKIP=0: groups, then quads, then single rounds): the same statuses as the twin on a
+    mixed batch."""
+    pk, msgs, bad, want = _mixed(2048, b"qpg" + "".join(shape.values()).encode())
     inp, out = tmp_path / "in.npz", tmp_path / "out.npy"
     np.savez(inp, pk=np.frombuffer(pk, np.uint8), msgs=msgs, sigs=bad, seed=9)
     r = subprocess.run([sys.executable, "-c", _QPG_CHILD, ROOT, str(inp), str(out)],
-                       env=dict(os.environ, DG_XR_QPG=qpg), capture_output=True, text=True, timeout=300, cwd=ROOT)
+                       env=dict(os.environ, **shape), capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     assert np.array_equal(np.load(out), want)
 

@@ -14,7 +14,7 @@ for cfg in ${CONFIGS:-base: skip:DG_XR_SKIP=1 q1:DG_XR_QPG=1 noprio:lib=tools/va
   case "$kv" in
     lib=*) envs="DRAND_GPU_LIB=${kv#lib=}";;
     "") envs="";;
-    *) envs="$kv";;
+    *) envs="${kv//,/ }";;
   esac
   env $envs timeout -k 10 300 python -u bench.py --steps ${BENCH_STEPS:-10} --recover-rounds 0 --c5-rounds 0 \
     --sync-rounds 0 --no-c1 --no-cpu-baseline --no-peak-detail --no-vp-negative --neg-steps ${NEG_STEPS:-10} \
