@@ -112,8 +112,9 @@ struct Ctx {
   // for every wave the device can hold, so the workspace queues stay at the check pipeline's ~4 KB (12 workspace
   // queues at 5.7 KB each failed dg_init with HSA_STATUS_ERROR_OUT_OF_RESOURCES)
   hipStream_t fb_stream = nullptr;
-  static constexpr int kTails = 4;
-  hipStream_t tails[kTails] = {};  // high-priority streams, set i -> tails[i % kTails] (DG_TAIL=0: none)
+  static constexpr int kTails = 12;
+  hipStream_t tails[kTails] = {};  // high-priority streams, set i -> tails[i % ntails] (DG_TAILS, 0: none)
+  int ntails = 0;
   hipStream_t last_stream = nullptr;  // the set stream of the last asynchronous batch (dg_last_batch_stream)
   int cur = 0, next = 0;
   bool timing = false;
@@ -1471,35 +1472,20 @@ int dg_init(int device) {
   int least_prio = 0, greatest_prio = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&least_prio, &greatest_prio));
   // (the odd sets on low-priority streams, queues of their own: 13.1 -> 12.2 M rounds/s, dropped -- DESIGN.md §5.3)
-  // A/B (DG_TAIL_CUS=k): k CUs, spread over the chip, reserved for the tail streams (the set streams masked off
-  // them), so the latency-bound waves never share a SIMD with the bulk kernels'
-  const int tail_cus = env_int("DG_TAIL_CUS", 0);
-  std::vector<uint32_t> set_mask, tail_mask;
-  if (tail_cus > 0 && tail_cus < prop.multiProcessorCount) {
-    const int ncu = prop.multiProcessorCount, every = ncu / tail_cus;
-    set_mask.assign((ncu + 31) / 32, 0u);
-    tail_mask.assign((ncu + 31) / 32, 0u);
-    for (int c = 0; c < ncu; ++c) ((c % every == every - 1) ? tail_mask : set_mask)[c / 32] |= 1u << (c % 32);
-  }
+  // (16 or 32 CUs reserved for the tail streams by CU masks, the set streams masked off them: 7.7 / 12.3 M rounds/s
+  // against 12.8 M, c2_negative 2.2 / 3.4 against 3.5 M -- dropped)
   for (int i = 0; i < kSets; ++i) {
     Set& x = g_ctx.sets[i];
-    if (!x.stream) {
-      if (!set_mask.empty())
-        HIPCHK(hipExtStreamCreateWithCUMask(&x.stream, (uint32_t)set_mask.size(), set_mask.data()));
-      else
-        HIPCHK(hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking));
-    }
+    if (!x.stream) HIPCHK(hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking));
     if (!x.done) HIPCHK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
     if (!x.hop) HIPCHK(hipEventCreateWithFlags(&x.hop, hipEventDisableTiming));
   }
-  if (env_int("DG_TAIL", 1) && !g_ctx.tails[0])
-    for (hipStream_t& t : g_ctx.tails) {
-      if (!tail_mask.empty())
-        HIPCHK(hipExtStreamCreateWithCUMask(&t, (uint32_t)tail_mask.size(), tail_mask.data()));
-      else
-        HIPCHK(hipStreamCreateWithPriority(&t, hipStreamNonBlocking, greatest_prio));
-    }
-  for (int i = 0; i < kSets; ++i) g_ctx.sets[i].tail = g_ctx.tails[i % Ctx::kTails];
+  if (!g_ctx.tails[0]) {
+    g_ctx.ntails = std::max(0, std::min(Ctx::kTails, env_int("DG_TAILS", 4)));
+    for (int i = 0; i < g_ctx.ntails; ++i)
+      HIPCHK(hipStreamCreateWithPriority(&g_ctx.tails[i], hipStreamNonBlocking, greatest_prio));
+  }
+  for (int i = 0; i < kSets; ++i) g_ctx.sets[i].tail = g_ctx.ntails ? g_ctx.tails[i % g_ctx.ntails] : nullptr;
   if (!g_ctx.fb_stream) HIPCHK(hipStreamCreateWithFlags(&g_ctx.fb_stream, hipStreamNonBlocking));
   if (!g_ctx.fallbacks) {
     HIPCHK(hipMalloc(&g_ctx.fallbacks, sizeof(unsigned long long)));
@@ -1611,6 +1597,7 @@ void dg_shutdown(void) {
     }
     t = nullptr;
   }
+  g_ctx.ntails = 0;
   if (g_ctx.fb_stream) {
     (void)hipStreamSynchronize(g_ctx.fb_stream);
     (void)hipStreamDestroy(g_ctx.fb_stream);
