@@ -349,6 +349,20 @@ DGI G2A ck_g2_affine(const G2J& b, const Fp& ninv) {
 
 #if defined(__HIP__)
 static_assert(CK_GRP == GRP, "one group per check");
+// the partner lane's value (lanes 2i, 2i + 1 swap: DPP quad_perm [1, 0, 3, 2]); both lanes must be active
+__device__ __forceinline__ uint32_t ck_xpair(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ Fp2 ck_xpair(const Fp2& a) {
+  Fp2 r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    r.c0.l[i] = ck_xpair(a.c0.l[i]);
+    r.c1.l[i] = ck_xpair(a.c1.l[i]);
+  }
+  return r;
+}
+
 // H_r = h_eff(Q_r) and its 68 lines (once per Recover call and round): rl[s * R + r]; hinf[r]: H_r is the identity
 // (kernels_check_a.hip)
 #if DG_TU_CHECK == 1
@@ -457,18 +471,6 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const 
 // k_ck_expsq with two lanes per check (lanes 2g, 2g + 1 of a wave: ck_cyc_half, the outputs swapped by a DPP quad
 // permutation): the same sn / nv / zero / zl, half the dependent products per squaring -- the cross-round isolation's
 // checks are few and latency-bound (drand_gpu.hip run_checks(latency))
-__device__ __forceinline__ uint32_t ck_xpair(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1, 0, 3, 2]
-}
-__device__ __forceinline__ Fp2 ck_xpair(const Fp2& a) {
-  Fp2 r;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    r.c0.l[i] = ck_xpair(a.c0.l[i]);
-    r.c1.l[i] = ck_xpair(a.c1.l[i]);
-  }
-  return r;
-}
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq2(uint32_t G, const uint32_t* gcnt, const Fp12* X, CycC* sn,
                                                                Fp* nv, uint8_t* zero, uint32_t* zl) {
   DG_HI();

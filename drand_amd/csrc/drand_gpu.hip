@@ -112,8 +112,8 @@ struct Ctx {
   // for every wave the device can hold, so the workspace queues stay at the check pipeline's ~4 KB (12 workspace
   // queues at 5.7 KB each failed dg_init with HSA_STATUS_ERROR_OUT_OF_RESOURCES)
   hipStream_t fb_stream = nullptr;
-  static constexpr int kTails = 12;
-  hipStream_t tails[kTails] = {};  // high-priority streams, set i -> tails[i % ntails] (DG_TAILS, 0: none)
+  static constexpr int kTails = 4;
+  hipStream_t tails[kTails] = {};  // high-priority streams, set i -> tails[i % ntails] (DG_TAIL=0: none)
   int ntails = 0;
   hipStream_t last_stream = nullptr;  // the set stream of the last asynchronous batch (dg_last_batch_stream)
   int cur = 0, next = 0;
@@ -1469,7 +1469,7 @@ int dg_init(int device) {
                     "workspace sets for them; a process that started HIP before loading the library has HIP's 4 -- set "
                     "GPU_MAX_HW_QUEUES before the first HIP call (DG_QUIET=1 silences this)\n",
             kDefaultHwQueues, active_sets());
-  int least_prio = 0, greatest_prio = 0;
+  int least_prio = 0, greatest_prio = 0;  // the tail streams take the greatest
   HIPCHK(hipDeviceGetStreamPriorityRange(&least_prio, &greatest_prio));
   // (the odd sets on low-priority streams, queues of their own: 13.1 -> 12.2 M rounds/s, dropped -- DESIGN.md §5.3)
   // (16 or 32 CUs reserved for the tail streams by CU masks, the set streams masked off them: 7.7 / 12.3 M rounds/s
@@ -1480,8 +1480,9 @@ int dg_init(int device) {
     if (!x.done) HIPCHK(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
     if (!x.hop) HIPCHK(hipEventCreateWithFlags(&x.hop, hipEventDisableTiming));
   }
+  // (8 or 12 tail streams, or 2-4 of 6-8 at low priority: no gain)
   if (!g_ctx.tails[0]) {
-    g_ctx.ntails = std::max(0, std::min(Ctx::kTails, env_int("DG_TAILS", 4)));
+    g_ctx.ntails = env_int("DG_TAIL", 1) ? Ctx::kTails : 0;
     for (int i = 0; i < g_ctx.ntails; ++i)
       HIPCHK(hipStreamCreateWithPriority(&g_ctx.tails[i], hipStreamNonBlocking, greatest_prio));
   }
