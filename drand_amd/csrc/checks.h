@@ -30,6 +30,7 @@
 // formulas in the same order, only split across kernels (tests/test_host_arith.py runs the pipeline's pieces on the
 // host against pair_check).
 #pragma once
+#include "fpd.h"
 
 namespace dg {
 
@@ -150,6 +151,28 @@ DGI Fp12 ck_miller(uint32_t np, const Fp& ax, const Fp& ay, Line line) {
   return fp12_conj(f);
 }
 
+// ck_miller with the accumulator and the line values in digit form through the whole loop (fpd.h): converted from the
+// 12-limb lines as they are read and back once at the end -- the same value (tests/native/hostcheck.cpp)
+#ifndef DG_CK_MILLER_D
+#define DG_CK_MILLER_D 0  // 1: measured 7% slower (k_ck_miller 678 -> 728 ms per C5 run: 213+ spilled VGPRs), DESIGN.md §8
+#endif
+template <class Line>
+DGI Fp12 ck_miller_d(uint32_t np, const Fp& ax, const Fp& ay, Line line) {
+  if (!np) return fp12_one();
+  const Fp gx = fp_const(G1_GEN_X), gy = fp_const(G1_GEN_NEG_Y);
+  Fd12 f = fd12_one();
+#pragma unroll 1
+  for (uint32_t it = 0; it < 2 * CK_STEPS; ++it) {
+    const uint32_t s = it >> 1, pair = it & 1;
+    if (pair == 0 && s != 0 && ck_step_is_dbl(s)) f = fd12_sqr(f);
+    if ((np >> pair) & 1) {
+      const CkLine l = line(s, pair);
+      const Fd px = fd_from(fp_sel(pair != 0, ax, gx)), py = fd_from(fp_sel(pair != 0, ay, gy));
+      f = fd12_mul_014(f, fd2_from(l.c0), fd2_mul_fp(fd2_from(l.c1), px), fd2_mul_fp(fd2_from(l.c4), py));
+    }
+  }
+  return fp12_conj(fd12_to(f));
+}
 // the Miller value of ONE pair of a check (pair 0: (a, H) at P = (px, py); pair 1: (-g1, b)), its own squarings included:
 // the two pairs' values multiply to ck_miller's (squaring is multiplicative), conjugated.  Two lanes per check halve the
 // lane's chain where the checks of a launch are too few to fill the chip (the cross-round isolation, xr.h).
@@ -584,9 +607,12 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, const 
   if (ck_dead(g, G, gcnt)) return;
   const uint32_t np = st[g].np, r = st[g].round;
   const Fp ax = st[g].a.x, ay = st[g].a.y;
-  F[g] = ck_miller(np, ax, ay, [&](uint32_t s, uint32_t pair) {
-    return pair ? l2[(size_t)s * G + g] : rl[(size_t)s * R + r];
-  });
+  const auto line = [&](uint32_t s, uint32_t pair) { return pair ? l2[(size_t)s * G + g] : rl[(size_t)s * R + r]; };
+#if DG_CK_MILLER_D
+  F[g] = ck_miller_d(np, ax, ay, line);
+#else
+  F[g] = ck_miller(np, ax, ay, line);
+#endif
 }
 // two lanes per check (lanes [0, Gp) pair 0, [Gp, 2 Gp) pair 1, Gp = G rounded up to whole waves): F[pair G + g]
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller2(uint32_t G, const uint32_t* gcnt, uint32_t R,

@@ -174,8 +174,8 @@ int dg_verify_beacons_dev_async(const uint8_t* pk48_host, size_t n, const uint64
  * every queue count since the check pipeline replaced the large-scratch per-item kernels).  Host-only, no device
  * needed.  (No reference counterpart.) */
 int dg_queue_plan(int hw_queues, int* sets, int* per_item_on_set_streams);
-/* The HIP stream (hipStream_t) the most recent dg_verify_beacons_dev_async batch was enqueued on.  Work the caller
- * enqueues there runs after that batch with no cross-stream wait: with fewer hardware queues than streams
+/* The HIP stream (hipStream_t) the most recent dg_verify_beacons_dev_async batch completes on (its high-priority tail
+ * stream).  Work the caller enqueues there runs after that batch with no cross-stream wait: with fewer hardware queues than streams
  * (GPU_MAX_HW_QUEUES, HIP's default 4) a wait queued on a shared queue holds every stream behind it, so a consumer
  * of one batch's statuses (an all-gather, a copy) is cheapest on this stream.  The stream stays owned by the library
  * (valid until dg_shutdown); DG_E_ARG before the first asynchronous batch.  (No reference counterpart: drand verifies

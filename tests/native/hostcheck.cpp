@@ -4,7 +4,16 @@
 
 #include <vector>
 
+#include <stdio.h>
+#define DG_FD_CHECK 1  // fpd.h: assert the digit-form bounds in every host product, subtraction and reduction
 #include "../../drand_amd/csrc/kernels.h"
+static bool g_fd_bad = false;
+namespace dg {
+void fd_check_fail(const char* what) {
+  if (!g_fd_bad) fprintf(stderr, "fpd bound violated: %s\n", what);
+  g_fd_bad = true;
+}
+}  // namespace dg
 using namespace dg;
 extern "C" {
 void hc_fp_mul(const uint8_t* a48, const uint8_t* b48, uint8_t* out48) {
@@ -561,6 +570,15 @@ extern "C" int hc_ck_pipeline_check(const uint8_t* pk48, const uint8_t* q1_96, c
   ck_lines(q1.x, q1.y, [&](uint32_t s, const CkLine& l) { l1[s] = l; });
   ck_lines(q2.x, q2.y, [&](uint32_t s, const CkLine& l) { l2[s] = l; });
   const Fp12 f = ck_miller((uint32_t)np, p1.x, p1.y, [&](uint32_t s, uint32_t pair) { return pair ? l2[s] : l1[s]; });
+  {
+    // k_ck_miller's digit-form loop (fpd.h, bounds asserted: DG_FD_CHECK)
+    const Fp12 fd = ck_miller_d((uint32_t)np, p1.x, p1.y, [&](uint32_t s, uint32_t pair) { return pair ? l2[s] : l1[s]; });
+    const Fp2* u[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+    const Fp2* v[6] = {&fd.c0.c0, &fd.c0.c1, &fd.c0.c2, &fd.c1.c0, &fd.c1.c1, &fd.c1.c2};
+    for (int i = 0; i < 6; ++i)
+      if (!fp2_eq(*u[i], *v[i])) return 6;
+    if (g_fd_bad) return 7;
+  }
   // k_ck_miller2: each pair in a lane of its own (its own squarings), the two values multiplied by k_ck_easy
   const Fp12 m0 = (np & 1) ? ck_miller1(p1.x, p1.y, [&](uint32_t s) { return l1[s]; }) : fp12_one();
   const Fp12 m1 = (np & 2) ? ck_miller1(fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), [&](uint32_t s) { return l2[s]; })
@@ -611,4 +629,54 @@ extern "C" int hc_xq_sum_check(const uint8_t* sigs384, const uint64_t* rho_in, u
   xq_sum4([&](uint32_t m) { return P[m]; }, rho, [&](uint32_t u) { return T[u]; },
           [&](uint32_t u, const G2A& t) { T[u] = t; }, acc);
   return jac_eq(acc, ref) ? 1 : 0;
+}
+
+// fpd.h against field.h: the digit-form Fp12 squaring and sparse line product on random elements and on the extreme one
+// (every component p - 1), bounds asserted.  Returns the number of mismatches (+1000 on a bound violation).
+extern "C" int hc_fd_check(uint64_t seed, int n) {
+  uint64_t st = seed * 0x9e3779b97f4a7c15ull + 1;
+  auto rnd = [&]() {
+    st ^= st << 13;
+    st ^= st >> 7;
+    st ^= st << 17;
+    return st;
+  };
+  auto rfp = [&](bool top) {
+    Fp a;
+    if (top) {
+      a = fp_const(FP_ONE);
+      a = fp_sub(fp_zero(), a);  // p - R mod p: a large value
+      for (int i = 0; i < 12; ++i) a.l[i] = i < 11 ? 0xffffffffu : a.l[i];
+      return fp_reduce_once(fp_reduce_once(a));
+    }
+    for (int i = 0; i < 12; ++i) a.l[i] = (uint32_t)rnd();
+    a.l[11] &= 0x0fffffffu;
+    return fp_reduce_once(fp_reduce_once(fp_reduce_once(a)));
+  };
+  int bad = 0;
+  g_fd_bad = false;
+  for (int t = 0; t < n; ++t) {
+    const bool top = t == 0;
+    Fp12 a;
+    Fp* c[12] = {&a.c0.c0.c0, &a.c0.c0.c1, &a.c0.c1.c0, &a.c0.c1.c1, &a.c0.c2.c0, &a.c0.c2.c1,
+                 &a.c1.c0.c0, &a.c1.c0.c1, &a.c1.c1.c0, &a.c1.c1.c1, &a.c1.c2.c0, &a.c1.c2.c1};
+    for (int i = 0; i < 12; ++i) *c[i] = rfp(top);
+    const Fp2 l0{rfp(top), rfp(top)}, l1{rfp(top), rfp(top)}, l4{rfp(top), rfp(top)};
+    const Fp12 s1 = fp12_sqr(a), s2 = fd12_to(fd12_sqr(fd12_from(a)));
+    const Fp12 m1 = fp12_mul_014(a, l0, l1, l4);
+    const Fp12 m2 = fd12_to(fd12_mul_014(fd12_from(a), fd2_from(l0), fd2_from(l1), fd2_from(l4)));
+    // chained: the reduced outputs of one operation as the next one's inputs
+    const Fp12 q1 = fp12_mul_014(fp12_sqr(s1), l0, l1, l4);
+    const Fp12 q2 = fd12_to(fd12_mul_014(fd12_sqr(fd12_sqr(fd12_from(a))), fd2_from(l0), fd2_from(l1), fd2_from(l4)));
+    const Fp12* x[3] = {&s1, &m1, &q1};
+    const Fp12* y[3] = {&s2, &m2, &q2};
+    for (int k = 0; k < 3; ++k) {
+      const Fp2* u[6] = {&x[k]->c0.c0, &x[k]->c0.c1, &x[k]->c0.c2, &x[k]->c1.c0, &x[k]->c1.c1, &x[k]->c1.c2};
+      const Fp2* v[6] = {&y[k]->c0.c0, &y[k]->c0.c1, &y[k]->c0.c2, &y[k]->c1.c0, &y[k]->c1.c1, &y[k]->c1.c2};
+      bool eq = true;
+      for (int i = 0; i < 6; ++i) eq = eq && fp2_eq(*u[i], *v[i]);
+      bad += !eq;
+    }
+  }
+  return bad + (g_fd_bad ? 1000 : 0);
 }

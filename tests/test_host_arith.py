@@ -309,7 +309,8 @@ def test_check_pipeline_matches_pair_check(hc):
     line tables -- also as two single-pair values multiplied, k_ck_miller2 -- the final exponentiation with in-lane
     inversions, the compressed chains and the fused next factors) equals
     final_exp_cubed(miller_loop<2>) on the host: valid and invalid (key, H, sigma) triples of the golden chain, each
-    pair dropped alone (np = 1, 2) and both."""
+    pair dropped alone (np = 1, 2) and both.  k_ck_miller's digit-form loop (fpd.h ck_miller_d) must give the same
+    Miller value with every digit-form bound holding."""
     from tests.fixtures import chain, chain_arrays
 
     c = chain()
@@ -323,6 +324,15 @@ def test_check_pipeline_matches_pair_check(hc):
         h = out.raw
         for sig, np_ in ((bytes(sigs[i]), 3), (bytes(sigs[i + 1]), 3), (bytes(sigs[i]), 1), (bytes(sigs[i]), 2)):
             assert hc.hc_ck_pipeline_check(pk, h, sig, np_) == 1, (i, np_)
+
+
+def test_digit_form_fp12_matches_field(hc):
+    """fpd.h (the Miller loop's digit form: 14 x 28-bit digits through whole Fp12 operations, fat multiples of p for
+    subtractions, one reduction per output) equals field.h's fp12_sqr and fp12_mul_014, alone and chained, on random
+    elements and on the extreme one, with the bounds asserted in every product, subtraction and reduction."""
+    hc.hc_fd_check.restype = ctypes.c_int
+    hc.hc_fd_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    assert hc.hc_fd_check(0xF0D5EED, 200) == 0
 
 
 def test_xr_quad_sum_matches_double_and_add(hc):
