@@ -1070,10 +1070,15 @@ int ck_bufs(CkBufs& b, size_t G, bool group_sums) {
 // X^z (pairing.h cyc_exp_z) times the hard part's next factor: the compressed chain (k_ck_expsq), the decompressed
 // product with the six norms inverted in the lane (k_ck_expdec), the uncompressed chain for the lanes with a zero
 // denominator (k_ck_explain over work list z, CK_EXPLAIN_LANES lanes: it is rare); out = X^z op(Y) (Y may be null)
+// DG_CK_EXPSQ2=1 (A/B): the two-lane compressed squarings in Recover's passes too (k_ck_expsq spills, k_ck_expsq2 not)
+bool ck_expsq2_always() {
+  static const bool v = env_int("DG_CK_EXPSQ2", 0) != 0;
+  return v;
+}
 int ck_expz(uint32_t z, uint32_t G, const uint32_t* gcnt, const Fp12* X, const Fp12* Y, uint32_t nfrob, uint32_t conj,
             Fp12* out, const CkBufs& b, hipStream_t st, bool latency) {
   uint32_t* zl = b.zl + (size_t)z * (G + 1);
-  if (latency)  // two lanes per check
+  if (latency || ck_expsq2_always())  // two lanes per check
     RET(launch("k_ck_expsq2", k_ck_expsq2, 2 * G, 64, st, G, gcnt, X, b.sn, b.nv, b.zero, zl));
   else
     RET(launch("k_ck_expsq", k_ck_expsq, G, 64, st, G, gcnt, X, b.sn, b.nv, b.zero, zl));
