@@ -18,7 +18,8 @@
 //     k_ck_lines2    the 68 lines of the pair (-g1, b) -> L2[s][g] (b's G2 state lives only here)
 //     k_ck_miller    f = the product of both pairs' lines at a and at -g1 (the Fp12 accumulator and one line)
 //     k_ck_easy      the easy part f2 = f1 frob^2(f1), f1 = f^-1 conj(f), with the one Fp inversion in the lane
-//     5 x [k_ck_expsq   63 compressed cyclotomic squarings (Karabina): the 6 powers, their denominators' norms
+//     5 x [k_ck_expsq2  63 compressed cyclotomic squarings (Karabina, two lanes per check): the 6 powers, their
+//                       denominators' norms
 //          k_ck_expdec  the 6 norms inverted in the lane (Montgomery's trick, one Fp inversion), decompression, the
 //                       product x^z, times the hard part's next factor  (k_ck_explain: the uncompressed chain where
 //                       a denominator is zero, same next factor)]
@@ -38,7 +39,7 @@ namespace dg {
 #ifndef DG_CK_WAVES
 #define DG_CK_WAVES 1
 #endif
-// ... of the kernels with a smaller live set (k_ck_prep, k_ck_fe1, k_ck_expsq: measured faster at 2 than at 1, their
+// ... of the kernels with a smaller live set (k_ck_prep, k_ck_fe1, k_ck_expsq2: measured faster at 2 than at 1, their
 // few spills notwithstanding; the Fp12-product kernels lost at 2)
 #ifndef DG_CK_WAVES2
 #define DG_CK_WAVES2 2
@@ -471,29 +472,11 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_L2_WAVES) k_ck_lines2(uint32_t G, con
   const G2A b = load_g2a(st[g].b);
   ck_lines(b.x, b.y, [&](uint32_t s, const CkLine& l) { l2[(size_t)s * G + g] = l; });
 }
-// the six compressed powers sn[i * G + g], their denominators' norms nv[i * G + g], zero[g]
-// (a lane with a zero denominator also appends itself to zl: zl[0] the count, zl[1..] the lanes; x = 1 -- the dead
-// checks, whose verdict k_ck_final ignores -- skips the chain: 1^z = 1, zero[g] = 2)
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const uint32_t* gcnt, const Fp12* X, CycC* sn,
-                                                              Fp* nv, uint8_t* zero, uint32_t* zl) {
-  DG_HI();
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ck_dead(g, G, gcnt)) return;
-  const Fp12 x = X[g];
-  if (fp12_is_one(x)) {  // 1^z = 1 (a check with no live member or no pair)
-    zero[g] = 2;
-    return;
-  }
-  const bool z = ck_expsq(x, [&](int i, const CycC& c, const Fp& n) {
-    sn[(size_t)i * G + g] = c;
-    nv[(size_t)i * G + g] = n;
-  });
-  zero[g] = z ? 1 : 0;
-  if (z) zl[1 + atomicAdd(zl, 1u)] = g;
-}
-// k_ck_expsq with two lanes per check (lanes 2g, 2g + 1 of a wave: ck_cyc_half, the outputs swapped by a DPP quad
-// permutation): the same sn / nv / zero / zl, half the dependent products per squaring -- the cross-round isolation's
-// checks are few and latency-bound (drand_gpu.hip run_checks(latency))
+// The six compressed powers of x^|z| (ck_expsq) sn[i * G + g], their denominators' norms nv[i * G + g], zero[g] (a
+// lane with a zero denominator also appends itself to zl: zl[0] the count, zl[1..] the lanes; x = 1 -- the dead
+// checks, whose verdict k_ck_final ignores -- skips the chain: 1^z = 1, zero[g] = 2), with two lanes per check (lanes
+// 2g, 2g + 1 of a wave: ck_cyc_half, the outputs swapped by a DPP quad permutation): half the dependent products per
+// squaring for the isolation's few checks, and no spills (the one-lane form spilled 79 VGPRs; C5 15.3 -> 15.6 k)
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq2(uint32_t G, const uint32_t* gcnt, const Fp12* X, CycC* sn,
                                                                Fp* nv, uint8_t* zero, uint32_t* zl) {
   DG_HI();
@@ -566,8 +549,6 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_ck_sub(uint32_t G, uint3
                                                                 const G2AStore* S, uint8_t* status, uint8_t* fin);
 DG_KERNEL void __launch_bounds__(64, DG_CK_L2_WAVES) k_ck_lines2(uint32_t G, const uint32_t* gcnt, const CkState* st,
                                                                  CkLine* l2);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq(uint32_t G, const uint32_t* gcnt, const Fp12* X, CycC* sn,
-                                                              Fp* nv, uint8_t* zero, uint32_t* zl);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_ck_expsq2(uint32_t G, const uint32_t* gcnt, const Fp12* X, CycC* sn,
                                                                Fp* nv, uint8_t* zero, uint32_t* zl);
 DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st, const uint8_t* good_, uint8_t* status,
@@ -666,7 +647,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expdec(uint32_t G, const 
   DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (ck_dead(g, G, gcnt) || zero[g] == 1) return;
-  Fp12 x = fp12_one();  // x = 1 (zero[g] == 2, k_ck_expsq)
+  Fp12 x = fp12_one();  // x = 1 (zero[g] == 2, k_ck_expsq2)
   if (zero[g] == 0) {
     ck_inv6([&](int i) { return nv[(size_t)i * G + g]; }, [&](int i, const Fp& v) { nv[(size_t)i * G + g] = v; });
     x = ck_expdec([&](int i, CycC& c, Fp& n) {
@@ -682,7 +663,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_expdec(uint32_t G, const 
                                                               uint32_t conj, Fp12* out);
 #endif
 // x^z by the uncompressed chain for the lanes with a zero Karabina denominator (kernels_check_e.hip)
-// over the work list zl (k_ck_expsq) with a fixed grid of CK_EXPLAIN_LANES lanes striding it; every lane exits when
+// over the work list zl (k_ck_expsq2) with a fixed grid of CK_EXPLAIN_LANES lanes striding it; every lane exits when
 // the list is done
 constexpr uint32_t CK_EXPLAIN_LANES = 4096;
 // the split G2 sums (kernels_check_e.hip): table levels, column loop, affine form.  T4: the affine table entries

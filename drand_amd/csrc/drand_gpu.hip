@@ -1067,21 +1067,14 @@ int ck_bufs(CkBufs& b, size_t G, bool group_sums) {
   }
   return 0;
 }
-// X^z (pairing.h cyc_exp_z) times the hard part's next factor: the compressed chain (k_ck_expsq), the decompressed
+// X^z (pairing.h cyc_exp_z) times the hard part's next factor: the compressed chain (k_ck_expsq2), the decompressed
 // product with the six norms inverted in the lane (k_ck_expdec), the uncompressed chain for the lanes with a zero
 // denominator (k_ck_explain over work list z, CK_EXPLAIN_LANES lanes: it is rare); out = X^z op(Y) (Y may be null)
-// DG_CK_EXPSQ2=1 (A/B): the two-lane compressed squarings in Recover's passes too (k_ck_expsq spills, k_ck_expsq2 not)
-bool ck_expsq2_always() {
-  static const bool v = env_int("DG_CK_EXPSQ2", 0) != 0;
-  return v;
-}
 int ck_expz(uint32_t z, uint32_t G, const uint32_t* gcnt, const Fp12* X, const Fp12* Y, uint32_t nfrob, uint32_t conj,
             Fp12* out, const CkBufs& b, hipStream_t st, bool latency) {
   uint32_t* zl = b.zl + (size_t)z * (G + 1);
-  if (latency || ck_expsq2_always())  // two lanes per check
-    RET(launch("k_ck_expsq2", k_ck_expsq2, 2 * G, 64, st, G, gcnt, X, b.sn, b.nv, b.zero, zl));
-  else
-    RET(launch("k_ck_expsq", k_ck_expsq, G, 64, st, G, gcnt, X, b.sn, b.nv, b.zero, zl));
+  (void)latency;  // two lanes per check everywhere (C5 15.3 -> 15.6 k: the one-lane form spilled 79 VGPRs)
+  RET(launch("k_ck_expsq2", k_ck_expsq2, 2 * G, 64, st, G, gcnt, X, b.sn, b.nv, b.zero, zl));
   RET(launch("k_ck_expdec", k_ck_expdec, G, 64, st, G, gcnt, (const CycC*)b.sn, b.nv, (const uint8_t*)b.zero, Y, nfrob,
              conj, out));
   return launch("k_ck_explain", k_ck_explain, CK_EXPLAIN_LANES, 64, st, (const uint32_t*)zl, X, Y, nfrob, conj, out);
@@ -1531,7 +1524,6 @@ int dg_init(int device) {
         {(const void*)k_ck_easy, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_easy, g1, b64, 0, q, 0u, cz, 0u, (const Fp12*)nullptr, (Fp12*)nullptr, (uint32_t*)nullptr); }},
         {(const void*)k_ck_miller2, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_miller2, g1, b64, 0, q, 0u, cz, 0u, (const CkState*)nullptr, (const CkLine*)nullptr, (const CkLine*)nullptr, (Fp12*)nullptr); }},
         {(const void*)k_xg_lines, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_lines, g1, b64, 0, q, 0u, cz, (const G2JStore*)nullptr, (CkLine*)nullptr, (CkState*)nullptr, (CkLine*)nullptr); }},
-        {(const void*)k_ck_expsq, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_expsq, g1, b64, 0, q, 0u, cz, (const Fp12*)nullptr, (CycC*)nullptr, (Fp*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr); }},
         {(const void*)k_ck_expsq2, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_expsq2, g1, b64, 0, q, 0u, cz, (const Fp12*)nullptr, (CycC*)nullptr, (Fp*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr); }},
         {(const void*)k_ck_expdec, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_expdec, g1, b64, 0, q, 0u, cz, (const CycC*)nullptr, (Fp*)nullptr, (const uint8_t*)nullptr, (const Fp12*)nullptr, 0u, 0u, (Fp12*)nullptr); }},
         {(const void*)k_ck_explain, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_explain, g1, b64, 0, q, cz, (const Fp12*)nullptr, (const Fp12*)nullptr, 0u, 0u, (Fp12*)nullptr); }},
