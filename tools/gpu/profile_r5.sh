@@ -43,7 +43,8 @@ pmc() {  # tag counters config-name config-args
   timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d $O/pmc_${cfg}_$tag -o run -- python3 $R/bench.py "$@" > $O/pmc_${cfg}_$tag.log 2>&1 || { echo "pmc $cfg $tag failed"; tail -5 $O/pmc_${cfg}_$tag.log; exit 1; }
 }
 for cfg in ${CONFIGS:-head c3 c5}; do
-  case $cfg in head) A="$HEAD --sync --steps 1 --warmup 1";; c3) A="$C3";; c5) A="$C5";; esac
+  case $cfg in head) A="$HEAD --sync --steps 1 --warmup 1";; c3) A="$C3";; c5) A="$C5";;
+    c2neg) A="$HEAD --steps 1 --warmup 1 --neg-steps 2";; esac
   pmc FETCH_SIZE FETCH_SIZE $cfg $A
   pmc WRITE_SIZE WRITE_SIZE $cfg $A
   pmc SQ_VALU "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES" $cfg $A
@@ -51,6 +52,7 @@ for cfg in ${CONFIGS:-head c3 c5}; do
   pmc GRBM "GRBM_GUI_ACTIVE GRBM_COUNT" $cfg $A
 done
 # the per-dispatch CSVs exceed what a call can bring back: summarise on the box, keep the summaries only
+cp $R/profiles/traffic.json $O/traffic.json 2>/dev/null
 python3 $R/tools/traffic.py $O $O/pmc_summary.csv $O/traffic.json > $O/traffic.log 2>&1 || { echo "summary failed"; tail -5 $O/traffic.log; exit 1; }
 rm -rf $O/pmc_*/
 fi

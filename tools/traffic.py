@@ -23,7 +23,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PLAUSIBLE_BYTES_S = 10e12  # above MI355X HBM (8 TB/s) plus on-die cache hits counted at the memory side
 
 
-def load(prof):
+acc_raw = {}
+
+
+def load(prof, raw=False):
     """{config: {kernel: {counter: mean value per dispatch}}}"""
     acc = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(list)))
     for f in glob.glob(os.path.join(prof, "pmc_*", "*counter_collection.csv")):
@@ -47,14 +50,22 @@ def load(prof):
             for c in ("FETCH_SIZE", "WRITE_SIZE"):
                 if c in cs:
                     out[cfg][k]["_n_" + c] = len(cs[c])
-    return out
+    return (out, acc) if raw else out
 
 
 def main(prof, out_csv, out_json=None):
-    m = load(prof)
+    global acc_raw
+    m, acc_raw = load(prof, raw=True)
     out = {"source": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate runs per counter (tools/gpu/profile_r2.sh, profile_r3.sh); "
                      "bytes = 2 * FETCH_SIZE + WRITE_SIZE (gfx950); head = bench.py --sync --steps 1, c3 = Recover "
                      "configs[2], c5 = adversarial Recover configs[4]", "configs": {}}
+    # configs of earlier runs that this one did not profile are kept (one call per config group fits the box limits)
+    dst = out_json or os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(dst):
+        try:
+            out["configs"].update(json.load(open(dst)).get("configs", {}))
+        except ValueError:
+            pass
     for cfg, ks in sorted(m.items()):
         sec = {}
         for k, c in sorted(ks.items()):
@@ -69,7 +80,8 @@ def main(prof, out_csv, out_json=None):
                                       "system: counter not usable for this (long, scratch-heavy) kernel" % (b / t / 1e12))
         # Recover's pairing-check pipeline (checks.h k_ck_*) as one unit, as bench.py prices it: the bytes of every
         # k_ck_* dispatch of the run over the number of per-item passes (one k_ck_round_lines per dg_recover call)
-        calls = ks.get("k_ck_round_lines", {}).get("_n_FETCH_SIZE", 0)
+        # (the real calls only: dg_init's prewarm dispatches of k_ck_round_lines read nothing)
+        calls = sum(1 for v in acc_raw.get(cfg, {}).get("k_ck_round_lines", {}).get("FETCH_SIZE", []) if v > 1024)
         if calls:
             tot = 0.0
             for k, c in ks.items():
@@ -77,8 +89,20 @@ def main(prof, out_csv, out_json=None):
                     tot += (2 * c["FETCH_SIZE"] * c["_n_FETCH_SIZE"] + c["WRITE_SIZE"] * c["_n_WRITE_SIZE"]) * 1024
             sec["k_ck_* pipeline"] = {"bytes_per_launch": tot / calls, "calls": calls,
                                       "note": "sum over every k_ck_* dispatch / dg_recover calls of the run"}
+        # the cross-round isolation of failed single-key batches (xr.h) as one unit, as bench.py's c2_negative line
+        # prices it: the bytes of every k_xq_* / k_xg_* / k_ck_* dispatch of the run over the failed batches (the
+        # k_xq_sum dispatches that read their candidates' points: FETCH_SIZE above 1 MB; a passed batch's is empty)
+        xq = acc_raw.get(cfg, {}).get("k_xq_sum", {}).get("FETCH_SIZE", [])
+        failed = sum(1 for v in xq if v > 1024)
+        if failed:
+            tot = 0.0
+            for k, c in ks.items():
+                if k.startswith(("k_xq_", "k_xg_", "k_ck_")) and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                    tot += (2 * c["FETCH_SIZE"] * c["_n_FETCH_SIZE"] + c["WRITE_SIZE"] * c["_n_WRITE_SIZE"]) * 1024
+            sec["xr pipeline"] = {"bytes_per_launch": tot / failed, "calls": failed,
+                                  "note": "sum over every k_xq_* / k_xg_* / k_ck_* dispatch / failed batches of the run"}
         out["configs"][cfg] = sec
-    json.dump(out, open(out_json or os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
+    json.dump(out, open(dst, "w"), indent=1)
     cols = sorted({c for ks in m.values() for cs in ks.values() for c in cs if not c.startswith("_")})
     with open(out_csv, "w", newline="") as f:
         w = csv.writer(f)
