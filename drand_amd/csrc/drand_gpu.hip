@@ -1340,7 +1340,7 @@ int recover_sac(uint32_t R, uint32_t k, uint32_t t, uint32_t Rn, const uint32_t*
   RET(wsT(S_RC_DEN, 6 * n, &den));
   dinv = den + 3 * n;
   RET(wsT(S_RC_A, (size_t)ngroups * Rn, &Aps));
-  RET(launch("k_rs_digits", k_rs_digits, (uint32_t)n, 64, st, R, Rn, t, nl, d_selidx, d_rst, dig));
+  RET(launch("k_rs_digits", k_rs_digits, (uint32_t)n, RS_DIG_NT, st, R, Rn, t, nl, d_selidx, d_rst, dig));
   for (uint32_t l = 0; l < 3; ++l) {
     RET(launch("k_rs_tab_den", k_rs_tab_den, (uint32_t)(3 * n), 128, st, l, R, Rn, k, t, nl, d_rst, d_sel, d_S,
                (const uint4*)T4, pinf, den));

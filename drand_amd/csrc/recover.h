@@ -403,6 +403,7 @@ DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rc_straus(uint32_t R, uin
 //   k_rs_sac       lane (share group, round): the group's joint column loop, running point in LDS
 //   k_rs_combine   per round: the sum of its group partial sums
 constexpr uint32_t RS_G = 8;  // shares per lane (default; DG_RS_G)
+constexpr uint32_t RS_DIG_NT = 256;  // k_rs_digits' workgroup: one Fr inversion per 256 coefficients
 
 // sign-aligned recoding of one share's psi digits (g2_mul_u256_psi_sac): bit c of sgn set = +T in column c
 // (c < 64; column 64 is always +), um[i] bit c = u_{i+1, c}, top = the column-64 entry, even: d0 was even (add
@@ -458,18 +459,81 @@ DGI bool rs_level(uint32_t l, uint32_t e, uint32_t& src, uint32_t& pb, uint32_t&
 }
 
 #if defined(__HIP__) && DG_TU_LIB
-// lane g < t * Rn: share j = g / Rn of divergent round u = g % Rn (round nl[u]); lambda_j of the round's own
-// selected set, its psi digits and their sign-aligned recoding, dig[g]
-DG_KERNEL void __launch_bounds__(64) k_rs_digits(uint32_t R, uint32_t Rn, uint32_t t, const uint32_t* nl,
-                                                 const uint32_t* selidx, const uint8_t* rst, RsDigits* dig) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= t * Rn) return;
-  const uint32_t j = g / Rn, r = nl[g % Rn];
-  if (r >= R || rst[r] != DG_ST_OK_) return;
-  const Fr lam = lagrange_at_zero(selidx + (size_t)r * t, t, j);
+// 1 / v for the NT threads of a workgroup by Montgomery's trick: per wave the inclusive prefix and suffix products
+// (shuffle scans, 12 Fr products a lane), the wave totals inverted together by thread 0 (ONE Fr inversion per
+// workgroup instead of one per lane: a lane's inversion is ~300 products and a wave pays it whether 1 or 64 lanes
+// need it), then 1 / v_i = (prod_{k < i} v_k)(prod_{k > i} v_k) / total_w.  v != 0; every thread calls it.
+template <uint32_t NT>
+DGI Fr fr_inv_block(const Fr& v) {
+  constexpr uint32_t NW = NT / 64;
+  __shared__ Fr s_w[NW];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  Fr pre = v, suf = v;
+#pragma unroll 1
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    Fr a, b;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a.l[i] = __shfl_up(pre.l[i], d, 64);
+      b.l[i] = __shfl_down(suf.l[i], d, 64);
+    }
+    if (lane >= d) pre = fr_mul_in(pre, a);
+    if (lane + d < 64) suf = fr_mul_in(suf, b);
+  }
+  Fr ep, es;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    ep.l[i] = __shfl_up(pre.l[i], 1, 64);
+    es.l[i] = __shfl_down(suf.l[i], 1, 64);
+  }
+  if (lane == 0) ep = fr_const(FR_ONE);
+  if (lane == 63) {
+    es = fr_const(FR_ONE);
+    s_w[w] = pre;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Fr p[NW], acc = fr_const(FR_ONE);
+#pragma unroll
+    for (uint32_t k = 0; k < NW; ++k) {
+      p[k] = acc;
+      acc = fr_mul_in(acc, s_w[k]);
+    }
+    Fr inv = fr_inv_in(acc);
+#pragma unroll
+    for (uint32_t k = NW; k-- > 0;) {
+      const Fr tw = s_w[k];
+      s_w[k] = fr_mul_in(inv, p[k]);
+      inv = fr_mul_in(inv, tw);
+    }
+  }
+  __syncthreads();
+  return fr_mul_in(fr_mul_in(ep, es), s_w[w]);
+}
+
+// lane g < t * Rn: share j = g % t of divergent round u = g / t (round nl[u]; a wave reads one or two rounds' index
+// rows); lambda_j of the round's own selected set (lagrange_nd, the workgroup's shared inversion), its psi digits
+// and their sign-aligned recoding, dig[j * Rn + u]
+DG_KERNEL void __launch_bounds__(RS_DIG_NT) k_rs_digits(uint32_t R, uint32_t Rn, uint32_t t, const uint32_t* nl,
+                                                        const uint32_t* selidx, const uint8_t* rst, RsDigits* dig) {
+  const uint32_t g = blockIdx.x * RS_DIG_NT + threadIdx.x;
+  const uint32_t u = g / t, j = g % t;
+  const uint32_t r = g < t * Rn ? nl[u] : R;
+  const bool live = r < R && rst[r] == DG_ST_OK_;
+  Fr num, den = fr_const(FR_ONE);
+  if (live) lagrange_nd(selidx + (size_t)r * t, t, j, num, den);
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) nz |= den.l[i];
+  const Fr dinv = fr_inv_block<RS_DIG_NT>(nz ? den : fr_const(FR_ONE));  // 0 (repeated index): lambda 0, as fr_inv
+  if (!live) return;
+  Fr lam = lagrange_finish(num, dinv);
+  if (!nz)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lam.l[i] = 0;
   uint64_t d[4];
   rc_psi_digits(lam, d);
-  dig[g] = rs_recode(d);
+  dig[(size_t)j * Rn + u] = rs_recode(d);
 }
 
 // per divergent round u: sigma = the sum of its ngroups group partial sums (Aps[q * Rn + u]) into out[r]

@@ -342,6 +342,19 @@ extern "C" int hc_g2_mul_lds_check(const uint8_t* sig96, const uint32_t* k8) {
   return jac_eq(acc, g2_mul_u256_psi(a, k8)) ? 1 : 0;
 }
 
+// fr.h lagrange_at_zero (64-bit plain chunks of the factors, quarter products) against rc_lambdas (one full
+// Montgomery product per factor, one inversion for all t) for t distinct indices < 2^32 - 1.  1 if all equal.
+extern "C" int hc_lagrange_check(const uint32_t* idx, uint32_t t) {
+  std::vector<Fr> lam(t), pre(t);
+  rc_lambdas(idx, t, lam.data(), pre.data());
+  for (uint32_t j = 0; j < t; ++j) {
+    const Fr l = lagrange_at_zero(idx, t, j);
+    for (int w = 0; w < 8; ++w)
+      if (l.l[w] != lam[j].l[w]) return 0;
+  }
+  return 1;
+}
+
 // Recover's per-round MSM (recover.h) on the host: lambdas with one Fr inversion (rc_lambdas) against
 // lagrange_at_zero, the odd-multiple tables by the device's affine formulas (g2_aff_den / g2_aff_sum with exact
 // inverses), the four wNAF schedules and the psi combination, against sum_j g2_mul_u256_psi(S_j, lambda_j).

@@ -263,6 +263,21 @@ def test_wnaf_digits_host_build(hc):
         assert hc.hc_wnaf_check(ctypes.c_uint64(d)) == 1, hex(d)
 
 
+def test_lagrange_chunked_products(hc):
+    """fr.h lagrange_at_zero (the factors x_m and |x_m - x_j| multiplied in plain 64-bit chunks, one quarter
+    Montgomery product per chunk pair, den's sign by parity) equals rc_lambdas' one-product-per-factor form: small
+    and consecutive indices (many factors per chunk), indices near 2^32 (one factor per chunk, the chunk boundary
+    at every step) and mixtures of both, unsorted."""
+    rng = random.Random(29)
+    top = (1 << 32) - 2
+    sets = [[0], [5], list(range(129)), sorted(rng.sample(range(256), 129)), [top - i for i in range(40)],
+            rng.sample(range(top), 64), [0, top, 1, top - 1, 7, 1 << 31, (1 << 31) + 1, 65535, 65536],
+            rng.sample(list(range(200)) + [top - i * 977 for i in range(100)], 150)]
+    for idx in sets:
+        t = len(idx)
+        assert hc.hc_lagrange_check((ctypes.c_uint32 * t)(*idx), t) == 1, idx[:8]
+
+
 @pytest.mark.parametrize("t,seed", [(1, 0), (3, 1), (33, 2), (33, 3), (12, 4), (33, -1), (70, -1)])
 def test_recover_msm_host_build(hc, t, seed):
     """recover.h on the host: one Straus MSM per round over the t selected shares (lambdas with one Fr inversion,
