@@ -112,6 +112,9 @@ struct Ctx {
   // for every wave the device can hold, so the workspace queues stay at the check pipeline's ~4 KB (12 workspace
   // queues at 5.7 KB each failed dg_init with HSA_STATUS_ERROR_OUT_OF_RESOURCES)
   hipStream_t fb_stream = nullptr;
+  // the keyed batches' side stream (k_key_combine beside the keyed MSM; the multi-key entry points are blocking)
+  hipStream_t kc_stream = nullptr;
+  hipEvent_t kc_fork = nullptr, kc_join = nullptr;
   static constexpr int kTails = 4;
   hipStream_t tails[kTails] = {};  // high-priority streams, set i -> tails[i % ntails] (DG_TAIL=0: none)
   int ntails = 0;
@@ -693,10 +696,23 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
     T = msm;
     K = msm + 1;
   } else {
+    // Xc = sum_s beta_s X_s (k_key_combine: one workgroup, ~2 ms of dependent doublings) on the side stream, joined
+    // before the Miller launch: it needs only the bound seed and the keys, so it runs beside the MSMs below
+    RET(wsT(S_XC, 1, &Xc));
+    Ctx& c = g_ctx;
+    if (!c.kc_stream) {
+      HIPCHK(hipStreamCreateWithFlags(&c.kc_stream, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&c.kc_fork, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&c.kc_join, hipEventDisableTiming));
+    }
+    HIPCHK(hipEventRecord(c.kc_fork, st));
+    HIPCHK(hipStreamWaitEvent(c.kc_stream, c.kc_fork, 0));
+    RET(launch("k_key_combine", k_key_combine, 256, 256, c.kc_stream, b.nslots, seed, b.keys, b.key_status, Xc));
+    HIPCHK(hipEventRecord(c.kc_join, c.kc_stream));
     // T = sum_s beta_s sum_{i in s} alpha_{r(i)} S_i by the keyed MSM (no per-item scalar multiplication)
     RET(msm_run_keyed(b, seed, iso, batched_sub != 0, &msm, &win, st));
     T = msm;
-    uint32_t nchunks = 16384 / b.nslots;
+    uint32_t nchunks = 65536 / b.nslots;  // 1024 waves (16384 lanes: C5's 157-round chains, 8.5 ms)
     if (nchunks < 1) nchunks = 1;
     if (nchunks > b.R) nchunks = b.R;
     uint32_t chunk = (b.R + nchunks - 1) / nchunks;
@@ -707,12 +723,11 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
                (const uint32_t*)cell, (const uint8_t*)active, (const G2JStore*)A, Kp));
     RET(reduce_rows(Kp, tmp, b.nslots, nchunks, st));  // -C_s = Kp[s]
     K = Kp;
-    // Kc = sum over the active rounds of alpha_r Q_r (one MSM), Xc = sum_s beta_s X_s
+    // Kc = sum over the active rounds of alpha_r Q_r (one MSM)
     G2JStore* kmsm;
     RET(msm_run(b.R, seed, active, b.Q, nullptr, false, true, &kmsm, nullptr, st, flag + 2));
     Kc = kmsm;
-    RET(wsT(S_XC, 1, &Xc));
-    RET(launch("k_key_combine", k_key_combine, 256, 256, st, b.nslots, seed, b.keys, b.key_status, Xc));
+    HIPCHK(hipStreamWaitEvent(st, c.kc_join, 0));
   }
   const uint32_t npairs = b.nslots + (b.nslots > 1 ? 2u : 1u);
   // the batched subgroup check's window sums ride in the Miller launch (extra workgroups); k_final_coop folds
@@ -1600,6 +1615,14 @@ void dg_shutdown(void) {
     (void)hipStreamSynchronize(g_ctx.fb_stream);
     (void)hipStreamDestroy(g_ctx.fb_stream);
     g_ctx.fb_stream = nullptr;
+  }
+  if (g_ctx.kc_stream) {
+    (void)hipStreamSynchronize(g_ctx.kc_stream);
+    (void)hipStreamDestroy(g_ctx.kc_stream);
+    (void)hipEventDestroy(g_ctx.kc_fork);
+    (void)hipEventDestroy(g_ctx.kc_join);
+    g_ctx.kc_stream = nullptr;
+    g_ctx.kc_fork = g_ctx.kc_join = nullptr;
   }
   if (g_ctx.pk_dev) (void)hipFree(g_ctx.pk_dev);
   if (g_ctx.pk_status) (void)hipFree(g_ctx.pk_status);

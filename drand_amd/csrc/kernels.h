@@ -308,13 +308,9 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_key_accum(uint32_t R, uint
     if (active[r] && !cell[(size_t)r * nslots + s]) g2_add_lds(acc, load_g2j(A[r]));
   store_g2j(Kp[g], jac_neg(load_g2j(acc)));
 }
-#elif defined(__HIP__)
-DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_key_accum(uint32_t R, uint32_t nslots, uint32_t chunk, uint32_t nchunks,
-                                                  const uint32_t* cell, const uint8_t* active, const G2JStore* A,
-                                                  G2JStore* Kp);
-#endif
-#if DG_TU_LIB
-// Xc = sum_s beta_s X_s over the key slots with a decoded key: per-lane 64-bit products, LDS tree sum
+// Xc = sum_s beta_s X_s over the key slots with a decoded key: per-lane 64-bit products, LDS tree sum.  One workgroup
+// whose ~2 ms are latency (64 dependent doublings per lane, one wave per SIMD; inline products did not change it):
+// batch_verify runs it on a side stream beside the keyed MSM, off the batch's critical path.
 DG_KERNEL void __launch_bounds__(256) k_key_combine(uint32_t nslots, const uint64_t* seedp, const G1AStore* keys,
                                                    const uint8_t* key_status, G1AStore* out) {
   const uint64_t seed = *seedp;
@@ -334,6 +330,12 @@ DG_KERNEL void __launch_bounds__(256) k_key_combine(uint32_t nslots, const uint6
   }
   if (t == 0) store_g1a(out[0], g1_to_aff(part[0]));
 }
+#elif defined(__HIP__)
+DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_key_accum(uint32_t R, uint32_t nslots, uint32_t chunk, uint32_t nchunks,
+                                                  const uint32_t* cell, const uint8_t* active, const G2JStore* A,
+                                                  G2JStore* Kp);
+DG_KERNEL void __launch_bounds__(256) k_key_combine(uint32_t nslots, const uint64_t* seedp, const G1AStore* keys,
+                                                   const uint8_t* key_status, G1AStore* out);
 #endif
 
 
