@@ -205,7 +205,10 @@ enum Slot {
   S_SEED2, S_SB, S_STB, S_ISOB, S_KMSM_GOFS, S_KMSM_BP, S_KMSM_BT2,
   S_CK_RL, S_CK_HINF, S_CK_ST, S_CK_L2, S_CK_F, S_CK_T0, S_CK_T1, S_CK_F2, S_CK_A, S_CK_NV, S_CK_SN, S_CK_ZERO,
   S_CK_ZL, S_CK_GOOD, S_CK_T4, S_CK_TINF, S_CK_DIG, S_CK_TDEN, S_CK_BJ, S_CK_BN, S_CK_G2M, S_KOK, S_XR_CNT, S_XR_CAND,
-  S_XR_QS, S_XR_T4, S_XR_TINF, S_XR_L2, S_XR_L3, S_XR_HS, S_XR_RL, S_COUNT
+  S_XR_QS, S_XR_T4, S_XR_TINF, S_XR_L2, S_XR_L3, S_XR_HS, S_XR_RL,
+  // msm_run / batch_inv on the keyed batches' side stream (alt): the same buffers, apart from the main stream's
+  S_MSM2_CNT, S_MSM2_LIST, S_MSM2_CHUNKS, S_MSM2_AFF, S_MSM2_DEN, S_MSM2_DINV, S_MSM2_B, S_MSM2_G, S_MSM2_P1, S_MSM2_W,
+  S_MSM2_OUT, S_BINV2_PRE, S_BINV2_ROOTS, S_BINV2, S_COUNT
 };
 
 Set& cur_set() { return g_ctx.sets[g_ctx.cur]; }
@@ -455,7 +458,7 @@ int bind_seed(const Batch& b, uint64_t seed, hipStream_t st, uint64_t** d_seed, 
 // Pippenger MSM (msm.h): out[0] = sum_r alpha_r PA_r, out[1] = sum_r alpha_r PB_r (PB may be null),
 // over the rounds with active[r] != 0.  With `test_windows` side A also gets the MSM_TWIN test windows of
 // the batched subgroup check; *win = its MSM_WT window sums (checked beside the Miller loops, k_pair_miller_coop).
-int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st);
+int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st, bool alt = false);
 
 // the per-item passes after a batch equation (defined with the check pipeline below)
 constexpr uint32_t kXrSeg = 131072;  // items per cross-round isolation run at most (bounded per-check workspace)
@@ -469,13 +472,16 @@ int prefix_pass(uint32_t R, uint32_t k, uint32_t t, int passes, const uint64_t* 
 // `bad` (device, affine only): raised when an input breaks that precondition (msm.h aff_input_ok); the caller
 // passes its batch-failure flag, so such a batch falls back to exact per-item checks.
 int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JStore* PA, const G2JStore* PB, bool test_windows,
-            bool affine, G2JStore** out, G2JStore** win, hipStream_t st, uint32_t* bad = nullptr, hipStream_t tst = nullptr) {
+            bool affine, G2JStore** out, G2JStore** win, hipStream_t st, uint32_t* bad = nullptr, hipStream_t tst = nullptr,
+            bool alt = false) {
   const uint32_t nsides = PB ? 2 : 1, nwin = test_windows ? MSM_WT : MSM_WIN, nbk = nwin * MSM_NB;
+  // alt: the side stream's copies of every buffer (it runs beside the keyed MSM, batch_verify)
+  auto SL = [alt](Slot a, Slot b) { return alt ? b : a; };
   uint32_t *cnt, *list;
   G2JStore *chunks, *BP, *tmp, *P1, *W;
-  RET(wsT(S_MSM_CNT, 4 * nbk + 1 + MSM_AFF_L * (nbk + 1), &cnt));
+  RET(wsT(SL(S_MSM_CNT, S_MSM2_CNT), 4 * nbk + 1 + MSM_AFF_L * (nbk + 1), &cnt));
   uint32_t *offset = cnt + nbk, *cursor = offset + nbk, *chunk_off = cursor + nbk;
-  RET(wsT(S_MSM_LIST, (size_t)nwin * R + 1, &list));
+  RET(wsT(SL(S_MSM_LIST, S_MSM2_LIST), (size_t)nwin * R + 1, &list));
   if (affine && !bad) return fail(DG_E_ARG, "msm_run: the affine levels need a failure flag");
   if (affine) {
     const size_t E = (size_t)nwin * R;
@@ -484,14 +490,14 @@ int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JSt
     G2AStore* A;
     Fp *den, *dinv;
     const uint32_t maxg0 = (uint32_t)(E / 2) + nbk;
-    RET(wsT(S_MSM_AFF, E * nsides, &A));
-    RET(wsT(S_MSM_DEN, (size_t)maxg0 * nsides, &den));
-    RET(wsT(S_MSM_DINV, (size_t)maxg0 * nsides, &dinv));
-    RET(wsT(S_MSM_B, (size_t)nbk * MSM_BSPLIT * nsides, &BP));
-    RET(wsT(S_MSM_G, (size_t)nbk * MSM_BSPLIT * nsides, &tmp));
-    RET(wsT(S_MSM_P1, (size_t)nwin * MSM_C * MSM_SLICE_LANES * nsides, &P1));
-    RET(wsT(S_MSM_W, (size_t)nwin * nsides, &W));
-    RET(wsT(S_MSM_OUT, 2, out));
+    RET(wsT(SL(S_MSM_AFF, S_MSM2_AFF), E * nsides, &A));
+    RET(wsT(SL(S_MSM_DEN, S_MSM2_DEN), (size_t)maxg0 * nsides, &den));
+    RET(wsT(SL(S_MSM_DINV, S_MSM2_DINV), (size_t)maxg0 * nsides, &dinv));
+    RET(wsT(SL(S_MSM_B, S_MSM2_B), (size_t)nbk * MSM_BSPLIT * nsides, &BP));
+    RET(wsT(SL(S_MSM_G, S_MSM2_G), (size_t)nbk * MSM_BSPLIT * nsides, &tmp));
+    RET(wsT(SL(S_MSM_P1, S_MSM2_P1), (size_t)nwin * MSM_C * MSM_SLICE_LANES * nsides, &P1));
+    RET(wsT(SL(S_MSM_W, S_MSM2_W), (size_t)nwin * nsides, &W));
+    RET(wsT(SL(S_MSM_OUT, S_MSM2_OUT), 2, out));
     HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * nbk, st));
     RET(launch("k_msm_count", k_msm_count, R, 256, st, R, nwin, seed, active, cnt));
     RET(launch("k_msm_scan_aff", k_msm_scan_aff, 256, 256, st, nbk, (const uint32_t*)cnt, offset, cursor, gofs));
@@ -501,7 +507,7 @@ int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JSt
       const uint32_t* gl = gofs + l * (nbk + 1);
       RET(launch("k_msm_aff_den", k_msm_aff_den, n, 128, st, l, maxg, nsides, nbk, (const uint32_t*)cnt,
                  (const uint32_t*)offset, gl, (const uint32_t*)list, PA, PB, (const G2AStore*)A, (uint32_t)E, den));
-      RET(batch_inv(n, den, dinv, st));
+      RET(batch_inv(n, den, dinv, st, alt));
       RET(launch("k_msm_aff_add", k_msm_aff_add, n, 128, st, l, maxg, nsides, nbk, (const uint32_t*)cnt,
                  (const uint32_t*)offset, gl, (const uint32_t*)list, PA, PB, A, (uint32_t)E, (const Fp*)dinv, bad));
     }
@@ -512,12 +518,12 @@ int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JSt
   const size_t max_chunks_sz = ((size_t)nwin * R) / MSM_CHUNK + nbk;
   if (max_chunks_sz * nsides > 0xffffffffull) return fail(DG_E_ARG, "batch too large for the MSM");
   const uint32_t max_chunks = (uint32_t)max_chunks_sz;
-  RET(wsT(S_MSM_CHUNKS, (size_t)max_chunks * nsides, &chunks));
-  RET(wsT(S_MSM_B, (size_t)nbk * MSM_BSPLIT * nsides, &BP));
-  RET(wsT(S_MSM_G, (size_t)nbk * MSM_BSPLIT * nsides, &tmp));
-  RET(wsT(S_MSM_P1, (size_t)nwin * MSM_C * MSM_SLICE_LANES * nsides, &P1));
-  RET(wsT(S_MSM_W, (size_t)nwin * nsides, &W));
-  RET(wsT(S_MSM_OUT, 2, out));
+  RET(wsT(SL(S_MSM_CHUNKS, S_MSM2_CHUNKS), (size_t)max_chunks * nsides, &chunks));
+  RET(wsT(SL(S_MSM_B, S_MSM2_B), (size_t)nbk * MSM_BSPLIT * nsides, &BP));
+  RET(wsT(SL(S_MSM_G, S_MSM2_G), (size_t)nbk * MSM_BSPLIT * nsides, &tmp));
+  RET(wsT(SL(S_MSM_P1, S_MSM2_P1), (size_t)nwin * MSM_C * MSM_SLICE_LANES * nsides, &P1));
+  RET(wsT(SL(S_MSM_W, S_MSM2_W), (size_t)nwin * nsides, &W));
+  RET(wsT(SL(S_MSM_OUT, S_MSM2_OUT), 2, out));
   HIPCHK(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * nbk, st));
   RET(launch("k_msm_count", k_msm_count, R, 256, st, R, nwin, seed, active, cnt));
   RET(launch("k_msm_scan", k_msm_scan, 256, 256, st, nbk, (const uint32_t*)cnt, offset, cursor, chunk_off));
@@ -696,8 +702,9 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
     T = msm;
     K = msm + 1;
   } else {
-    // Xc = sum_s beta_s X_s (k_key_combine: one workgroup, ~2 ms of dependent doublings) on the side stream, joined
-    // before the Miller launch: it needs only the bound seed and the keys, so it runs beside the MSMs below
+    // Xc = sum_s beta_s X_s (k_key_combine: one workgroup, ~2 ms of dependent doublings) and Kc on the side stream,
+    // joined before the Miller launch: they need only the bound seed, the keys, the hashes and `active`, so they run
+    // beside the keyed MSM below
     RET(wsT(S_XC, 1, &Xc));
     Ctx& c = g_ctx;
     if (!c.kc_stream) {
@@ -708,6 +715,11 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
     HIPCHK(hipEventRecord(c.kc_fork, st));
     HIPCHK(hipStreamWaitEvent(c.kc_stream, c.kc_fork, 0));
     RET(launch("k_key_combine", k_key_combine, 256, 256, c.kc_stream, b.nslots, seed, b.keys, b.key_status, Xc));
+    // Kc = sum over the active rounds of alpha_r Q_r (one MSM, a ~3.4 ms chain of small launches at 100k rounds): on
+    // the side stream too, in its own buffers
+    G2JStore* kmsm;
+    RET(msm_run(b.R, seed, active, b.Q, nullptr, false, true, &kmsm, nullptr, c.kc_stream, flag + 2, nullptr, true));
+    Kc = kmsm;
     HIPCHK(hipEventRecord(c.kc_join, c.kc_stream));
     // T = sum_s beta_s sum_{i in s} alpha_{r(i)} S_i by the keyed MSM (no per-item scalar multiplication)
     RET(msm_run_keyed(b, seed, iso, batched_sub != 0, &msm, &win, st));
@@ -723,10 +735,6 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
                (const uint32_t*)cell, (const uint8_t*)active, (const G2JStore*)A, Kp));
     RET(reduce_rows(Kp, tmp, b.nslots, nchunks, st));  // -C_s = Kp[s]
     K = Kp;
-    // Kc = sum over the active rounds of alpha_r Q_r (one MSM)
-    G2JStore* kmsm;
-    RET(msm_run(b.R, seed, active, b.Q, nullptr, false, true, &kmsm, nullptr, st, flag + 2));
-    Kc = kmsm;
     HIPCHK(hipStreamWaitEvent(st, c.kc_join, 0));
   }
   const uint32_t npairs = b.nslots + (b.nslots > 1 ? 2u : 1u);
@@ -809,20 +817,20 @@ int decode_key(const uint8_t* pk48_host, hipStream_t st, G1AStore** keys, uint8_
 // out[i] = 1 / vals[i] (0 for 0) for n Fp values on the device: Montgomery's trick over chunks of BINV_C, a tree of
 // chunk products, one safegcd inversion at the root (phases.h k_binv_*)
 int batch_inv_chunked(uint32_t n, const Fp* vals, Fp* out, hipStream_t st, Slot slot);
-int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st) {
+int batch_inv(uint32_t n, const Fp* vals, Fp* out, hipStream_t st, bool alt) {
   constexpr uint32_t PER = BINV_T * BINV_K;
   if (n <= BINV_T * BINV_R) return launch("k_binv_blk_root", k_binv_blk_root, BINV_T, BINV_T, st, n, vals, out);
   // block tree (phases.h k_binv_blk_*): per block of PER values a root; the roots by the chunked form
   const uint32_t nb = (n + PER - 1) / PER;
   Fp *pre, *roots, *rinv;
-  RET(wsT(S_BINV_PRE, n, &pre));
-  RET(wsT(S_BINV_ROOTS, 2 * (size_t)nb, &roots));
+  RET(wsT(alt ? S_BINV2_PRE : S_BINV_PRE, n, &pre));
+  RET(wsT(alt ? S_BINV2_ROOTS : S_BINV_ROOTS, 2 * (size_t)nb, &roots));
   rinv = roots + nb;
   RET(launch("k_binv_blk_up", k_binv_blk_up, nb * BINV_T, BINV_T, st, n, vals, pre, roots));
   if (nb <= BINV_T * BINV_R)
     RET(launch("k_binv_blk_root", k_binv_blk_root, BINV_T, BINV_T, st, nb, (const Fp*)roots, rinv));
   else
-    RET(batch_inv_chunked(nb, roots, rinv, st, S_BINV));  // n > 2M values (its own slot: no reentry)
+    RET(batch_inv_chunked(nb, roots, rinv, st, alt ? S_BINV2 : S_BINV));  // n > 2M values (its own slot: no reentry)
   return launch("k_binv_blk_down", k_binv_blk_down, nb * BINV_T, BINV_T, st, n, vals, (const Fp*)pre, (const Fp*)rinv,
                 out);
 }
