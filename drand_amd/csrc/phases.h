@@ -43,7 +43,10 @@ struct DecState {
 };
 constexpr uint32_t DEC_PENDING = 1, DEC_SIGN = 2, DEC_INF = 4;
 constexpr uint32_t BINV_C = 32;  // chunk of the batch inversion (k_binv_*)
-constexpr uint32_t BINV_T = 256, BINV_K = 4;  // block-tree batch inversion (k_binv_blk_*): lanes x values per lane
+#ifndef DG_BINV_K
+#define DG_BINV_K 8  // 4: C3 816 / 814 k against 826 / 820 k at 8 (one root launch up to 4.2 M values), headline equal
+#endif
+constexpr uint32_t BINV_T = 256, BINV_K = DG_BINV_K;  // block-tree batch inversion (k_binv_blk_*): lanes x values per lane
 constexpr uint32_t BINV_R = 8;                // values per lane of the single-workgroup root inversion
 
 // ------------------------------------------------------------------------------ exponentiation
@@ -443,7 +446,7 @@ DG_KERNEL void __launch_bounds__(64) k_binv_root(uint32_t n, const Fp* vals, Fp*
 
 // ---- the same batch inversion as a block tree: a workgroup of BINV_T lanes takes BINV_T * BINV_K consecutive
 // values (BINV_K per lane: running products in `pre`, the last one is the lane's leaf), multiplies the leaves up a
-// binary tree in LDS and writes the root; the roots are inverted by the chunked form above (n / 1024 values); the
+// binary tree in LDS and writes the root; the roots are inverted by the chunked form above (n / (BINV_T BINV_K) values); the
 // down kernel rebuilds the tree, sends each node's inverse to its children (inv(left) = inv(node) * right) and
 // walks each lane's values back.  Per value ~3 products, every lane busy: the chunked form left n / 32 lanes
 // with 32 dependent products each (k_binv_down 113 us per 200k values, one pass per level).
