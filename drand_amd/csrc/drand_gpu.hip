@@ -112,12 +112,18 @@ struct Ctx {
   // for every wave the device can hold, so the workspace queues stay at the check pipeline's ~4 KB (12 workspace
   // queues at 5.7 KB each failed dg_init with HSA_STATUS_ERROR_OUT_OF_RESOURCES)
   hipStream_t fb_stream = nullptr;
-  // the keyed batches' side stream (k_key_combine beside the keyed MSM; the multi-key entry points are blocking)
+  // the keyed batches' side stream (k_key_combine and Kc beside the keyed MSM; dg_init): the multi-key entry points
+  // block until their batch is done, which the shared fork / join events rely on
   hipStream_t kc_stream = nullptr;
   hipEvent_t kc_fork = nullptr, kc_join = nullptr;
   static constexpr int kTails = 4;
   hipStream_t tails[kTails] = {};  // high-priority streams, set i -> tails[i % ntails] (DG_TAIL=0: none)
   int ntails = 0;
+  // the cross-round isolation's workspace (xr.h: ~0.8 GB at its capacity) per TAIL stream, not per set: the sets that
+  // share a tail stream run their isolations one after another in that stream's order, so they can share its buffers
+  // (4 copies instead of one per set).  xr_pool >= 0 while xr_isolate allocates (ws() takes that pool).
+  Set xr_pools[kTails];
+  int xr_pool = -1;
   hipStream_t last_stream = nullptr;  // the set stream of the last asynchronous batch (dg_last_batch_stream)
   int cur = 0, next = 0;
   bool timing = false;
@@ -205,7 +211,7 @@ enum Slot {
   S_SEED2, S_SB, S_STB, S_ISOB, S_KMSM_GOFS, S_KMSM_BP, S_KMSM_BT2,
   S_CK_RL, S_CK_HINF, S_CK_ST, S_CK_L2, S_CK_F, S_CK_T0, S_CK_T1, S_CK_F2, S_CK_A, S_CK_NV, S_CK_SN, S_CK_ZERO,
   S_CK_ZL, S_CK_GOOD, S_CK_T4, S_CK_TINF, S_CK_DIG, S_CK_TDEN, S_CK_BJ, S_CK_BN, S_CK_G2M, S_KOK, S_XR_CNT, S_XR_CAND,
-  S_XR_QS, S_XR_T4, S_XR_TINF, S_XR_L2, S_XR_L3, S_XR_HS, S_XR_RL,
+  S_XR_QS, S_XR_T4, S_XR_TINF, S_XR_L3, S_XR_HS, S_XR_RL,
   // msm_run / batch_inv on the keyed batches' side stream (alt): the same buffers, apart from the main stream's
   S_MSM2_CNT, S_MSM2_LIST, S_MSM2_CHUNKS, S_MSM2_AFF, S_MSM2_DEN, S_MSM2_DINV, S_MSM2_B, S_MSM2_G, S_MSM2_P1, S_MSM2_W,
   S_MSM2_OUT, S_BINV2_PRE, S_BINV2_ROOTS, S_BINV2, S_COUNT
@@ -225,14 +231,21 @@ inline double hp_now_us() {
 }
 
 int ws(Slot s, size_t bytes, void** out) {
-  Set& c = cur_set();
+  Set& c = g_ctx.xr_pool >= 0 ? g_ctx.xr_pools[g_ctx.xr_pool] : cur_set();
   if (c.pool.size() < S_COUNT) {
     c.pool.assign(S_COUNT, nullptr);
     c.pool_size.assign(S_COUNT, 0);
   }
   if (bytes == 0) bytes = 16;
   if (c.pool_size[s] < bytes) {
-    if (c.pool[s]) HIPCHK(hipFree(c.pool[s]));
+    // A slot grows while kernels enqueued earlier may still read it: this batch's own earlier launches (batch_inv
+    // takes the same slots at several sizes), or, for a tail pool, another set's isolation.  The old buffer is freed
+    // only after the device is idle, whatever hipFree itself waits for.  Slots only grow, so this happens in the first
+    // batches of a size and never in the steady state.
+    if (c.pool[s]) {
+      HIPCHK(hipDeviceSynchronize());
+      HIPCHK(hipFree(c.pool[s]));
+    }
     c.pool[s] = nullptr;
     size_t sz = bytes + bytes / 4;
     HIPCHK(hipMalloc(&c.pool[s], sz));
@@ -707,11 +720,8 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
     // beside the keyed MSM below
     RET(wsT(S_XC, 1, &Xc));
     Ctx& c = g_ctx;
-    if (!c.kc_stream) {
-      HIPCHK(hipStreamCreateWithFlags(&c.kc_stream, hipStreamNonBlocking));
-      HIPCHK(hipEventCreateWithFlags(&c.kc_fork, hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&c.kc_join, hipEventDisableTiming));
-    }
+    // kc_fork / kc_join are global while the S_MSM2_* / S_BINV2_* buffers belong to the set: safe only because every
+    // multi-key entry point blocks until its batch is done (one keyed batch in flight at a time)
     HIPCHK(hipEventRecord(c.kc_fork, st));
     HIPCHK(hipStreamWaitEvent(c.kc_stream, c.kc_fork, 0));
     RET(launch("k_key_combine", k_key_combine, 256, 256, c.kc_stream, b.nslots, seed, b.keys, b.key_status, Xc));
@@ -758,6 +768,11 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
   if (b.nslots == 1 && b.k == 1 && !b.item_slot) {
     // one key, one item per round (VerifyBeacon / VerifyRecovered): a failed batch isolates its bad rounds by group
     // tests across rounds (xr.h), enqueued whole and decided on the device, so asynchronous batches stay asynchronous
+    // (on a tail stream: the workspace of that stream, shared by the sets it serves)
+    struct PoolGuard {
+      explicit PoolGuard(int p) { g_ctx.xr_pool = p; }
+      ~PoolGuard() { g_ctx.xr_pool = -1; }
+    } guard(tst && g_ctx.ntails ? g_ctx.cur % g_ctx.ntails : -1);
     for (uint32_t i0 = 0; i0 < N; i0 += kXrSeg)
       RET(xr_isolate(i0, std::min(kXrSeg, N - i0), flag, seed, b.keys, b.Q, b.S, b.status, st));
   } else {
@@ -1156,51 +1171,57 @@ int check_chunk(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k, uin
 }
 
 // Cross-round isolation of a failed single-key batch (xr.h): items [i0, i0 + n) of the batch (its status, decoded S,
-// uncleared hashes Q, the group key keys[0]), levels of group tests on the device, no host round trip; after a passed
-// batch every launch returns at once.  At most kXrSeg items per run, so the per-check workspace stays bounded.
-uint32_t xr_qpg() {
+// uncleared hashes Q, the group key keys[0]), two levels of group tests on the device, no host round trip; after a
+// passed batch every launch returns at once.  At most kXrSeg items per run, and the single checks of level 3 in chunks
+// of at most kXrL3Cap, each gated on its own device count: the per-check workspace (~45 KB a check) is sized for one
+// chunk, ~0.75 GB, instead of ~6 GB for every round of a 131072-round segment (round-5 advice).  At 1% bad rounds a
+// 100k-round batch lists ~15 k single checks: one chunk, sometimes two.  (A 100k-round batch on a fresh context: 3.9 GB
+// with chunks of 32768, tests/test_gpu_round5.py.)
+uint32_t xr_qpg() {  // quads per level-1 group (DG_XR_QPG: a test hook for the level shapes)
   static const uint32_t v = (uint32_t)std::max(1, std::min(64, env_int("DG_XR_QPG", (int)XR_QPG)));
   return v;
 }
-// DG_XR_SKIP=1: a failed level-1 group lists its rounds for the single checks directly (two levels)
-uint32_t xr_skip() {
-  static const uint32_t v = env_int("DG_XR_SKIP", (int)XR_SKIP) ? 1u : 0u;
+constexpr uint32_t kXrL3Cap = 16384;
+uint32_t xr_l3cap() {  // DG_XR_L3CAP: a test hook (small chunks on small batches)
+  static const uint32_t v = (uint32_t)std::max(64, std::min((int)kXrL3Cap, env_int("DG_XR_L3CAP", (int)kXrL3Cap)));
   return v;
 }
 int xr_isolate(uint32_t i0, uint32_t n, const uint32_t* flag, const uint64_t* seed, const G1AStore* keys,
                const G2JStore* Q, const G2AStore* S, uint8_t* status, hipStream_t st) {
-  const uint32_t qpg = xr_qpg(), skip = qpg > 1 ? xr_skip() : 0u, nqmax = (n + 3) / 4, G1 = (nqmax + qpg - 1) / qpg;
-  uint32_t *cnt, *cand, *l2, *l3;
+  const uint32_t qpg = xr_qpg(), nqmax = (n + 3) / 4, G1 = (nqmax + qpg - 1) / qpg;
+  const uint32_t C = std::min(n, xr_l3cap()), nch = (n + C - 1) / C, Gmax = std::max(G1, C);
+  uint32_t *cnt, *cand, *l3;
   G2JStore *QS, *HS;
   uint4* T4;
   uint8_t* tinf;
   CkLine* rl;
   CkBufs b;
-  RET(wsT(S_XR_CNT, XR_NCNT, &cnt));
+  RET(wsT(S_XR_CNT, XR_CHUNK0 + nch, &cnt));
   RET(wsT(S_XR_CAND, n, &cand));
-  RET(wsT(S_XR_L2, nqmax, &l2));
   RET(wsT(S_XR_L3, n, &l3));
   RET(wsT(S_XR_QS, 2 * (size_t)nqmax, &QS));
   RET(wsT(S_XR_T4, (size_t)8 * RC_Q * 2 * nqmax, &T4));
   RET(wsT(S_XR_TINF, (size_t)8 * 2 * nqmax, &tinf));
-  RET(wsT(S_XR_HS, n, &HS));
-  RET(wsT(S_XR_RL, (size_t)CK_STEPS * n, &rl));
-  RET(ck_bufs(b, n, false));
+  RET(wsT(S_XR_HS, Gmax, &HS));
+  RET(wsT(S_XR_RL, (size_t)CK_STEPS * Gmax, &rl));
+  RET(ck_bufs(b, Gmax, false));
   RET(launch("k_xg_sub", k_xg_sub, n, 64, st, i0, n, flag, S, status, cnt));
   RET(launch("k_xg_cand", k_xg_cand, n, 256, st, i0, n, flag, (const uint8_t*)status, cand, cnt));
-  RET(launch("k_xq_sum", k_xq_sum, 2 * nqmax, 64, st, nqmax, qpg, seed, cnt, (const uint32_t*)cand, Q, S, T4, tinf, l2,
-             QS));
-  for (uint32_t level = qpg > 1 ? 1u : 2u; level <= 3; ++level) {
-    if (level == 2 && skip) continue;
-    const uint32_t G = level == 1 ? G1 : level == 2 ? nqmax : n, Gp = (G + 63) & ~63u;
-    const uint32_t* gcnt = cnt + level;
-    RET(launch("k_xg_prep", k_xg_prep, G, 64, st, level, G, (const uint32_t*)cnt, qpg, (const uint32_t*)l2,
-               (const uint32_t*)l3, (const G2JStore*)QS, Q, S, keys, b.st, HS));
+  RET(launch("k_xq_sum", k_xq_sum, 2 * nqmax, 64, st, nqmax, qpg, seed, cnt, (const uint32_t*)cand, Q, S, T4, tinf, QS));
+  // one level of checks: G lanes gated on gcnt, level 3's rounds at lst
+  auto level = [&](uint32_t lv, uint32_t G, const uint32_t* gcnt, uint32_t* lst) -> int {
+    const uint32_t Gp = (G + 63) & ~63u;
+    RET(launch("k_xg_prep", k_xg_prep, G, 64, st, lv, G, gcnt, (const uint32_t*)cnt, qpg, (const uint32_t*)lst,
+               (const G2JStore*)QS, Q, S, keys, b.st, HS));
     RET(launch("k_xg_lines", k_xg_lines, 2 * Gp, 64, st, G, gcnt, (const G2JStore*)HS, rl, b.st, b.l2));
     RET(run_checks(G, gcnt, G, rl, b, st, true));
-    RET(launch("k_xg_verdict", k_xg_verdict, G, 128, st, level, G, qpg, skip, cnt, (const uint8_t*)b.good,
-               (const uint32_t*)cand, l2, l3, status, g_ctx.xrcount));
-  }
+    return launch("k_xg_verdict", k_xg_verdict, G, 128, st, lv, G, gcnt, qpg, cnt, (const uint8_t*)b.good,
+                  (const uint32_t*)cand, lst, status, g_ctx.xrcount);
+  };
+  RET(level(1, G1, cnt + 1, l3));
+  RET(launch("k_xg_split", k_xg_split, nch, 64, st, C, nch, cnt));
+  for (uint32_t j = 0; j < nch; ++j)
+    RET(level(3, std::min(C, n - j * C), cnt + XR_CHUNK0 + j, l3 + (size_t)j * C));
   return 0;
 }
 
@@ -1509,6 +1530,13 @@ int dg_init(int device) {
   }
   for (int i = 0; i < kSets; ++i) g_ctx.sets[i].tail = g_ctx.ntails ? g_ctx.tails[i % g_ctx.ntails] : nullptr;
   if (!g_ctx.fb_stream) HIPCHK(hipStreamCreateWithFlags(&g_ctx.fb_stream, hipStreamNonBlocking));
+  // the keyed batches' side stream: a high-priority stream like the tails (a queue of its own beside the 4 normal ones,
+  // so its fork / join waits stall no set stream), created here rather than on the first keyed batch
+  if (!g_ctx.kc_stream) {
+    HIPCHK(hipStreamCreateWithPriority(&g_ctx.kc_stream, hipStreamNonBlocking, greatest_prio));
+    HIPCHK(hipEventCreateWithFlags(&g_ctx.kc_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&g_ctx.kc_join, hipEventDisableTiming));
+  }
   if (!g_ctx.fallbacks) {
     HIPCHK(hipMalloc(&g_ctx.fallbacks, sizeof(unsigned long long)));
     HIPCHK(hipMemset(g_ctx.fallbacks, 0, sizeof(unsigned long long)));
@@ -1554,8 +1582,8 @@ int dg_init(int device) {
         {(const void*)k_ck_sub, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_sub, g1, b64, 0, q, 0u, 0u, cz, (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr); }},
         {(const void*)k_ck_sac, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_sac, g1, b64, 0, q, 0u, (const uint8_t*)nullptr, (const RsDigits*)nullptr, (const uint4*)nullptr, (const uint8_t*)nullptr, (G2JStore*)nullptr, (Fp*)nullptr); }},
         {(const void*)k_xg_sub, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_sub, g1, b64, 0, q, 0u, 0u, cz, (const G2AStore*)nullptr, (uint8_t*)nullptr, z); }},
-        {(const void*)k_xq_sum, [&](hipStream_t q) { hipLaunchKernelGGL(k_xq_sum, g1, b64, 0, q, 0u, 1u, (const uint64_t*)nullptr, z, cz, (const G2JStore*)nullptr, (const G2AStore*)nullptr, (uint4*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr, (G2JStore*)nullptr); }},
-        {(const void*)k_xg_prep, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_prep, g1, b64, 0, q, 1u, 0u, cz, 1u, cz, cz, (const G2JStore*)nullptr, (const G2JStore*)nullptr, (const G2AStore*)nullptr, (const G1AStore*)nullptr, (CkState*)nullptr, (G2JStore*)nullptr); }},
+        {(const void*)k_xq_sum, [&](hipStream_t q) { hipLaunchKernelGGL(k_xq_sum, g1, b64, 0, q, 0u, 1u, (const uint64_t*)nullptr, z, cz, (const G2JStore*)nullptr, (const G2AStore*)nullptr, (uint4*)nullptr, (uint8_t*)nullptr, (G2JStore*)nullptr); }},
+        {(const void*)k_xg_prep, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_prep, g1, b64, 0, q, 1u, 0u, cz, cz, 1u, cz, (const G2JStore*)nullptr, (const G2JStore*)nullptr, (const G2AStore*)nullptr, (const G1AStore*)nullptr, (CkState*)nullptr, (G2JStore*)nullptr); }},
         {(const void*)k_xg_hlines, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_hlines, g1, b64, 0, q, 0u, cz, (const G2JStore*)nullptr, (CkLine*)nullptr, (CkState*)nullptr); }},
     };
     const std::vector<Warm> on_fb = {
@@ -1617,6 +1645,12 @@ void dg_shutdown(void) {
       (void)hipStreamDestroy(t);
     }
     t = nullptr;
+  }
+  for (Set& x : g_ctx.xr_pools) {
+    for (void* p : x.pool)
+      if (p) (void)hipFree(p);
+    x.pool.clear();
+    x.pool_size.clear();
   }
   g_ctx.ntails = 0;
   if (g_ctx.fb_stream) {

@@ -9,34 +9,34 @@
 //     e(X, h_eff(sum rho_i Q_i)) == e(g1, sum rho_i S_i)          (Q_i the uncleared hash of round i: h_eff is linear)
 // holds for a set of valid rounds, and a set holding a bad round passes with probability <= 2^-63 (every S_i in G2 --
 // the batch's windowed subgroup check, or k_xg_sub after it failed -- and E_i = x h(Q_i) - S_i != 0 vanishes in the
-// weighted sum for at most one rho_i mod r).  Levels, each one run of the pipeline with its checks listed on the
+// weighted sum for at most one rho_i mod r).  Two levels, each one run of the pipeline with its checks listed on the
 // device:
-//     level 1  groups of qpg quads (4 qpg rounds; default 16)          -> a failed group lists its rounds (default) or
-//                                                                         its quads (DG_XR_SKIP=0)
-//     level 2  quads (4 rounds; DG_XR_SKIP=0 only)                     -> a failed quad lists its rounds
+//     level 1  groups of qpg quads (4 qpg rounds; default 16)          -> a failed group lists its rounds
 //     level 3  single rounds: e(X, h(Q_i)) == e(g1, S_i), kyber's bls.Verify verdict, exact
-// Every round of a passed group or quad keeps its OK status (error <= 2^-63); every rejected round was rejected by its
-// own exact check.  At 1% bad rounds a 100k-round batch takes ~6.3 k + ~15 k checks (three levels: ~6.3 k + ~3.7 k +
-// ~4 k) instead of 100 k.  Each level costs the latency of one check, so two levels beat three (c2_negative 3.3 vs
-// 2.8 M rounds/s).
+// (the numbering keeps the round-5 counters: a level 2 of quads between them measured slower, 2.8 against 3.3 M
+// rounds/s, and is gone).  Every round of a passed group keeps its OK status (error <= 2^-63); every rejected round was
+// rejected by its own exact check.  At 1% bad rounds a 100k-round batch takes ~6.3 k + ~15 k checks instead of 100 k.
 //
 //   k_xg_sub    (after a failed windowed subgroup check only) the G2 subgroup check of every decoded signature
 //   k_xg_cand   the decoded rounds of a failed batch, compacted (nothing after a passed batch)
 //   k_xq_sum    per quad and side: sum rho_i P_i (P = Q or S) by the four-point sign-aligned column form over an affine
 //               8-entry table built in the lane (three levels of affine additions, one Fp inversion per level)
-//   per level:  k_xg_prep (the check's sums; sigma side affine), k_xg_hlines (h_eff of the hash side and its 68 lines),
-//               checks.h k_ck_lines2 .. k_ck_final (gated on the level's device count), k_xg_verdict
-// The launches are sized for the worst case (every round bad: N / 4 quads, N singles) and gated on the device counts,
-// so the host enqueues the whole isolation without a round trip; after a passed batch every launch returns at once.
+//   per level:  k_xg_prep (the check's sums; sigma side affine), k_xg_lines (h_eff of the hash side and the 68 lines of
+//               both pairs), checks.h k_ck_miller2 .. k_ck_final (gated on the level's device count), k_xg_verdict
+//   k_xg_split  the level-3 list cut into chunks of at most `cap` checks (the count of each chunk)
+// The launches are sized for the worst case and gated on the device counts, so the host enqueues the whole isolation
+// without a round trip; after a passed batch every launch returns at once.  Level 3 runs in chunks of a fixed capacity
+// (drand_gpu.hip kXrL3Cap), each gated on its own count: its per-check workspace (~45 KB: the 68 lines of both pairs,
+// the Fp12 values) is sized for one chunk, not for every round of the batch.
 #pragma once
 
 namespace dg {
 
 constexpr uint64_t XR_TAG = 0x63726f7373726e64ull;  // "crossrnd": domain of the cross-round weights rho_i
-constexpr uint32_t XR_QPG = 4;                       // quads per level-1 group (default; DG_XR_QPG, 1 = no level 1)
-constexpr uint32_t XR_SKIP = 1;                      // 1: no level 2, failed groups go to single checks (DG_XR_SKIP)
-// device counters: [0] candidates, [1] level-1 checks, [2] level-2 checks (quads), [3] level-3 checks (rounds)
-constexpr uint32_t XR_NCNT = 4;
+constexpr uint32_t XR_QPG = 4;                       // quads per level-1 group (default; DG_XR_QPG, a test hook)
+// device counters: [0] candidates, [1] level-1 checks, [2] unused, [3] level-3 checks (rounds), then from XR_CHUNK0 the
+// check count of each level-3 chunk (k_xg_split)
+constexpr uint32_t XR_NCNT = 4, XR_CHUNK0 = 4;
 
 DGI uint64_t xr_rho(uint64_t seed, uint32_t i) { return rlc_coeff(seed ^ XR_TAG, i); }
 
@@ -105,17 +105,16 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_xg_sub(uint32_t i0, uint
   const G2A s = load_g2a(S[i]);
   if (!s.inf && !ck_in_subgroup(s.x, s.y, s_acc[threadIdx.x])) status[i] = DG_ST_SIG_DECODE_;
 }
-// one check of `level` (1: group g of qpg quads, 2: quad l2list[g], 3: round l3list[g] alone): HS[g] = its uncleared
-// hash-side sum, st[g] = {a: the group key, b: the signature-side sum (affine), np bit 1}
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xg_prep(uint32_t level, uint32_t G, const uint32_t* cnt,
-                                                             uint32_t qpg, const uint32_t* l2list,
-                                                             const uint32_t* l3list, const G2JStore* QS,
-                                                             const G2JStore* Q, const G2AStore* S,
+// one check of `level` (1: group g of qpg quads, 3: round l3list[g] alone; gcnt: the launch's device count): HS[g] = its
+// uncleared hash-side sum, st[g] = {a: the group key, b: the signature-side sum (affine), np bit 1}
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xg_prep(uint32_t level, uint32_t G, const uint32_t* gcnt,
+                                                             const uint32_t* cnt, uint32_t qpg, const uint32_t* l3list,
+                                                             const G2JStore* QS, const G2JStore* Q, const G2AStore* S,
                                                              const G1AStore* keys, CkState* st, G2JStore* HS) {
   DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   __shared__ G2JStore s_h[64], s_s[64];
-  if (ck_dead(g, G, cnt + level)) return;
+  if (ck_dead(g, G, gcnt)) return;
   CkState c{};
   G2A b;
   if (level == 3) {
@@ -125,8 +124,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xg_prep(uint32_t level, uin
     c.live[0] = i;
   } else {
     const uint32_t nq = (cnt[0] + 3) / 4;
-    const uint32_t q0 = level == 1 ? g * qpg : l2list[g];
-    const uint32_t q1 = level == 1 ? (q0 + qpg < nq ? q0 + qpg : nq) : q0 + 1;
+    const uint32_t q0 = g * qpg, q1 = q0 + qpg < nq ? q0 + qpg : nq;
     G2JStore& h = s_h[threadIdx.x];
     G2JStore& s = s_s[threadIdx.x];
     h.x = h.y = h.z = fp2_zero();
@@ -184,35 +182,27 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_lines(uint32_t G, const u
                                                              CkLine* rl, CkState* st, CkLine* l2);
 DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_xg_sub(uint32_t i0, uint32_t n, const uint32_t* flag,
                                                                const G2AStore* S, uint8_t* status, uint32_t* cnt);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xg_prep(uint32_t level, uint32_t G, const uint32_t* cnt,
-                                                             uint32_t qpg, const uint32_t* l2list,
-                                                             const uint32_t* l3list, const G2JStore* QS,
-                                                             const G2JStore* Q, const G2AStore* S,
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xg_prep(uint32_t level, uint32_t G, const uint32_t* gcnt,
+                                                             const uint32_t* cnt, uint32_t qpg, const uint32_t* l3list,
+                                                             const G2JStore* QS, const G2JStore* Q, const G2AStore* S,
                                                              const G1AStore* keys, CkState* st, G2JStore* HS);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_hlines(uint32_t G, const uint32_t* gcnt, const G2JStore* HS,
                                                               CkLine* rl, CkState* st);
 #endif
 #if DG_TU_CHECK == 5
 // lane 2 q + side (side 0: the hashes Q, side 1: the signatures S) of quad q = candidates [4 q, 4 q + 4): QS[2 q + side] =
-// sum rho_i P_i (xq_sum4; the table SoA at T4 / tinf with stride 2 nqmax).  Lane 0 sets the level counts from the
-// candidate count: level 1 ceil(nq / qpg) groups, or with qpg = 1 level 2 takes every quad (l2list[q] = q).
+// sum rho_i P_i (xq_sum4; the table SoA at T4 / tinf with stride 2 nqmax).  Lane 0 sets the level-1 count from the
+// candidate count: ceil(nq / qpg) groups.
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xq_sum(uint32_t nqmax, uint32_t qpg, const uint64_t* seedp,
                                                             uint32_t* cnt, const uint32_t* cand, const G2JStore* Q,
-                                                            const G2AStore* S, uint4* T4, uint8_t* tinf,
-                                                            uint32_t* l2list, G2JStore* QS) {
+                                                            const G2AStore* S, uint4* T4, uint8_t* tinf, G2JStore* QS) {
   DG_HI();
   const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
   __shared__ G2JStore s_acc[64];
   const uint32_t c = cnt[0], nq = (c + 3) / 4;
-  if (gl == 0) {
-    if (qpg > 1)
-      cnt[1] = (nq + qpg - 1) / qpg;
-    else
-      cnt[2] = nq;
-  }
+  if (gl == 0) cnt[1] = (nq + qpg - 1) / qpg;
   const uint32_t q = gl >> 1, side = gl & 1;
   if (q >= nq || q >= nqmax) return;
-  if (qpg == 1 && side == 0) l2list[q] = q;
   const uint64_t seed = *seedp;
   uint32_t idx[4];
   uint64_t rho[4];
@@ -244,8 +234,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xq_sum(uint32_t nqmax, uint
 #else
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xq_sum(uint32_t nqmax, uint32_t qpg, const uint64_t* seedp,
                                                             uint32_t* cnt, const uint32_t* cand, const G2JStore* Q,
-                                                            const G2AStore* S, uint4* T4, uint8_t* tinf,
-                                                            uint32_t* l2list, G2JStore* QS);
+                                                            const G2AStore* S, uint4* T4, uint8_t* tinf, G2JStore* QS);
 #endif
 #if DG_TU_LIB
 // the decoded items of [i0, i0 + n) of a failed batch (flag[0] == 0), compacted into cand (one atomic per wave, input
@@ -263,16 +252,15 @@ DG_KERNEL void __launch_bounds__(256) k_xg_cand(uint32_t i0, uint32_t n, const u
   base = __shfl(base, (int)first);
   if (on) cand[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = i0 + g;
 }
-// the verdicts of level `level` (good[g]: k_ck_final): a passed check leaves its rounds valid (their status is OK
-// already); a failed group lists its quads for level 2, a failed quad its rounds for level 3; a single check writes
-// kyber's verdict.  xrc[level - 1] counts the checks (dg_group_counts).
-// (skip != 0: a failed group lists its rounds for level 3 directly -- two levels, groups then single rounds)
-DG_KERNEL void __launch_bounds__(128) k_xg_verdict(uint32_t level, uint32_t G, uint32_t qpg, uint32_t skip, uint32_t* cnt,
-                                                   const uint8_t* good, const uint32_t* cand, uint32_t* l2list,
+// the verdicts of level `level` (good[g]: k_ck_final; gcnt: the launch's device count): a passed group leaves its rounds
+// valid (their status is OK already), a failed group lists its rounds for level 3; a single check writes kyber's
+// verdict.  xrc[level - 1] counts the checks (dg_isolation_counts).
+DG_KERNEL void __launch_bounds__(128) k_xg_verdict(uint32_t level, uint32_t G, const uint32_t* gcnt, uint32_t qpg,
+                                                   uint32_t* cnt, const uint8_t* good, const uint32_t* cand,
                                                    uint32_t* l3list, uint8_t* status, unsigned long long* xrc) {
   DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G || g >= cnt[level]) return;
+  if (ck_dead(g, G, gcnt)) return;
   atomicAdd(&xrc[level - 1], 1ull);
   const bool ok = good[g] != 0;
   if (level == 3) {
@@ -280,20 +268,17 @@ DG_KERNEL void __launch_bounds__(128) k_xg_verdict(uint32_t level, uint32_t G, u
     return;
   }
   if (ok) return;
-  const uint32_t c = cnt[0], nq = (c + 3) / 4;
-  if (level == 1 && skip) {
-    const uint32_t j0 = 4 * g * qpg, j1 = j0 + 4 * qpg < c ? j0 + 4 * qpg : c;
-    const uint32_t pos = atomicAdd(&cnt[3], j1 - j0);
-    for (uint32_t j = j0; j < j1; ++j) l3list[pos + j - j0] = cand[j];
-  } else if (level == 1) {
-    const uint32_t q0 = g * qpg, q1 = q0 + qpg < nq ? q0 + qpg : nq;
-    const uint32_t pos = atomicAdd(&cnt[2], q1 - q0);
-    for (uint32_t q = q0; q < q1; ++q) l2list[pos + q - q0] = q;
-  } else {
-    const uint32_t q = l2list[g], j0 = 4 * q, j1 = j0 + 4 < c ? j0 + 4 : c;
-    const uint32_t pos = atomicAdd(&cnt[3], j1 - j0);
-    for (uint32_t j = j0; j < j1; ++j) l3list[pos + j - j0] = cand[j];
-  }
+  const uint32_t c = cnt[0], j0 = 4 * g * qpg, j1 = j0 + 4 * qpg < c ? j0 + 4 * qpg : c;
+  const uint32_t pos = atomicAdd(&cnt[3], j1 - j0);
+  for (uint32_t j = j0; j < j1; ++j) l3list[pos + j - j0] = cand[j];
+}
+// the level-3 list (cnt[3] rounds) cut into nch chunks of at most cap checks: cnt[XR_CHUNK0 + j] = chunk j's count
+DG_KERNEL void __launch_bounds__(64) k_xg_split(uint32_t cap, uint32_t nch, uint32_t* cnt) {
+  DG_HI();
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nch) return;
+  const uint32_t n = cnt[3], lo = j * cap;
+  cnt[XR_CHUNK0 + j] = n > lo ? (n - lo < cap ? n - lo : cap) : 0u;
 }
 #endif
 #endif

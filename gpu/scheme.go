@@ -144,7 +144,9 @@ func flatten(items [][]byte, size int) ([]byte, error) {
 	return out, nil
 }
 
-// VerifyRecoveredBatch returns one error (nil = valid) per signature, exactly kyber's bls.Verify verdicts.
+// VerifyRecoveredBatch returns one error (nil = valid) per signature: kyber's bls.Verify verdict for every rejected
+// signature (each failed its own exact check); an accepted one passed a random-linear-combination batch or group test,
+// which a bad signature survives with probability <= 2^-63 (drand_gpu.h Conventions).
 func (s *Scheme) VerifyRecoveredBatch(public kyber.Point, msgs, sigs [][]byte) ([]error, error) {
 	n := len(msgs)
 	if n != len(sigs) {

@@ -77,8 +77,10 @@ int dg_sign(size_t n, const uint8_t* scalars32, const uint16_t* index, const uin
 
 /* A3/A4 -- tbls.VerifyRecovered / bls.Verify batch against one key (beacon/beacon.go:494,575,
  * beacon/chain.go:70, core/client_public.go:116).  Random-linear-combination multi-pairing with one
- * shared final exponentiation; on a failed batch, every item is re-checked on its own so `status` is
- * exactly the per-item bls.Verify verdict.  `seed` keys the 64-bit RLC coefficients (0: from the OS). */
+ * shared final exponentiation; on a failed batch the bad items are isolated on the device by group tests
+ * across items (groups of 16, then every item of a failed group alone): a rejected item failed its own exact
+ * check, an accepted item is valid except with probability <= 2^-63 (see Conventions).  `seed` keys the 64-bit
+ * RLC coefficients (0: from the OS). */
 int dg_verify(const uint8_t pk48[48], size_t n, const uint8_t* msgs, size_t msg_len, const uint8_t* sigs96,
               uint8_t* status, uint64_t seed);
 
@@ -175,11 +177,15 @@ int dg_verify_beacons_dev_async(const uint8_t* pk48_host, size_t n, const uint64
  * needed.  (No reference counterpart.) */
 int dg_queue_plan(int hw_queues, int* sets, int* per_item_on_set_streams);
 /* The HIP stream (hipStream_t) the most recent dg_verify_beacons_dev_async batch completes on (its high-priority tail
- * stream).  Work the caller enqueues there runs after that batch with no cross-stream wait: with fewer hardware queues than streams
- * (GPU_MAX_HW_QUEUES, HIP's default 4) a wait queued on a shared queue holds every stream behind it, so a consumer
- * of one batch's statuses (an all-gather, a copy) is cheapest on this stream.  The stream stays owned by the library
- * (valid until dg_shutdown); DG_E_ARG before the first asynchronous batch.  (No reference counterpart: drand verifies
- * beacons one at a time, beacon/chain.go:65-71.) */
+ * stream).  Work the caller enqueues there runs after that batch with no cross-stream wait: with fewer
+ * hardware queues than streams (GPU_MAX_HW_QUEUES, HIP's default 4) a wait queued on a shared queue holds every stream
+ * behind it, so a short consumer of one batch's statuses (a bitmap pack, an all-gather, a copy) is cheapest on this
+ * stream.  The stream is SHARED and HIGH PRIORITY: the library has 4 tail streams, set i ends on tail i mod 4, so the
+ * batch two sets later ends on the same one, and whatever the caller enqueues there runs at high priority and ahead of
+ * that later batch's tail (its Miller loops, final exponentiation and isolation).  Keep it short; for long work record
+ * an event here and wait for it on a stream of the caller's.  The stream stays owned by the library (valid until
+ * dg_shutdown); DG_E_ARG before the first asynchronous batch.  (No reference counterpart: drand verifies beacons one
+ * at a time, beacon/chain.go:65-71.) */
 int dg_last_batch_stream(void** out);
 /* Diagnostics of the most recent verification batch: out2[0] = 1 if the random-linear-combination
  * batch equation held, out2[1] = 1 if some item was checked on its own (duplicate key cell).  A valid
@@ -192,8 +198,9 @@ int dg_fallback_count(uint64_t* out);
  * one round at once (m = 1: a share's own bls.Verify; m = 2..4: a random-linear-combination group test). */
 int dg_group_counts(uint64_t* out4);
 /* The isolation of failed single-key batches (dg_verify, dg_verify_beacons*) since dg_init (waits for batches in
- * flight): out3[0] = group tests of 4..64 rounds, out3[1] = tests of 4 rounds, out3[2] = single bls.Verify checks
- * (beacon/chain.go:65-71 decides every round alone; a failed batch equation splits its rounds this way). */
+ * flight): out3[0] = group tests of 4..256 rounds (16 by default), out3[1] = 0 (the round-5 quad level, removed),
+ * out3[2] = single bls.Verify checks (beacon/chain.go:65-71 decides every round alone; a failed batch equation splits
+ * its rounds this way). */
 int dg_isolation_counts(uint64_t* out3);
 /* Shares per group test in Recover's per-item pass: 1..4 (default 4, or the DG_GROUP environment variable);
  * 1 = every examined share gets its own exact pairing check.  Process-wide. */
