@@ -478,16 +478,11 @@ def recover_bench(L, tbls, shard, src, R_total, t, n, world, rank, peak, steps=2
     return out, (commits, msgs, parts), vp_line
 
 
-def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=256, frac=0.10, n_short=3, vp_neg=True):
-    """BASELINE configs[4] (SURVEY C5): n = 256, t = 129, ~10% of the (round, share) cells corrupted with the six
-    cycling modes of tools/corrupt.py, plus `n_short` rounds with more than n - t corrupted shares (-> "not
-    enough shares"); each rank its contiguous range of R_total rounds through dg_recover_dev (inputs resident
-    in HBM; the batch equation fails, so the examined prefix of every round takes the per-item pass: group
-    tests of up to 4 shares -- a passed group's members are accepted with error probability <= 2^-63 (odd 64-bit weights) -- and
-    single pairing checks for the members of failed groups; DG_GROUP=1 makes every check a single one), then
-    the all-gather of the outputs.  Checked without the CPU: recovered signatures equal the chain's, exactly the short rounds
-    report NOT_ENOUGH, every examined corrupted share is rejected and every examined clean one accepted
-    (per-share parity with the CPU twin is tests/test_gpu_parity.py's job)."""
+def make_c5_inputs(tbls, shard, src, R_total, world, rank, t=129, n=256, frac=0.10, n_short=3):
+    """configs[4]'s inputs for this rank's contiguous range of R_total rounds: n partials per round signed by the
+    GPU (dg_sign), ~frac of the (round, share) cells corrupted with the six modes of tools/corrupt.py (pattern of the
+    GLOBAL round numbers), `n_short` rounds with too few valid shares.  Returns (pub, msgs, parts, bad, short, items,
+    gen_s, a, b)."""
     from tools import corrupt
 
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "groups.json")))["t%d" % t]
@@ -520,6 +515,22 @@ def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=
     bad = np.zeros((R, n), dtype=bool)
     for r, j, _ in items:
         bad[r, j] = True
+    return pub, msgs, parts, bad, short, items, gen_s, a, b
+
+
+def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=256, frac=0.10, n_short=3, vp_neg=True):
+    """BASELINE configs[4] (SURVEY C5): n = 256, t = 129, ~10% of the (round, share) cells corrupted with the six
+    cycling modes of tools/corrupt.py, plus `n_short` rounds with more than n - t corrupted shares (-> "not
+    enough shares"); each rank its contiguous range of R_total rounds through dg_recover_dev (inputs resident
+    in HBM; the batch equation fails, so the examined prefix of every round takes the per-item pass: group
+    tests of up to 4 shares -- a passed group's members are accepted with error probability <= 2^-63 (odd 64-bit weights) -- and
+    single pairing checks for the members of failed groups; DG_GROUP=1 makes every check a single one), then
+    the all-gather of the outputs.  Checked without the CPU: recovered signatures equal the chain's, exactly the short rounds
+    report NOT_ENOUGH, every examined corrupted share is rejected and every examined clean one accepted
+    (per-share parity with the CPU twin is tests/test_gpu_parity.py's job)."""
+    pub, msgs, parts, bad, short, items, gen_s, a, b = make_c5_inputs(tbls, shard, src, R_total, world, rank, t, n,
+                                                                    frac, n_short)
+    R = b - a
     import torch
 
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -1063,6 +1074,9 @@ def main():
     sig_src = [d_sig]  # the signatures the steps verify (the c2_negative line swaps in a corrupted copy)
 
     hostprof = collections.defaultdict(float) if os.environ.get("DG_BENCH_HOSTPROF") else None
+    # BENCH_STEP_TIMES=1 (diagnostics): each timed step's completion (its bitmap's event) in ms from the region's start,
+    # on stderr -- the pipeline's fill, steady spacing and drain
+    step_times = None
 
     def enqueue(lo, hi, d_st, seed, blocking):
         args_ = (pkb, hi - lo, L.ptr(d_pr[lo:]), L.ptr(d_r[lo:]), L.ptr(d_ps), L.ptr(d_off[lo:]),
@@ -1098,9 +1112,11 @@ def main():
             gs = torch.cuda.ExternalStream(sp.value, device=dev)
         with torch.cuda.stream(gs):
             bits = shard.allgather_verdicts(d_st, world, m=mbytes)
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(enable_timing=step_times is not None)
             ev.record(gs)
         gathered[i] = (bits, ev)
+        if step_times is not None:
+            step_times.append(ev)
         return bits
 
     def drain():
@@ -1126,6 +1142,11 @@ def main():
     if world > 1:
         dist.barrier()
     fb0 = L.fallback_count()
+    ev0 = None
+    if os.environ.get("BENCH_STEP_TIMES"):
+        step_times = []
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record(torch.cuda.current_stream(dev))
     t0 = time.perf_counter()
     if hostprof is not None:
         hostprof.clear()
@@ -1136,6 +1157,10 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if ev0 is not None:
+        ts = [round(ev0.elapsed_time(e), 3) for e in step_times]
+        print("[step_times] region %.3f ms, completions (ms): %s" % (dt * 1e3, ts), file=sys.stderr, flush=True)
+        step_times = None
     if hostprof is not None:
         hostprof["timed_s"] = dt
         print("[hostprof]", json.dumps({k: round(v, 5) for k, v in hostprof.items()}), file=sys.stderr, flush=True)

@@ -189,6 +189,26 @@ DGI Fp12 ck_miller1(const Fp& px, const Fp& py, Line line) {
   return fp12_conj(f);
 }
 
+// ck_miller1 with the pair's lines computed in the lane from Q (affine, not the identity) as the loop runs: no line table.
+// The isolation's checks (xr.h k_xg_miller) have no per-round line sharing, so storing each check's 68 lines to HBM
+// for a second kernel bought nothing but 19.6 KB per pair of workspace and a launch
+DGI Fp12 ck_miller1_fly(const Fp2& qx, const Fp2& qy, const Fp& px, const Fp& py) {
+  G2Proj T{qx, qy, fp2_one()};
+  Fp12 f = fp12_one();
+#pragma unroll 1
+  for (uint32_t s = 0; s < CK_STEPS; ++s) {
+    const bool dbl = ck_step_is_dbl(s);
+    if (s != 0 && dbl) f = fp12_sqr(f);
+    CkLine l;
+    if (dbl)
+      ck_line_dbl(T, l);
+    else
+      ck_line_add(T, qx, qy, l);
+    f = fp12_mul_014(f, l.c0, fp2_mul_fp(l.c1, px), fp2_mul_fp(l.c4, py));
+  }
+  return fp12_conj(f);
+}
+
 // ---- final exponentiation in pieces (pairing.h final_exp_cubed)
 // f^-1 = (f0 t6^-1, -f1 t6^-1) with t6 = f0^2 - v f1^2 (field.h fp12_inv); t6^-1 by fp6_inv, whose one inversion
 // (of the Fp2 value t) becomes an inversion of N(t) in Fp, batched across the checks
@@ -559,7 +579,7 @@ DG_KERNEL void __launch_bounds__(128) k_ck_verdict(uint32_t G, const CkState* st
 // the easy part of the final exponentiation: F2[g] = f1 frob^2(f1), f1 = f^-1 conj(f); f^-1 by ck_fe1 / ck_inv with the
 // one Fp inversion of the check in the lane (field.h fp_inv, safegcd) -- no batch inversion across the checks.  Lane 0
 // also empties the CK_NEXP work lists of k_ck_explain (zl + z (G + 1), z < CK_NEXP).
-// (two != 0: F holds the two pairs' values of k_ck_miller2, F[g] and F[G + g]; f is their product)
+// (two != 0: F holds the two pairs' values of xr.h k_xg_miller, F[g] and F[G + g]; f is their product)
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_easy(uint32_t G, const uint32_t* gcnt, uint32_t two, const Fp12* F,
                                                             Fp12* F2, uint32_t* zl) {
   DG_HI();
@@ -578,7 +598,7 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_easy(uint32_t G, const ui
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_easy(uint32_t G, const uint32_t* gcnt, uint32_t two, const Fp12* F,
                                                             Fp12* F2, uint32_t* zl);
 #endif
-// the Miller value of every check (kernels_check_b.hip)
+// the Miller value of every check (kernels_check_b.hip): both pairs in one lane, the squarings shared
 #if DG_TU_CHECK == 2
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, const uint32_t* gcnt, uint32_t R,
                                                               const CkState* st, const CkLine* rl, const CkLine* l2,
@@ -595,31 +615,10 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, const 
   F[g] = ck_miller(np, ax, ay, line);
 #endif
 }
-// two lanes per check (lanes [0, Gp) pair 0, [Gp, 2 Gp) pair 1, Gp = G rounded up to whole waves): F[pair G + g]
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller2(uint32_t G, const uint32_t* gcnt, uint32_t R,
-                                                               const CkState* st, const CkLine* rl, const CkLine* l2,
-                                                               Fp12* F) {
-  DG_HI();
-  const uint32_t Gp = (G + 63) & ~63u, lane = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t pair = lane >= Gp ? 1u : 0u, g = lane - pair * Gp;
-  if (ck_dead(g, G, gcnt)) return;
-  const uint32_t np = st[g].np, r = st[g].round;
-  Fp12 f = fp12_one();
-  if ((np >> pair) & 1) {
-    if (pair)
-      f = ck_miller1(fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), [&](uint32_t s) { return l2[(size_t)s * G + g]; });
-    else
-      f = ck_miller1(st[g].a.x, st[g].a.y, [&](uint32_t s) { return rl[(size_t)s * R + r]; });
-  }
-  F[(size_t)pair * G + g] = f;
-}
 #else
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, const uint32_t* gcnt, uint32_t R,
                                                               const CkState* st, const CkLine* rl, const CkLine* l2,
                                                               Fp12* F);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller2(uint32_t G, const uint32_t* gcnt, uint32_t R,
-                                                               const CkState* st, const CkLine* rl, const CkLine* l2,
-                                                               Fp12* F);
 #endif
 // the end of final_exp_cubed and the check's verdict (kernels_check_c.hip): T = (a^z)^z frob^2(a) (k_ck_expdec's
 // product), b = T conj(a), c = f2^3, good[g] = (no pair, or b c == 1)

@@ -211,7 +211,7 @@ enum Slot {
   S_SEED2, S_SB, S_STB, S_ISOB, S_KMSM_GOFS, S_KMSM_BP, S_KMSM_BT2,
   S_CK_RL, S_CK_HINF, S_CK_ST, S_CK_L2, S_CK_F, S_CK_T0, S_CK_T1, S_CK_F2, S_CK_A, S_CK_NV, S_CK_SN, S_CK_ZERO,
   S_CK_ZL, S_CK_GOOD, S_CK_T4, S_CK_TINF, S_CK_DIG, S_CK_TDEN, S_CK_BJ, S_CK_BN, S_CK_G2M, S_KOK, S_XR_CNT, S_XR_CAND,
-  S_XR_QS, S_XR_T4, S_XR_TINF, S_XR_L3, S_XR_HS, S_XR_RL,
+  S_XR_QS, S_XR_T4, S_XR_TINF, S_XR_L3, S_XR_HS,
   // msm_run / batch_inv on the keyed batches' side stream (alt): the same buffers, apart from the main stream's
   S_MSM2_CNT, S_MSM2_LIST, S_MSM2_CHUNKS, S_MSM2_AFF, S_MSM2_DEN, S_MSM2_DINV, S_MSM2_B, S_MSM2_G, S_MSM2_P1, S_MSM2_W,
   S_MSM2_OUT, S_BINV2_PRE, S_BINV2_ROOTS, S_BINV2, S_COUNT
@@ -226,6 +226,22 @@ struct HostProf {
   double launch_us = 0, wait_us = 0;
   uint64_t launches = 0, waits = 0;
 } g_hp;
+// DG_BATCH_TRACE=1 (diagnostics): per asynchronous beacon batch, timing events at its start on the set stream, at
+// the hand-over to its tail stream (hop) and at its end; printed (ms from the first start) and reset by dg_wait_all
+struct BatchTrace {
+  int set;
+  hipEvent_t s, h, d;
+};
+struct BatchTraces {
+  bool on = getenv("DG_BATCH_TRACE") != nullptr;
+  std::vector<BatchTrace> v;
+  BatchTrace* cur = nullptr;
+} g_bt;
+hipEvent_t bt_event(hipStream_t st) {
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) == hipSuccess) (void)hipEventRecord(e, st);
+  return e;
+}
 inline double hp_now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -551,6 +567,7 @@ int msm_run(uint32_t R, const uint64_t* seed, const uint8_t* active, const G2JSt
   if (tst) {
     // the rest is latency-bound: it moves to the batch's tail stream (Set::tail)
     HIPCHK(hipEventRecord(cur_set().hop, st));
+    if (g_bt.cur) g_bt.cur->h = bt_event(st);
     HIPCHK(hipStreamWaitEvent(tst, cur_set().hop, 0));
     st = tst;
   }
@@ -1081,10 +1098,11 @@ struct CkBufs {
   Fp *tden, *bn;
   G2JStore* bj;
 };
-int ck_bufs(CkBufs& b, size_t G, bool group_sums) {
+int ck_bufs(CkBufs& b, size_t G, bool group_sums, bool lines = true) {
   RET(wsT(S_CK_ST, G, &b.st));
-  RET(wsT(S_CK_L2, (size_t)CK_STEPS * G, &b.l2));
-  RET(wsT(S_CK_F, 2 * G, &b.F));  // (two pairs' values per check for k_ck_miller2)
+  b.l2 = nullptr;
+  if (lines) RET(wsT(S_CK_L2, (size_t)CK_STEPS * G, &b.l2));  // (not for the isolation: xr.h k_xg_miller)
+  RET(wsT(S_CK_F, 2 * G, &b.F));  // (two pairs' values per check for xr.h k_xg_miller)
   RET(wsT(S_CK_F2, G, &b.F2));
   RET(wsT(S_CK_T0, G, &b.T0));
   RET(wsT(S_CK_T1, G, &b.T1));
@@ -1109,39 +1127,36 @@ int ck_bufs(CkBufs& b, size_t G, bool group_sums) {
 // product with the six norms inverted in the lane (k_ck_expdec), the uncompressed chain for the lanes with a zero
 // denominator (k_ck_explain over work list z, CK_EXPLAIN_LANES lanes: it is rare); out = X^z op(Y) (Y may be null)
 int ck_expz(uint32_t z, uint32_t G, const uint32_t* gcnt, const Fp12* X, const Fp12* Y, uint32_t nfrob, uint32_t conj,
-            Fp12* out, const CkBufs& b, hipStream_t st, bool latency) {
+            Fp12* out, const CkBufs& b, hipStream_t st) {
   uint32_t* zl = b.zl + (size_t)z * (G + 1);
-  (void)latency;  // two lanes per check everywhere (C5 15.3 -> 15.6 k: the one-lane form spilled 79 VGPRs)
+  // two lanes per check everywhere (C5 15.3 -> 15.6 k: the one-lane form spilled 79 VGPRs)
   RET(launch("k_ck_expsq2", k_ck_expsq2, 2 * G, 64, st, G, gcnt, X, b.sn, b.nv, b.zero, zl));
   RET(launch("k_ck_expdec", k_ck_expdec, G, 64, st, G, gcnt, (const CycC*)b.sn, b.nv, (const uint8_t*)b.zero, Y, nfrob,
              conj, out));
   return launch("k_ck_explain", k_ck_explain, CK_EXPLAIN_LANES, 64, st, (const uint32_t*)zl, X, Y, nfrob, conj, out);
 }
-// The checks b.st[0..G) (pair 0: (a, the lines rl[s R + round]), pair 1: (-g1, b)) -> b.good: the (-g1, b) lines, the
-// Miller values, the final exponentiation (k_ck_easy, five x^z with their next factors, k_ck_final).  Every kernel is
-// one lane per check without exchange, so gcnt (device, may be null) gates the lanes of a launch sized for G.
-// latency (the cross-round isolation: few checks per launch): the lines are already in l2 (xr.h k_xg_lines) and each
-// check's two Miller pairs run in lanes of their own (k_ck_miller2)
-int run_checks(uint32_t G, const uint32_t* gcnt, uint32_t R, const CkLine* rl, const CkBufs& b, hipStream_t st,
-               bool latency = false) {
-  const uint32_t Gp = (G + 63) & ~63u;
-  if (latency) {
-    RET(launch("k_ck_miller2", k_ck_miller2, 2 * Gp, 64, st, G, gcnt, R, (const CkState*)b.st, rl, (const CkLine*)b.l2,
-               b.F));
-  } else {
-    RET(launch("k_ck_lines2", k_ck_lines2, G, 64, st, G, gcnt, (const CkState*)b.st, b.l2));
-    RET(launch("k_ck_miller", k_ck_miller, G, 64, st, G, gcnt, R, (const CkState*)b.st, rl, (const CkLine*)b.l2, b.F));
-  }
-  RET(launch("k_ck_easy", k_ck_easy, G, 64, st, G, gcnt, latency ? 1u : 0u, (const Fp12*)b.F, b.F2, b.zl));
+// The final exponentiation of the checks b.st[0..G) from their Miller values b.F (two != 0: the two pairs' values F[g],
+// F[G + g], multiplied first) -> b.good: k_ck_easy, five x^z with their next factors, k_ck_final.  Every kernel is one
+// lane per check without exchange, so gcnt (device, may be null) gates the lanes of a launch sized for G.
+int run_final(uint32_t G, const uint32_t* gcnt, const CkBufs& b, hipStream_t st, uint32_t two) {
+  RET(launch("k_ck_easy", k_ck_easy, G, 64, st, G, gcnt, two, (const Fp12*)b.F, b.F2, b.zl));
   // hard part (final_exp_cubed): t0 = f2^z conj(f2), t1 = t0^z conj(t0), a = t1^z frob(t1),
   // b = (a^z)^z frob^2(a) conj(a), c = f2^3, result b c
-  RET(ck_expz(0, G, gcnt, b.F2, b.F2, 0, 1, b.T0, b, st, latency));
-  RET(ck_expz(1, G, gcnt, b.T0, b.T0, 0, 1, b.T1, b, st, latency));
-  RET(ck_expz(2, G, gcnt, b.T1, b.T1, 1, 0, b.A, b, st, latency));
-  RET(ck_expz(3, G, gcnt, b.A, nullptr, 0, 0, b.T0, b, st, latency));
-  RET(ck_expz(4, G, gcnt, b.T0, b.A, 2, 0, b.T1, b, st, latency));
+  RET(ck_expz(0, G, gcnt, b.F2, b.F2, 0, 1, b.T0, b, st));
+  RET(ck_expz(1, G, gcnt, b.T0, b.T0, 0, 1, b.T1, b, st));
+  RET(ck_expz(2, G, gcnt, b.T1, b.T1, 1, 0, b.A, b, st));
+  RET(ck_expz(3, G, gcnt, b.A, nullptr, 0, 0, b.T0, b, st));
+  RET(ck_expz(4, G, gcnt, b.T0, b.A, 2, 0, b.T1, b, st));
   return launch("k_ck_final", k_ck_final, G, 64, st, G, gcnt, (const CkState*)b.st, (const Fp12*)b.T1,
                 (const Fp12*)b.A, (const Fp12*)b.F2, b.good);
+}
+// The checks b.st[0..G) of Recover's / VerifyPartial's passes (pair 0: (a, the lines rl[s R + round]), pair 1: (-g1, b))
+// -> b.good: the (-g1, b) lines, the Miller values (both pairs in one lane), the final exponentiation
+int run_checks(uint32_t G, uint32_t R, const CkLine* rl, const CkBufs& b, hipStream_t st) {
+  RET(launch("k_ck_lines2", k_ck_lines2, G, 64, st, G, (const uint32_t*)nullptr, (const CkState*)b.st, b.l2));
+  RET(launch("k_ck_miller", k_ck_miller, G, 64, st, G, (const uint32_t*)nullptr, R, (const CkState*)b.st, rl,
+             (const CkLine*)b.l2, b.F));
+  return run_final(G, nullptr, b, st, 0u);
 }
 // Recover's / VerifyPartial's group checks glist[4 + 4 (off + g)] of one pass (G <= CK_CHUNK): members and weighted
 // sums, the checks, the verdicts
@@ -1166,62 +1181,49 @@ int check_chunk(uint32_t G, uint32_t off, const uint32_t* glist, uint32_t k, uin
   RET(batch_inv(G, b.bn, b.bn + G, st));
   RET(launch("k_ck_bfin", k_ck_bfin, G, 64, st, G, (const uint8_t*)b.g2m, (const G2JStore*)b.bj, (const Fp*)(b.bn + G),
              hinf, b.st));
-  RET(run_checks(G, nullptr, R, rl, b, st));
+  RET(run_checks(G, R, rl, b, st));
   return launch("k_ck_verdict", k_ck_verdict, G, 128, st, G, (const CkState*)b.st, (const uint8_t*)b.good, status, fin);
 }
 
 // Cross-round isolation of a failed single-key batch (xr.h): items [i0, i0 + n) of the batch (its status, decoded S,
 // uncleared hashes Q, the group key keys[0]), two levels of group tests on the device, no host round trip; after a
-// passed batch every launch returns at once.  At most kXrSeg items per run, and the single checks of level 3 in chunks
-// of at most kXrL3Cap, each gated on its own device count: the per-check workspace (~45 KB a check) is sized for one
-// chunk, ~0.75 GB, instead of ~6 GB for every round of a 131072-round segment (round-5 advice).  At 1% bad rounds a
-// 100k-round batch lists ~15 k single checks: one chunk, sometimes two.  (A 100k-round batch on a fresh context: 3.9 GB
-// with chunks of 32768, tests/test_gpu_round5.py.)
+// passed batch every launch returns at once.  At most kXrSeg items per run; a check's workspace is ~5 KB (no line
+// table: k_xg_miller computes each pair's lines in the lane), so a segment's worst case -- every round a single check --
+// is ~0.7 GB, held once per tail stream.
 uint32_t xr_qpg() {  // quads per level-1 group (DG_XR_QPG: a test hook for the level shapes)
   static const uint32_t v = (uint32_t)std::max(1, std::min(64, env_int("DG_XR_QPG", (int)XR_QPG)));
-  return v;
-}
-constexpr uint32_t kXrL3Cap = 16384;
-uint32_t xr_l3cap() {  // DG_XR_L3CAP: a test hook (small chunks on small batches)
-  static const uint32_t v = (uint32_t)std::max(64, std::min((int)kXrL3Cap, env_int("DG_XR_L3CAP", (int)kXrL3Cap)));
   return v;
 }
 int xr_isolate(uint32_t i0, uint32_t n, const uint32_t* flag, const uint64_t* seed, const G1AStore* keys,
                const G2JStore* Q, const G2AStore* S, uint8_t* status, hipStream_t st) {
   const uint32_t qpg = xr_qpg(), nqmax = (n + 3) / 4, G1 = (nqmax + qpg - 1) / qpg;
-  const uint32_t C = std::min(n, xr_l3cap()), nch = (n + C - 1) / C, Gmax = std::max(G1, C);
   uint32_t *cnt, *cand, *l3;
   G2JStore *QS, *HS;
   uint4* T4;
   uint8_t* tinf;
-  CkLine* rl;
   CkBufs b;
-  RET(wsT(S_XR_CNT, XR_CHUNK0 + nch, &cnt));
+  RET(wsT(S_XR_CNT, XR_NCNT, &cnt));
   RET(wsT(S_XR_CAND, n, &cand));
   RET(wsT(S_XR_L3, n, &l3));
   RET(wsT(S_XR_QS, 2 * (size_t)nqmax, &QS));
   RET(wsT(S_XR_T4, (size_t)8 * RC_Q * 2 * nqmax, &T4));
   RET(wsT(S_XR_TINF, (size_t)8 * 2 * nqmax, &tinf));
-  RET(wsT(S_XR_HS, Gmax, &HS));
-  RET(wsT(S_XR_RL, (size_t)CK_STEPS * Gmax, &rl));
-  RET(ck_bufs(b, Gmax, false));
+  RET(wsT(S_XR_HS, n, &HS));
+  RET(ck_bufs(b, n, false, false));
   RET(launch("k_xg_sub", k_xg_sub, n, 64, st, i0, n, flag, S, status, cnt));
   RET(launch("k_xg_cand", k_xg_cand, n, 256, st, i0, n, flag, (const uint8_t*)status, cand, cnt));
   RET(launch("k_xq_sum", k_xq_sum, 2 * nqmax, 64, st, nqmax, qpg, seed, cnt, (const uint32_t*)cand, Q, S, T4, tinf, QS));
-  // one level of checks: G lanes gated on gcnt, level 3's rounds at lst
-  auto level = [&](uint32_t lv, uint32_t G, const uint32_t* gcnt, uint32_t* lst) -> int {
-    const uint32_t Gp = (G + 63) & ~63u;
-    RET(launch("k_xg_prep", k_xg_prep, G, 64, st, lv, G, gcnt, (const uint32_t*)cnt, qpg, (const uint32_t*)lst,
+  for (uint32_t level : {1u, 3u}) {
+    const uint32_t G = level == 1 ? G1 : n, Gp = (G + 63) & ~63u;
+    const uint32_t* gcnt = cnt + level;
+    RET(launch("k_xg_prep", k_xg_prep, G, 64, st, level, G, gcnt, (const uint32_t*)cnt, qpg, (const uint32_t*)l3,
                (const G2JStore*)QS, Q, S, keys, b.st, HS));
-    RET(launch("k_xg_lines", k_xg_lines, 2 * Gp, 64, st, G, gcnt, (const G2JStore*)HS, rl, b.st, b.l2));
-    RET(run_checks(G, gcnt, G, rl, b, st, true));
-    return launch("k_xg_verdict", k_xg_verdict, G, 128, st, lv, G, gcnt, qpg, cnt, (const uint8_t*)b.good,
-                  (const uint32_t*)cand, lst, status, g_ctx.xrcount);
-  };
-  RET(level(1, G1, cnt + 1, l3));
-  RET(launch("k_xg_split", k_xg_split, nch, 64, st, C, nch, cnt));
-  for (uint32_t j = 0; j < nch; ++j)
-    RET(level(3, std::min(C, n - j * C), cnt + XR_CHUNK0 + j, l3 + (size_t)j * C));
+    RET(launch("k_xg_heff", k_xg_heff, G, 64, st, G, gcnt, HS, b.st));
+    RET(launch("k_xg_miller", k_xg_miller, 2 * Gp, 64, st, G, gcnt, (const G2JStore*)HS, (const CkState*)b.st, b.F));
+    RET(run_final(G, gcnt, b, st, 1u));
+    RET(launch("k_xg_verdict", k_xg_verdict, G, 128, st, level, G, gcnt, qpg, cnt, (const uint8_t*)b.good,
+               (const uint32_t*)cand, l3, status, g_ctx.xrcount));
+  }
   return 0;
 }
 
@@ -1573,8 +1575,8 @@ int dg_init(int device) {
         {(const void*)k_ck_lines2, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_lines2, g1, b64, 0, q, 0u, cz, (const CkState*)nullptr, (CkLine*)nullptr); }},
         {(const void*)k_ck_miller, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_miller, g1, b64, 0, q, 0u, cz, 0u, (const CkState*)nullptr, (const CkLine*)nullptr, (const CkLine*)nullptr, (Fp12*)nullptr); }},
         {(const void*)k_ck_easy, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_easy, g1, b64, 0, q, 0u, cz, 0u, (const Fp12*)nullptr, (Fp12*)nullptr, (uint32_t*)nullptr); }},
-        {(const void*)k_ck_miller2, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_miller2, g1, b64, 0, q, 0u, cz, 0u, (const CkState*)nullptr, (const CkLine*)nullptr, (const CkLine*)nullptr, (Fp12*)nullptr); }},
-        {(const void*)k_xg_lines, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_lines, g1, b64, 0, q, 0u, cz, (const G2JStore*)nullptr, (CkLine*)nullptr, (CkState*)nullptr, (CkLine*)nullptr); }},
+        {(const void*)k_xg_miller, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_miller, g1, b64, 0, q, 0u, cz, (const G2JStore*)nullptr, (const CkState*)nullptr, (Fp12*)nullptr); }},
+        {(const void*)k_xg_heff, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_heff, g1, b64, 0, q, 0u, cz, (G2JStore*)nullptr, (CkState*)nullptr); }},
         {(const void*)k_ck_expsq2, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_expsq2, g1, b64, 0, q, 0u, cz, (const Fp12*)nullptr, (CycC*)nullptr, (Fp*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr); }},
         {(const void*)k_ck_expdec, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_expdec, g1, b64, 0, q, 0u, cz, (const CycC*)nullptr, (Fp*)nullptr, (const uint8_t*)nullptr, (const Fp12*)nullptr, 0u, 0u, (Fp12*)nullptr); }},
         {(const void*)k_ck_explain, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_explain, g1, b64, 0, q, cz, (const Fp12*)nullptr, (const Fp12*)nullptr, 0u, 0u, (Fp12*)nullptr); }},
@@ -1584,7 +1586,6 @@ int dg_init(int device) {
         {(const void*)k_xg_sub, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_sub, g1, b64, 0, q, 0u, 0u, cz, (const G2AStore*)nullptr, (uint8_t*)nullptr, z); }},
         {(const void*)k_xq_sum, [&](hipStream_t q) { hipLaunchKernelGGL(k_xq_sum, g1, b64, 0, q, 0u, 1u, (const uint64_t*)nullptr, z, cz, (const G2JStore*)nullptr, (const G2AStore*)nullptr, (uint4*)nullptr, (uint8_t*)nullptr, (G2JStore*)nullptr); }},
         {(const void*)k_xg_prep, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_prep, g1, b64, 0, q, 1u, 0u, cz, cz, 1u, cz, (const G2JStore*)nullptr, (const G2JStore*)nullptr, (const G2AStore*)nullptr, (const G1AStore*)nullptr, (CkState*)nullptr, (G2JStore*)nullptr); }},
-        {(const void*)k_xg_hlines, [&](hipStream_t q) { hipLaunchKernelGGL(k_xg_hlines, g1, b64, 0, q, 0u, cz, (const G2JStore*)nullptr, (CkLine*)nullptr, (CkState*)nullptr); }},
     };
     const std::vector<Warm> on_fb = {
         {(const void*)k_sign, [&](hipStream_t q) { hipLaunchKernelGGL(k_sign, g1, b128, 0, q, 0u, (const uint8_t*)nullptr, (const uint16_t*)nullptr, (const uint8_t*)nullptr, 0u, (const uint8_t*)nullptr, 0u, (uint8_t*)nullptr); }},
@@ -1837,9 +1838,17 @@ static int enqueue_beacons_dev(const uint8_t* pk48_host, size_t n, const uint64_
     HIPCHK(hipStreamWaitEvent(st, set.done, 0));
   }
   uint8_t* d_msgs;
+  if (g_bt.on) {
+    g_bt.v.push_back(BatchTrace{g_ctx.cur, bt_event(st), nullptr, nullptr});
+    g_bt.cur = &g_bt.v.back();
+  }
   RET(beacons_to_msgs(n, d_pr, d_r, d_ps, d_off, &d_msgs, st));
   RET(verify_single_key(pk48_host, (uint32_t)n, d_msgs, 32, d_sigs, d_status, fresh_seed(seed), st, set.tail));
   if (set.tail) st = set.tail;  // the batch ends on its tail stream
+  if (g_bt.cur) {
+    g_bt.cur->d = bt_event(st);
+    g_bt.cur = nullptr;
+  }
   HIPCHK(hipEventRecord(set.done, st));
   set.busy = true;
   g_ctx.last_stream = st;
@@ -1861,6 +1870,21 @@ static int wait_all() {
       x.busy = false;
     }
   if (g_ctx.timing) collect_timings();
+  if (!g_bt.v.empty()) {
+    HIPCHK(hipDeviceSynchronize());
+    fprintf(stderr, "[dg batch trace] set start hop done (ms from the first start)\n");
+    for (BatchTrace& b : g_bt.v) {
+      float ts = 0, th = 0, td = 0;
+      (void)hipEventElapsedTime(&ts, g_bt.v[0].s, b.s);
+      if (b.h) (void)hipEventElapsedTime(&th, g_bt.v[0].s, b.h);
+      (void)hipEventElapsedTime(&td, g_bt.v[0].s, b.d);
+      fprintf(stderr, "[dg batch trace] %d %.3f %.3f %.3f\n", b.set, ts, th, td);
+    }
+    for (BatchTrace& b : g_bt.v)  // (after the loop: the first start is every line's reference)
+      for (hipEvent_t e : {b.s, b.h, b.d})
+        if (e) (void)hipEventDestroy(e);
+    g_bt.v.clear();
+  }
   return 0;
 }
 

@@ -21,22 +21,21 @@
 //   k_xg_cand   the decoded rounds of a failed batch, compacted (nothing after a passed batch)
 //   k_xq_sum    per quad and side: sum rho_i P_i (P = Q or S) by the four-point sign-aligned column form over an affine
 //               8-entry table built in the lane (three levels of affine additions, one Fp inversion per level)
-//   per level:  k_xg_prep (the check's sums; sigma side affine), k_xg_lines (h_eff of the hash side and the 68 lines of
-//               both pairs), checks.h k_ck_miller2 .. k_ck_final (gated on the level's device count), k_xg_verdict
-//   k_xg_split  the level-3 list cut into chunks of at most `cap` checks (the count of each chunk)
-// The launches are sized for the worst case and gated on the device counts, so the host enqueues the whole isolation
-// without a round trip; after a passed batch every launch returns at once.  Level 3 runs in chunks of a fixed capacity
-// (drand_gpu.hip kXrL3Cap), each gated on its own count: its per-check workspace (~45 KB: the 68 lines of both pairs,
-// the Fp12 values) is sized for one chunk, not for every round of the batch.
+//   per level:  k_xg_prep (the check's sums; sigma side affine), k_xg_heff (h_eff of the hash side), k_xg_miller (both
+//               pairs' Miller values, their lines computed in the lane), checks.h k_ck_easy .. k_ck_final (gated on
+//               the level's device count), k_xg_verdict
+// The launches are sized for the worst case (every round bad: every round a single check) and gated on the device
+// counts, so the host enqueues the whole isolation without a round trip; after a passed batch every launch returns at
+// once.  A check's workspace is ~5 KB (its state and Fp12 values: no line table), ~0.7 GB for a 131072-round segment
+// (round 5 stored both pairs' lines, ~45 KB a check, ~6 GB a segment, per workspace set).
 #pragma once
 
 namespace dg {
 
 constexpr uint64_t XR_TAG = 0x63726f7373726e64ull;  // "crossrnd": domain of the cross-round weights rho_i
 constexpr uint32_t XR_QPG = 4;                       // quads per level-1 group (default; DG_XR_QPG, a test hook)
-// device counters: [0] candidates, [1] level-1 checks, [2] unused, [3] level-3 checks (rounds), then from XR_CHUNK0 the
-// check count of each level-3 chunk (k_xg_split)
-constexpr uint32_t XR_NCNT = 4, XR_CHUNK0 = 4;
+// device counters: [0] candidates, [1] level-1 checks, [2] unused, [3] level-3 checks (rounds)
+constexpr uint32_t XR_NCNT = 4;
 
 DGI uint64_t xr_rho(uint64_t seed, uint32_t i) { return rlc_coeff(seed ^ XR_TAG, i); }
 
@@ -145,49 +144,45 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xg_prep(uint32_t level, uin
   c.n = c.nl = 1;
   st[g] = c;
 }
-// H = h_eff(HS[g]) and its 68 lines rl[s G + g] (k_ck_round_lines with one "round" per check); np bit 0 when the pair
-// (a, H) has no identity
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_hlines(uint32_t G, const uint32_t* gcnt, const G2JStore* HS,
-                                                              CkLine* rl, CkState* st) {
+// H = h_eff(HS[g]) in place, affine (z = 1; the identity z = 0), and np bit 0 when neither H nor a is the identity --
+// a kernel of its own, so the cofactor clearing's registers do not add to the Miller loop's
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_heff(uint32_t G, const uint32_t* gcnt, G2JStore* HS, CkState* st) {
   DG_HI();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (ck_dead(g, G, gcnt)) return;
   const G2A h = g2_to_aff(g2_clear_cofactor(load_g2j(HS[g])));
-  if (h.inf || st[g].a.inf) return;
-  st[g].np |= 1u;
-  ck_lines(h.x, h.y, [&](uint32_t s, const CkLine& l) { rl[(size_t)s * G + g] = l; });
+  store_g2j(HS[g], h.inf ? G2J{fp2_zero(), fp2_zero(), fp2_zero()} : G2J{h.x, h.y, fp2_one()});
+  if (!h.inf && !st[g].a.inf) st[g].np |= 1u;
 }
-// k_xg_hlines and checks.h k_ck_lines2 in one launch, in waves of their own (lanes [0, Gp): the hash side, h_eff and
-// its lines into rl; [Gp, 2 Gp): the signature side's lines into l2, Gp = G rounded up to whole waves): the level's two
-// line chains run side by side instead of one after the other
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_lines(uint32_t G, const uint32_t* gcnt, const G2JStore* HS,
-                                                             CkLine* rl, CkState* st, CkLine* l2) {
+// The Miller value of one pair of check g, its lines computed in the lane (checks.h ck_miller1_fly): lanes [0, Gp) pair 0
+// = (a, H) with H = HS[g] from k_xg_heff, lanes [Gp, 2 Gp) pair 1 = (-g1, b), Gp = G rounded up to whole waves, so the
+// two chains run side by side; F[pair G + g] (k_ck_easy multiplies the two).  No line table: round 5 wrote both pairs'
+// 68 lines to HBM (k_xg_lines, 2 x 19.6 KB per check) for k_ck_miller2 to read back.
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_miller(uint32_t G, const uint32_t* gcnt, const G2JStore* HS,
+                                                              const CkState* st, Fp12* F) {
   DG_HI();
   const uint32_t Gp = (G + 63) & ~63u, lane = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t side = lane >= Gp ? 1u : 0u, g = lane - side * Gp;
+  const uint32_t pair = lane >= Gp ? 1u : 0u, g = lane - pair * Gp;
   if (ck_dead(g, G, gcnt)) return;
-  if (side) {
-    if (!(st[g].np & 2)) return;
-    const G2A b = load_g2a(st[g].b);
-    ck_lines(b.x, b.y, [&](uint32_t s, const CkLine& l) { l2[(size_t)s * G + g] = l; });
-    return;
+  Fp12 f = fp12_one();
+  if ((st[g].np >> pair) & 1) {
+    // pair 1: b at P = -g1; pair 0: H at P = a
+    const G2A q = pair ? load_g2a(st[g].b) : G2A{HS[g].x, HS[g].y, false};
+    const Fp px = pair ? fp_const(G1_GEN_X) : st[g].a.x, py = pair ? fp_const(G1_GEN_NEG_Y) : st[g].a.y;
+    f = ck_miller1_fly(q.x, q.y, px, py);
   }
-  const G2A h = g2_to_aff(g2_clear_cofactor(load_g2j(HS[g])));
-  if (h.inf || st[g].a.inf) return;
-  atomicOr(&st[g].np, 1u);
-  ck_lines(h.x, h.y, [&](uint32_t s, const CkLine& l) { rl[(size_t)s * G + g] = l; });
+  F[(size_t)pair * G + g] = f;
 }
 #else
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_lines(uint32_t G, const uint32_t* gcnt, const G2JStore* HS,
-                                                             CkLine* rl, CkState* st, CkLine* l2);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_miller(uint32_t G, const uint32_t* gcnt, const G2JStore* HS,
+                                                              const CkState* st, Fp12* F);
+DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_heff(uint32_t G, const uint32_t* gcnt, G2JStore* HS, CkState* st);
 DG_KERNEL void __launch_bounds__(64, DG_CK_SUB_WAVES) k_xg_sub(uint32_t i0, uint32_t n, const uint32_t* flag,
                                                                const G2AStore* S, uint8_t* status, uint32_t* cnt);
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES2) k_xg_prep(uint32_t level, uint32_t G, const uint32_t* gcnt,
                                                              const uint32_t* cnt, uint32_t qpg, const uint32_t* l3list,
                                                              const G2JStore* QS, const G2JStore* Q, const G2AStore* S,
                                                              const G1AStore* keys, CkState* st, G2JStore* HS);
-DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_hlines(uint32_t G, const uint32_t* gcnt, const G2JStore* HS,
-                                                              CkLine* rl, CkState* st);
 #endif
 #if DG_TU_CHECK == 5
 // lane 2 q + side (side 0: the hashes Q, side 1: the signatures S) of quad q = candidates [4 q, 4 q + 4): QS[2 q + side] =
@@ -271,14 +266,6 @@ DG_KERNEL void __launch_bounds__(128) k_xg_verdict(uint32_t level, uint32_t G, c
   const uint32_t c = cnt[0], j0 = 4 * g * qpg, j1 = j0 + 4 * qpg < c ? j0 + 4 * qpg : c;
   const uint32_t pos = atomicAdd(&cnt[3], j1 - j0);
   for (uint32_t j = j0; j < j1; ++j) l3list[pos + j - j0] = cand[j];
-}
-// the level-3 list (cnt[3] rounds) cut into nch chunks of at most cap checks: cnt[XR_CHUNK0 + j] = chunk j's count
-DG_KERNEL void __launch_bounds__(64) k_xg_split(uint32_t cap, uint32_t nch, uint32_t* cnt) {
-  DG_HI();
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= nch) return;
-  const uint32_t n = cnt[3], lo = j * cap;
-  cnt[XR_CHUNK0 + j] = n > lo ? (n - lo < cap ? n - lo : cap) : 0u;
 }
 #endif
 #endif

@@ -592,11 +592,22 @@ extern "C" int hc_ck_pipeline_check(const uint8_t* pk48, const uint8_t* q1_96, c
       if (!fp2_eq(*u[i], *v[i])) return 6;
     if (g_fd_bad) return 7;
   }
-  // k_ck_miller2: each pair in a lane of its own (its own squarings), the two values multiplied by k_ck_easy
+  // each pair in a lane of its own (its own squarings; xr.h k_xg_miller), the two values multiplied by k_ck_easy
   const Fp12 m0 = (np & 1) ? ck_miller1(p1.x, p1.y, [&](uint32_t s) { return l1[s]; }) : fp12_one();
   const Fp12 m1 = (np & 2) ? ck_miller1(fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), [&](uint32_t s) { return l2[s]; })
                            : fp12_one();
   const Fp12 f01 = fp12_mul(m0, m1);
+  {
+    // xr.h k_xg_miller: each pair's lines computed in the lane (ck_miller1_fly), the same values as from the tables
+    const Fp12 w0 = (np & 1) ? ck_miller1_fly(q1.x, q1.y, p1.x, p1.y) : fp12_one();
+    const Fp12 w1 = (np & 2) ? ck_miller1_fly(q2.x, q2.y, fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y)) : fp12_one();
+    const Fp2* u[12] = {&m0.c0.c0, &m0.c0.c1, &m0.c0.c2, &m0.c1.c0, &m0.c1.c1, &m0.c1.c2,
+                        &m1.c0.c0, &m1.c0.c1, &m1.c0.c2, &m1.c1.c0, &m1.c1.c1, &m1.c1.c2};
+    const Fp2* v[12] = {&w0.c0.c0, &w0.c0.c1, &w0.c0.c2, &w0.c1.c0, &w0.c1.c1, &w0.c1.c2,
+                        &w1.c0.c0, &w1.c0.c1, &w1.c0.c2, &w1.c1.c0, &w1.c1.c1, &w1.c1.c2};
+    for (int i = 0; i < 12; ++i)
+      if (!fp2_eq(*u[i], *v[i])) return 8;
+  }
   {
     const Fp2* u[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
     const Fp2* v[6] = {&f01.c0.c0, &f01.c0.c1, &f01.c0.c2, &f01.c1.c0, &f01.c1.c1, &f01.c1.c2};

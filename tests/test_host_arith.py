@@ -321,7 +321,8 @@ def test_karabina_exponentiation_matches_granger_scott(hc):
 
 def test_check_pipeline_matches_pair_check(hc):
     """Recover's pairing-check pipeline (checks.h: per-round lines without the G1 point, the Miller value from two
-    line tables -- also as two single-pair values multiplied, k_ck_miller2 -- the final exponentiation with in-lane
+    line tables -- also as two single-pair values multiplied, with the lines from the tables and computed in the lane
+    (ck_miller1_fly, the isolation's k_xg_miller) -- the final exponentiation with in-lane
     inversions, the compressed chains and the fused next factors) equals
     final_exp_cubed(miller_loop<2>) on the host: valid and invalid (key, H, sigma) triples of the golden chain, each
     pair dropped alone (np = 1, 2) and both.  k_ck_miller's digit-form loop (fpd.h ck_miller_d) must give the same
