@@ -481,8 +481,8 @@ def recover_bench(L, tbls, shard, src, R_total, t, n, world, rank, peak, steps=2
 def make_c5_inputs(tbls, shard, src, R_total, world, rank, t=129, n=256, frac=0.10, n_short=3):
     """configs[4]'s inputs for this rank's contiguous range of R_total rounds: n partials per round signed by the
     GPU (dg_sign), ~frac of the (round, share) cells corrupted with the six modes of tools/corrupt.py (pattern of the
-    GLOBAL round numbers), `n_short` rounds with too few valid shares.  Returns (pub, msgs, parts, bad, short, items,
-    gen_s, a, b)."""
+    GLOBAL round numbers), `n_short` rounds with too few valid shares.  Returns (pub, commits, msgs, parts, bad, short,
+    items, gen_s, a, b)."""
     from tools import corrupt
 
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "groups.json")))["t%d" % t]
@@ -515,7 +515,7 @@ def make_c5_inputs(tbls, shard, src, R_total, world, rank, t=129, n=256, frac=0.
     bad = np.zeros((R, n), dtype=bool)
     for r, j, _ in items:
         bad[r, j] = True
-    return pub, msgs, parts, bad, short, items, gen_s, a, b
+    return pub, commits, msgs, parts, bad, short, items, gen_s, a, b
 
 
 def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=256, frac=0.10, n_short=3, vp_neg=True):
@@ -528,8 +528,8 @@ def adversarial_bench(L, tbls, shard, src, R_total, world, rank, peak, t=129, n=
     the all-gather of the outputs.  Checked without the CPU: recovered signatures equal the chain's, exactly the short rounds
     report NOT_ENOUGH, every examined corrupted share is rejected and every examined clean one accepted
     (per-share parity with the CPU twin is tests/test_gpu_parity.py's job)."""
-    pub, msgs, parts, bad, short, items, gen_s, a, b = make_c5_inputs(tbls, shard, src, R_total, world, rank, t, n,
-                                                                    frac, n_short)
+    pub, commits, msgs, parts, bad, short, items, gen_s, a, b = make_c5_inputs(tbls, shard, src, R_total, world, rank,
+                                                                             t, n, frac, n_short)
     R = b - a
     import torch
 

@@ -73,8 +73,9 @@ struct CkState {
   uint32_t live[CK_GRP];  // the live members' item indices
 };
 
-// pairing.h line_dbl / line_add with c1, c4 left unscaled by P
-DGI void ck_line_dbl(G2Proj& T, CkLine& l) {
+// pairing.h line_dbl / line_add with c1, c4 left unscaled by P (T: a G2Proj, or an LDS slot with the same x, y, z)
+template <class P>
+DGI void ck_line_dbl(P& T, CkLine& l) {
   const Fp2 a = fp2_mul_fp(fp2_mul(T.x, T.y), fp_const(FP_TWO_INV));
   const Fp2 b = fp2_sqr(T.y);
   const Fp2 c = fp2_sqr(T.z);
@@ -91,7 +92,8 @@ DGI void ck_line_dbl(G2Proj& T, CkLine& l) {
   T.y = fp2_sub(fp2_sqr(g), fp2_add(fp2_dbl(e2), e2));
   T.z = fp2_mul(b, h);
 }
-DGI void ck_line_add(G2Proj& T, const Fp2& qx, const Fp2& qy, CkLine& l) {
+template <class P>
+DGI void ck_line_add(P& T, const Fp2& qx, const Fp2& qy, CkLine& l) {
   const Fp2 theta = fp2_sub(T.y, fp2_mul(qy, T.z));
   const Fp2 lambda = fp2_sub(T.x, fp2_mul(qx, T.z));
   const Fp2 c = fp2_sqr(theta);
@@ -192,18 +194,28 @@ DGI Fp12 ck_miller1(const Fp& px, const Fp& py, Line line) {
 // ck_miller1 with the pair's lines computed in the lane from Q (affine, not the identity) as the loop runs: no line table.
 // The isolation's checks (xr.h k_xg_miller) have no per-round line sharing, so storing each check's 68 lines to HBM
 // for a second kernel bought nothing but 19.6 KB per pair of workspace and a launch
-DGI Fp12 ck_miller1_fly(const Fp2& qx, const Fp2& qy, const Fp& px, const Fp& py) {
-  G2Proj T{qx, qy, fp2_one()};
+// (T: the running point's storage, an LDS slot on the device -- out of the register file beside the Fp12 accumulator;
+// q(): Q again, for the five addition steps, instead of keeping it live)
+template <class LoadQ, class Slot>
+DGI Fp12 ck_miller1_fly(LoadQ q, const Fp& px, const Fp& py, Slot& T) {
+  {
+    const G2A q0 = q();
+    T.x = q0.x;
+    T.y = q0.y;
+    T.z = fp2_one();
+  }
   Fp12 f = fp12_one();
 #pragma unroll 1
   for (uint32_t s = 0; s < CK_STEPS; ++s) {
     const bool dbl = ck_step_is_dbl(s);
     if (s != 0 && dbl) f = fp12_sqr(f);
     CkLine l;
-    if (dbl)
+    if (dbl) {
       ck_line_dbl(T, l);
-    else
-      ck_line_add(T, qx, qy, l);
+    } else {
+      const G2A qa = q();
+      ck_line_add(T, qa.x, qa.y, l);
+    }
     f = fp12_mul_014(f, l.c0, fp2_mul_fp(l.c1, px), fp2_mul_fp(l.c4, py));
   }
   return fp12_conj(f);

@@ -1425,7 +1425,11 @@ int recover_msm(uint32_t R, uint32_t k, uint32_t t, uint32_t U, const uint32_t* 
   RET(wsT(S_RC_PINF, nel, &pinf));
   RET(wsT(S_RC_DEN, 2 * nel, &den));
   dinv = den + nel;
-  RET(wsT(S_RC_A, (size_t)4 * Ru, &A));
+  // share subsets per (component, block): the blocks' 4 U one-wave workgroups alone leave the chip idle when U is small
+  // (the live round: one block, ~430 dependent point operations in one lane, 7 ms); each subset runs the doubling
+  // chain again, so only while 4 U nsplit stays under ~one wave per SIMD
+  const uint32_t nsplit = std::max(1u, std::min({8u, t, 1024u / (4 * U)}));
+  RET(wsT(S_RC_A, (size_t)4 * nsplit * Ru, &A));
   RET(launch("k_rc_digits", k_rc_digits, U * RC_BLK, RC_BLK, st, U, t, maxev, ub, ref, d_selidx, naf, ev, hdr));
   for (uint32_t l = 0; l < RC_TAB; ++l) {
     RET(launch("k_rc_tab_den", k_rc_tab_den, (uint32_t)nel, 128, st, l, R, Ru, k, t, ub, d_rst, d_sel, d_S,
@@ -1434,9 +1438,9 @@ int recover_msm(uint32_t R, uint32_t k, uint32_t t, uint32_t U, const uint32_t* 
     RET(launch("k_rc_tab_add", k_rc_tab_add, (uint32_t)nel, 128, st, l, R, Ru, k, t, ub, d_rst, d_sel, d_S, T4, D4,
                (const uint8_t*)pinf, (const Fp*)dinv));
   }
-  RET(launch("k_rc_straus", k_rc_straus, 4 * Ru, 64, st, R, Ru, maxev, ub, d_rst, (const uint32_t*)ev,
-             (const uint32_t*)hdr, (const uint4*)T4, (const uint8_t*)pinf, A));
-  return launch("k_rc_combine", k_rc_combine, Ru, 128, st, R, Ru, ub, d_rst, (const G2JStore*)A, out);
+  RET(launch("k_rc_straus", k_rc_straus, 4 * Ru * nsplit, 64, st, R, Ru, maxev, ub, d_rst, (const uint32_t*)ev,
+             (const uint32_t*)hdr, (const uint4*)T4, (const uint8_t*)pinf, A, nsplit));
+  return launch("k_rc_combine", k_rc_combine, Ru, 128, st, R, Ru, ub, d_rst, (const G2JStore*)A, out, nsplit);
 }
 
 // Recover after the VerifyPartial statuses are known (d_st): per round the first t valid partials, xyCommit
@@ -1569,7 +1573,7 @@ int dg_init(int device) {
     };
     const dim3 g1(1), b64(64), b128(128);
     const std::vector<Warm> on_sets = {
-        {(const void*)k_rc_combine, [&](hipStream_t q) { hipLaunchKernelGGL(k_rc_combine, g1, b128, 0, q, 0u, 0u, (const uint32_t*)nullptr, (const uint8_t*)nullptr, (const G2JStore*)nullptr, (G2JStore*)nullptr); }},
+        {(const void*)k_rc_combine, [&](hipStream_t q) { hipLaunchKernelGGL(k_rc_combine, g1, b128, 0, q, 0u, 0u, (const uint32_t*)nullptr, (const uint8_t*)nullptr, (const G2JStore*)nullptr, (G2JStore*)nullptr, 1u); }},
         {(const void*)k_ck_prep, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_prep, g1, b64, 0, q, 0u, 0u, cz, 1u, (const uint64_t*)nullptr, (const G1AStore*)nullptr, cz, (const uint8_t*)nullptr, (const G2AStore*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr, 0u, g_ctx.gcount, (CkState*)nullptr, (uint8_t*)nullptr, (RsDigits*)nullptr); }},
         {(const void*)k_ck_round_lines, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_round_lines, g1, b64, 0, q, 0u, (const G2JStore*)nullptr, (CkLine*)nullptr, (uint8_t*)nullptr); }},
         {(const void*)k_ck_lines2, [&](hipStream_t q) { hipLaunchKernelGGL(k_ck_lines2, g1, b64, 0, q, 0u, cz, (const CkState*)nullptr, (CkLine*)nullptr); }},

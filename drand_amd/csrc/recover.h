@@ -272,16 +272,23 @@ DG_KERNEL void __launch_bounds__(64) k_rc_digits(uint32_t U, uint32_t t, uint32_
   }
 }
 
-// per round r of a uniform block: sigma = A0 - psi(A1) + psi^2(A2) - psi^3(A3) into out[r] (A: 4 x Ru, rounds in
-// uniform-block order); rounds without status OK are left alone (k_compress_g2 writes zeros for them)
+// per round r of a uniform block: sigma = A0 - psi(A1) + psi^2(A2) - psi^3(A3) into out[r] (A: nsplit x 4 x Ru, the
+// share subsets' parts of each A_i summed first; rounds in uniform-block order); rounds without status OK are left
+// alone (k_compress_g2 writes zeros for them)
 DG_KERNEL void __launch_bounds__(128, DG_BULK_WAVES) k_rc_combine(uint32_t R, uint32_t Ru, const uint32_t* ub,
-                                                                  const uint8_t* rst, const G2JStore* A, G2JStore* out) {
+                                                                  const uint8_t* rst, const G2JStore* A, G2JStore* out,
+                                                                  uint32_t nsplit) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= Ru) return;
   const uint32_t r = ub[u / RC_BLK] * RC_BLK + u % RC_BLK;
   if (r >= R || rst[r] != DG_ST_OK_) return;
-  store_g2j(out[r], rc_combine(load_g2j(A[u]), load_g2j(A[(size_t)Ru + u]), load_g2j(A[2 * (size_t)Ru + u]),
-                               load_g2j(A[3 * (size_t)Ru + u])));
+  auto part = [&](uint32_t i) {
+    G2J a = load_g2j(A[(size_t)i * Ru + u]);
+#pragma unroll 1
+    for (uint32_t s = 1; s < nsplit; ++s) a = jac_add(a, load_g2j(A[((size_t)s * 4 + i) * Ru + u]));
+    return a;
+  };
+  store_g2j(out[r], rc_combine(part(0), part(1), part(2), part(3)));
 }
 #endif
 
@@ -342,14 +349,17 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_rc_tab_add(uint32_t l, uin
   }
 }
 
-// One 64-lane workgroup per (component i, uniform block): lane = round of the block; A_i of the round by the
-// block's schedule (wave-uniform: scalar loads, uniform branches), the running point in LDS (g2_madd_lds /
-// g2_dbl_lds: the register file holds one table entry and one formula's temporaries).
+// One 64-lane workgroup per (component i, uniform block, share subset s < nsplit): lane = round of the block; the
+// part of A_i from the shares j = s mod nsplit by the block's schedule (wave-uniform: scalar loads, uniform branches;
+// every subset runs the whole doubling chain), the running point in LDS (g2_madd_lds / g2_dbl_lds: the register file
+// holds one table entry and one formula's temporaries); A[(s 4 + i) Ru + u], summed by k_rc_combine.  nsplit > 1 when
+// the blocks are too few to fill the chip (the live round: one block, whose ~430 dependent point operations took 7 ms
+// in one lane; drand_gpu.hip recover_msm)
 DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rc_straus(uint32_t R, uint32_t Ru, uint32_t maxev, const uint32_t* ub,
                                                                  const uint8_t* rst, const uint32_t* ev,
                                                                  const uint32_t* hdr, const uint4* T4,
-                                                                 const uint8_t* pinf, G2JStore* A) {
-  const uint32_t U = Ru / RC_BLK, w = blockIdx.x, i = w / U, ubk = w % U;  // uniform
+                                                                 const uint8_t* pinf, G2JStore* A, uint32_t nsplit) {
+  const uint32_t U = Ru / RC_BLK, s = blockIdx.x % nsplit, w = blockIdx.x / nsplit, i = w / U, ubk = w % U;  // uniform
   const uint32_t u = ubk * RC_BLK + threadIdx.x, r = ub[ubk] * RC_BLK + threadIdx.x;
   const bool live = r < R && rst[r] == DG_ST_OK_;
   const uint32_t* e = ev + ((size_t)ubk * 4 + i) * maxev;
@@ -363,14 +373,14 @@ DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rc_straus(uint32_t R, uin
     const uint32_t v = e[q];
     for (uint32_t d = rc_ev_dbl(v); d > 0; --d) g2_dbl_lds(acc);
     const uint32_t j = rc_ev_j(v);
-    if (live && !pinf[(size_t)j * Ru + u]) {
+    if (live && j % nsplit == s && !pinf[(size_t)j * Ru + u]) {
       Fp2 x, y;
       rc_ld(T4 + ((size_t)j * RC_TAB + rc_ev_e(v)) * RC_Q * Ru + u, Ru, x, y);
       g2_madd_lds(acc, x, rc_ev_neg(v) ? fp2_neg(y) : y);
     }
   }
   for (uint32_t d = tail; d > 0; --d) g2_dbl_lds(acc);
-  if (live) A[(size_t)i * Ru + u] = acc;
+  if (live) A[((size_t)s * 4 + i) * Ru + u] = acc;
 }
 #elif defined(__HIP__)
 DG_KERNEL void __launch_bounds__(128) k_rc_tab_den(uint32_t l, uint32_t R, uint32_t Ru, uint32_t k, uint32_t t,
@@ -384,7 +394,7 @@ DG_KERNEL void __launch_bounds__(128, DG_HOT_WAVES) k_rc_tab_add(uint32_t l, uin
 DG_KERNEL void __launch_bounds__(64, DG_TERMS_WAVES) k_rc_straus(uint32_t R, uint32_t Ru, uint32_t maxev, const uint32_t* ub,
                                                                  const uint8_t* rst, const uint32_t* ev,
                                                                  const uint32_t* hdr, const uint4* T4,
-                                                                 const uint8_t* pinf, G2JStore* A);
+                                                                 const uint8_t* pinf, G2JStore* A, uint32_t nsplit);
 #endif
 
 // ---------------------------------------------------------------------------------------------------

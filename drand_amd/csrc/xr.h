@@ -163,13 +163,14 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_xg_miller(uint32_t G, const 
   DG_HI();
   const uint32_t Gp = (G + 63) & ~63u, lane = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t pair = lane >= Gp ? 1u : 0u, g = lane - pair * Gp;
+  __shared__ G2JStore s_T[64];
   if (ck_dead(g, G, gcnt)) return;
   Fp12 f = fp12_one();
   if ((st[g].np >> pair) & 1) {
     // pair 1: b at P = -g1; pair 0: H at P = a
-    const G2A q = pair ? load_g2a(st[g].b) : G2A{HS[g].x, HS[g].y, false};
+    const auto q = [&]() { return pair ? load_g2a(st[g].b) : G2A{HS[g].x, HS[g].y, false}; };
     const Fp px = pair ? fp_const(G1_GEN_X) : st[g].a.x, py = pair ? fp_const(G1_GEN_NEG_Y) : st[g].a.y;
-    f = ck_miller1_fly(q.x, q.y, px, py);
+    f = ck_miller1_fly(q, px, py, s_T[threadIdx.x]);
   }
   F[(size_t)pair * G + g] = f;
 }

@@ -599,8 +599,10 @@ extern "C" int hc_ck_pipeline_check(const uint8_t* pk48, const uint8_t* q1_96, c
   const Fp12 f01 = fp12_mul(m0, m1);
   {
     // xr.h k_xg_miller: each pair's lines computed in the lane (ck_miller1_fly), the same values as from the tables
-    const Fp12 w0 = (np & 1) ? ck_miller1_fly(q1.x, q1.y, p1.x, p1.y) : fp12_one();
-    const Fp12 w1 = (np & 2) ? ck_miller1_fly(q2.x, q2.y, fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y)) : fp12_one();
+    G2Proj T;
+    const Fp12 w0 = (np & 1) ? ck_miller1_fly([&]() { return q1; }, p1.x, p1.y, T) : fp12_one();
+    const Fp12 w1 =
+        (np & 2) ? ck_miller1_fly([&]() { return q2; }, fp_const(G1_GEN_X), fp_const(G1_GEN_NEG_Y), T) : fp12_one();
     const Fp2* u[12] = {&m0.c0.c0, &m0.c0.c1, &m0.c0.c2, &m0.c1.c0, &m0.c1.c1, &m0.c1.c2,
                         &m1.c0.c0, &m1.c0.c1, &m1.c0.c2, &m1.c1.c0, &m1.c1.c1, &m1.c1.c2};
     const Fp2* v[12] = {&w0.c0.c0, &w0.c0.c1, &w0.c0.c2, &w0.c1.c0, &w0.c1.c1, &w0.c1.c2,

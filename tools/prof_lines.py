@@ -39,7 +39,7 @@ def main():
     else:
         R, t, n = a.rounds or 10000, 129, 256
         src = bench.RoundSource(tbls, R + 1)
-        pub, msgs, parts, _, _, _, _, _, _ = bench.make_c5_inputs(tbls, shard, src, R, 1, 0, t, n)
+        pub, _, msgs, parts, _, _, _, _, _, _ = bench.make_c5_inputs(tbls, shard, src, R, 1, 0, t, n)
     d_msgs = torch.from_numpy(np.ascontiguousarray(msgs)).to(dev)
     d_parts = torch.from_numpy(np.ascontiguousarray(parts)).to(dev)
     if a.line in ("c3", "c5"):
