@@ -12,7 +12,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6prof
 mkdir -p $O
 export TMPDIR=/tmp
-HEAD="--gpus 1 --steps 20 --warmup 5 --recover-rounds 0 --c5-rounds 0 --sync-rounds 0 --no-c1 --no-cpu-baseline --neg-steps 0 --no-peak-detail --tables-out $O/tables.json"
+HEAD="--gpus 1 --warmup 5 --recover-rounds 0 --c5-rounds 0 --sync-rounds 0 --no-c1 --no-cpu-baseline --neg-steps 0 --no-peak-detail --tables-out $O/tables.json"
 cd /tmp
 run() {  # name limit args...
   local name=$1 lim=$2
@@ -22,7 +22,7 @@ run() {  # name limit args...
 }
 for p in ${PASSES:-trace stats pmc}; do case $p in
 trace)
-  run trace 300 --kernel-trace --output-format csv -d $O/trace -o run -- python3 $R/bench.py $HEAD --no-kernel-timing
+  run trace 300 --kernel-trace --output-format csv -d $O/trace -o run -- python3 $R/bench.py $HEAD --steps 20 --no-kernel-timing
   f=$(find $O/trace -name "*kernel_trace.csv" | head -1)
   python3 - "$f" $O/head_trace.csv <<'PY'
 import csv, sys
@@ -38,7 +38,7 @@ print(len(rows), "dispatches")
 PY
   rm -rf $O/trace;;
 stats)
-  run stats_async 300 --kernel-trace --stats --output-format csv -d $O/stats_async -o run -- python3 $R/bench.py $HEAD
+  run stats_async 300 --kernel-trace --stats --output-format csv -d $O/stats_async -o run -- python3 $R/bench.py $HEAD --steps 20
   run stats_sync 300 --kernel-trace --stats --output-format csv -d $O/stats_sync -o run -- python3 $R/bench.py $HEAD --sync --steps 10
   for l in c3 c5; do
     run stats_$l 300 --kernel-trace --stats --output-format csv -d $O/stats_$l -o run -- python3 $R/tools/prof_lines.py $l --calls 2
@@ -51,8 +51,13 @@ pmc)
   for cfg in ${CONFIGS:-c3 c3vp c5vp}; do
     for ctr in FETCH_SIZE WRITE_SIZE; do
       echo "[profile] pmc $cfg $ctr" >&2
+      case $cfg in
+        head) CMD="$R/bench.py $HEAD --sync --steps 1 --warmup 1";;
+        c2neg) CMD="$R/bench.py $HEAD --steps 1 --warmup 1 --neg-steps 2";;
+        *) CMD="$R/tools/prof_lines.py $cfg";;
+      esac
       timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $O/pmc_${cfg}_$ctr -o run -- \
-        python3 $R/tools/prof_lines.py $cfg > $O/pmc_${cfg}_$ctr.log 2>&1 \
+        python3 $CMD > $O/pmc_${cfg}_$ctr.log 2>&1 \
         || { echo "pmc $cfg $ctr failed"; tail -5 $O/pmc_${cfg}_$ctr.log; exit 1; }
     done
   done
