@@ -95,6 +95,7 @@ struct Set {
   // batch's few-workgroup tail no longer holds one of the 4 queues the bulk kernels share.  hop: the set stream's
   // bulk part done (the tail stream waits for it).
   hipStream_t tail = nullptr;
+  int tail_idx = -1;  // which of Ctx::tails (and of Ctx::xr_pools: the sets sharing a tail stream share its pool)
   hipEvent_t hop = nullptr;
 };
 
@@ -117,7 +118,7 @@ struct Ctx {
   hipStream_t kc_stream = nullptr;
   hipEvent_t kc_fork = nullptr, kc_join = nullptr;
   static constexpr int kTails = 4;
-  hipStream_t tails[kTails] = {};  // high-priority streams, set i -> tails[i % ntails] (DG_TAIL=0: none)
+  hipStream_t tails[kTails] = {};  // high-priority streams, by rotation position (Set::tail_idx; DG_TAIL=0: none)
   int ntails = 0;
   // the cross-round isolation's workspace (xr.h: ~0.8 GB at its capacity) per TAIL stream, not per set: the sets that
   // share a tail stream run their isolations one after another in that stream's order, so they can share its buffers
@@ -271,10 +272,23 @@ int ws(Slot s, size_t bytes, void** out) {
   return 0;
 }
 
+// The order in which batches take the workspace sets.  HIP binds the set streams to its hardware queues as they first
+// dispatch (dg_init's prewarm, sets 0, 1, 2, ...), and at 4 queues the binding zigzags: sets 0..7 on queues 1, 2, 3, 4,
+// 4, 3, 2, 1.  Taking the sets in index order sent batches 3, 4 to queue 4 and 7, 0 to queue 1, so a
+// window of 20 batches gave queue 4 six heads and queue 1 four, and the region waited for queue 4 alone at its end
+// (DESIGN.md §5.5).  With 8 sets on 4 queues the order 0, 1, 2, 3, 7, 6, 5, 4 visits queues 1, 2, 3, 4, 1, 2, 3, 4:
+// every window of batches is spread over the queues to within one.  DG_SET_ORDER=0: index order (A/B).
+int set_at(int slot) {
+  static const bool zigzag = env_int("DG_SET_ORDER", 1) != 0;
+  const int n = active_sets();
+  if (!zigzag || n != 8 || env_hw_queues() != 4) return slot;
+  static const int order[8] = {0, 1, 2, 3, 7, 6, 5, 4};
+  return order[slot];
+}
 // Take the next workspace set (waiting for the batch still using it) and make it current.
 int acquire_set(hipStream_t* st) {
   Ctx& c = g_ctx;
-  int i = c.next;
+  const int i = set_at(c.next);
   c.next = (c.next + 1) % active_sets();
   Set& s = c.sets[i];
   if (s.busy) {
@@ -789,7 +803,7 @@ int batch_verify(const Batch& b, uint64_t seed_in, hipStream_t st, BatchOut* out
     struct PoolGuard {
       explicit PoolGuard(int p) { g_ctx.xr_pool = p; }
       ~PoolGuard() { g_ctx.xr_pool = -1; }
-    } guard(tst && g_ctx.ntails ? g_ctx.cur % g_ctx.ntails : -1);
+    } guard(tst ? cur_set().tail_idx : -1);
     for (uint32_t i0 = 0; i0 < N; i0 += kXrSeg)
       RET(xr_isolate(i0, std::min(kXrSeg, N - i0), flag, seed, b.keys, b.Q, b.S, b.status, st));
   } else {
@@ -1534,7 +1548,14 @@ int dg_init(int device) {
     for (int i = 0; i < g_ctx.ntails; ++i)
       HIPCHK(hipStreamCreateWithPriority(&g_ctx.tails[i], hipStreamNonBlocking, greatest_prio));
   }
-  for (int i = 0; i < kSets; ++i) g_ctx.sets[i].tail = g_ctx.ntails ? g_ctx.tails[i % g_ctx.ntails] : nullptr;
+  // the tail stream of a set by its position in the rotation (set_at), so the batches of one round of concurrent heads
+  // -- consecutive positions -- end on different tail streams: with set i -> tail i mod 4 and the zigzag order, sets 3
+  // and 7 (and 0 and 4) shared a tail stream within a round, and the second's tail waited ~12 ms for the first's
+  for (int k = 0; k < kSets; ++k) {
+    const int i = k < active_sets() ? set_at(k) : k;
+    g_ctx.sets[i].tail_idx = g_ctx.ntails ? k % g_ctx.ntails : -1;
+    g_ctx.sets[i].tail = g_ctx.ntails ? g_ctx.tails[k % g_ctx.ntails] : nullptr;
+  }
   if (!g_ctx.fb_stream) HIPCHK(hipStreamCreateWithFlags(&g_ctx.fb_stream, hipStreamNonBlocking));
   // the keyed batches' side stream: a high-priority stream like the tails (a queue of its own beside the 4 normal ones,
   // so its fork / join waits stall no set stream), created here rather than on the first keyed batch

@@ -180,9 +180,9 @@ int dg_queue_plan(int hw_queues, int* sets, int* per_item_on_set_streams);
  * stream).  Work the caller enqueues there runs after that batch with no cross-stream wait: with fewer
  * hardware queues than streams (GPU_MAX_HW_QUEUES, HIP's default 4) a wait queued on a shared queue holds every stream
  * behind it, so a short consumer of one batch's statuses (a bitmap pack, an all-gather, a copy) is cheapest on this
- * stream.  The stream is SHARED and HIGH PRIORITY: the library has 4 tail streams, set i ends on tail i mod 4, so the
- * batch two sets later ends on the same one, and whatever the caller enqueues there runs at high priority and ahead of
- * that later batch's tail (its Miller loops, final exponentiation and isolation).  Keep it short; for long work record
+ * stream.  The stream is SHARED and HIGH PRIORITY: the library has 4 tail streams and consecutive batches end on
+ * different ones, so the batch four batches later ends on the same one, and whatever the caller enqueues there runs
+ * at high priority and ahead of that later batch's tail (its Miller loops, final exponentiation and isolation).  Keep it short; for long work record
  * an event here and wait for it on a stream of the caller's.  The stream stays owned by the library (valid until
  * dg_shutdown); DG_E_ARG before the first asynchronous batch.  (No reference counterpart: drand verifies beacons one
  * at a time, beacon/chain.go:65-71.) */
