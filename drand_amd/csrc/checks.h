@@ -154,27 +154,27 @@ DGI Fp12 ck_miller(uint32_t np, const Fp& ax, const Fp& ay, Line line) {
   return fp12_conj(f);
 }
 
-// ck_miller with the accumulator and the line values in digit form through the whole loop (fpd.h): converted from the
-// 12-limb lines as they are read and back once at the end -- the same value (tests/native/hostcheck.cpp)
-#ifndef DG_CK_MILLER_D
-#define DG_CK_MILLER_D 0  // 1: measured 7% slower (k_ck_miller 678 -> 728 ms per C5 run: 213+ spilled VGPRs), DESIGN.md §8
-#endif
-template <class Line>
-DGI Fp12 ck_miller_d(uint32_t np, const Fp& ax, const Fp& ay, Line line) {
+// ck_miller with the accumulator and the line values in digit form through the whole loop (fpd.h), the accumulator in a
+// column outside the register file (Fd12Col: k_ck_miller's LDS): the lines converted as they are read, the accumulator
+// back once at the end -- the same value (tests/native/hostcheck.cpp, the digit-form bounds asserted).  17 spilled
+// VGPRs against 36 for ck_miller and 213-430 for the digit form with the accumulator in registers; 1% faster than
+// ck_miller (k_ck_miller 24.1 -> 23.8 ms per C5 launch)
+template <class Line, class C>
+DGI Fp12 ck_miller_col(uint32_t np, const Fp& ax, const Fp& ay, Line line, C& f) {
   if (!np) return fp12_one();
   const Fp gx = fp_const(G1_GEN_X), gy = fp_const(G1_GEN_NEG_Y);
-  Fd12 f = fd12_one();
+  f.set_one();
 #pragma unroll 1
   for (uint32_t it = 0; it < 2 * CK_STEPS; ++it) {
     const uint32_t s = it >> 1, pair = it & 1;
-    if (pair == 0 && s != 0 && ck_step_is_dbl(s)) f = fd12_sqr(f);
+    if (pair == 0 && s != 0 && ck_step_is_dbl(s)) fd12_sqr_col(f);
     if ((np >> pair) & 1) {
       const CkLine l = line(s, pair);
       const Fd px = fd_from(fp_sel(pair != 0, ax, gx)), py = fd_from(fp_sel(pair != 0, ay, gy));
-      f = fd12_mul_014(f, fd2_from(l.c0), fd2_mul_fp(fd2_from(l.c1), px), fd2_mul_fp(fd2_from(l.c4), py));
+      fd12_mul_014_col(f, fd2_from(l.c0), fd2_mul_fp(fd2_from(l.c1), px), fd2_mul_fp(fd2_from(l.c4), py));
     }
   }
-  return fp12_conj(fd12_to(f));
+  return fp12_conj(f.to_fp12());
 }
 // the Miller value of ONE pair of a check (pair 0: (a, H) at P = (px, py); pair 1: (-g1, b)), its own squarings included:
 // the two pairs' values multiply to ck_miller's (squaring is multiplicative), conjugated.  Two lanes per check halve the
@@ -621,11 +621,9 @@ DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, const 
   const uint32_t np = st[g].np, r = st[g].round;
   const Fp ax = st[g].a.x, ay = st[g].a.y;
   const auto line = [&](uint32_t s, uint32_t pair) { return pair ? l2[(size_t)s * G + g] : rl[(size_t)s * R + r]; };
-#if DG_CK_MILLER_D
-  F[g] = ck_miller_d(np, ax, ay, line);
-#else
-  F[g] = ck_miller(np, ax, ay, line);
-#endif
+  __shared__ uint32_t s_f[144 * 64];  // the accumulators: one 576 B column per lane (fpd.h Fd12Col)
+  Fd12Col<64> f{s_f + threadIdx.x};
+  F[g] = ck_miller_col(np, ax, ay, line, f);
 }
 #else
 DG_KERNEL void __launch_bounds__(64, DG_CK_WAVES) k_ck_miller(uint32_t G, const uint32_t* gcnt, uint32_t R,

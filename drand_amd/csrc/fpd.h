@@ -1,5 +1,5 @@
 // Digit form through whole Fp12 operations (host and device): the Miller loops of the check pipeline (checks.h
-// ck_miller_d) keep their accumulator and the line values as 14 digits of 28 bits -- the form the Montgomery
+// ck_miller_col) keep their accumulator and the line values as 14 digits of 28 bits -- the form the Montgomery
 // products of fp28.h work in -- across every product, addition and subtraction of an Fp12 squaring or sparse line
 // product, and convert only at the loop's edges.  field.h's 12-limb path unpacks the operands and packs the result of
 // every product and reduces after every addition (~740 VALU instructions per product against the product's 392
@@ -11,7 +11,7 @@
 //   - additions and subtractions leave digits normalised (below 2^28, the top one small); a - b adds the fat multiple
 //     M p whose digits are all >= 2^28 - 1, so a + M p - b is digit-wise non-negative for any normalised b below M p;
 //   - every Fp12 operation reduces its twelve outputs (fd_red: below 3 p) so the next one starts below 3 p.
-// tests/native/hostcheck.cpp checks ck_miller_d against ck_miller with DG_FD_CHECK asserting the bounds.
+// tests/native/hostcheck.cpp checks ck_miller_col against ck_miller with DG_FD_CHECK asserting the bounds.
 #pragma once
 #include "fp28.h"
 
@@ -267,6 +267,102 @@ DGI Fd12 fd12_mul_014(const Fd12& f, const Fd2& c0, const Fd2& c1, const Fd2& c4
 DGI Fd12 fd12_one() {
   const Fd one = fd_from(fp_one()), z = fd_zero();
   return Fd12{Fd6{Fd2{one, z}, Fd2{z, z}, Fd2{z, z}}, Fd6{Fd2{z, z}, Fd2{z, z}, Fd2{z, z}}};
+}
+
+// ---- an Fp12 accumulator outside the register file (checks.h k_ck_miller: one LDS column per lane, 576 B)
+// Component i (0..11, the Fd12 order c0.c0.c0, c0.c0.c1, c0.c1.c0, ...) is 12 limbs of a value below 3 p (fd_red, not
+// fully reduced: 3 p < 2^384) at w[(12 i + k) kStride]; lanes of a wave read consecutive words (kStride = the lanes).
+// The loop's live set is then the operation's own temporaries: the 168 digit registers of the accumulator are what
+// made the register form of this loop spill (213-430 VGPRs).
+#define DG_FD_RELOAD() asm volatile("" ::: "memory")  // a later get() reads the column again (no live copy kept)
+#if defined(__HIP__)
+#define DG_MEMBER __host__ __device__ __forceinline__
+#else
+#define DG_MEMBER inline
+#endif
+template <uint32_t kStride>
+struct Fd12Col {
+  uint32_t* w;
+  DG_MEMBER Fd get(int i) const {
+    uint32_t l[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) l[k] = w[(size_t)(12 * i + k) * kStride];
+    return fd_from(Fp{{l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7], l[8], l[9], l[10], l[11]}});
+  }
+  DG_MEMBER void put(int i, const Fd& a) {
+    const Fd r = fd_red(a);
+    uint32_t l[12];
+    fp28_pack(r.d, l);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) w[(size_t)(12 * i + k) * kStride] = l[k];
+  }
+  DG_MEMBER Fd6 get6(int h) const {
+    return Fd6{Fd2{get(6 * h), get(6 * h + 1)}, Fd2{get(6 * h + 2), get(6 * h + 3)}, Fd2{get(6 * h + 4), get(6 * h + 5)}};
+  }
+  DG_MEMBER void put6(int h, const Fd6& a) {
+    put(6 * h, a.c0.c0);
+    put(6 * h + 1, a.c0.c1);
+    put(6 * h + 2, a.c1.c0);
+    put(6 * h + 3, a.c1.c1);
+    put(6 * h + 4, a.c2.c0);
+    put(6 * h + 5, a.c2.c1);
+  }
+  DG_MEMBER void set_one() {
+    const Fd one = fd_from(fp_one()), z = fd_zero();
+    put(0, one);
+#pragma unroll 1
+    for (int i = 1; i < 12; ++i) put(i, z);
+  }
+  DG_MEMBER Fp12 to_fp12() const {
+    Fp c[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) c[i] = fd_to(get(i));
+    return Fp12{Fp6{Fp2{c[0], c[1]}, Fp2{c[2], c[3]}, Fp2{c[4], c[5]}}, Fp6{Fp2{c[6], c[7]}, Fp2{c[8], c[9]}, Fp2{c[10], c[11]}}};
+  }
+};
+// fd12_sqr on a column: the same formula and bounds; each half is loaded where it is used (twice, instead of a live
+// copy beside the products) and the outputs stored as they are formed
+template <class C>
+DGI void fd12_sqr_col(C& f) {
+  Fd6 ab;
+  {
+    const Fd6 a0 = f.get6(0), a1 = f.get6(1);
+    ab = fd6_mul(a0, a1);
+  }
+  fd6_pin(ab);
+  DG_FD_RELOAD();
+  Fd6 x, y;
+  {
+    const Fd6 a0 = f.get6(0), a1 = f.get6(1);
+    x = fd6_add(a0, a1);
+    y = fd6_add(a0, fd6_mul_v<4>(a1));
+  }
+  fd6_pin(x);
+  fd6_pin(y);
+  f.put6(1, fd6_add(ab, ab));
+  const Fd6 s = fd6_mul(x, y);
+  f.put6(0, fd6_sub<256>(fd6_sub<128>(s, ab), fd6_mul_v<128>(ab)));
+  DG_FD_RELOAD();
+}
+// fd12_mul_014 on a column (n0 = v bb + aa, n1 = s - (aa + bb), s = (f0 + f1)(c0 + (c1 + c4) v))
+template <class C>
+DGI void fd12_mul_014_col(C& f, const Fd2& c0, const Fd2& c1, const Fd2& c4) {
+  Fd6 bb = fd6_mul_1(f.get6(1), c4);
+  fd6_pin(bb);
+  DG_FD_RELOAD();
+  Fd6 aa = fd6_mul_01(f.get6(0), c0, c1);
+  fd6_pin(aa);
+  Fd6 u = fd6_add(aa, bb);
+  fd6_pin(u);
+  Fd6 n0 = fd6_add(fd6_mul_v<64>(bb), aa);
+  fd6_pin(n0);
+  DG_FD_RELOAD();
+  Fd6 t = fd6_add(f.get6(0), f.get6(1));
+  fd6_pin(t);
+  f.put6(0, n0);
+  const Fd6 s = fd6_mul_01(t, c0, fd2_add(c1, c4));
+  f.put6(1, fd6_sub<128>(s, u));
+  DG_FD_RELOAD();
 }
 
 }  // namespace dg

@@ -584,12 +584,15 @@ extern "C" int hc_ck_pipeline_check(const uint8_t* pk48, const uint8_t* q1_96, c
   ck_lines(q2.x, q2.y, [&](uint32_t s, const CkLine& l) { l2[s] = l; });
   const Fp12 f = ck_miller((uint32_t)np, p1.x, p1.y, [&](uint32_t s, uint32_t pair) { return pair ? l2[s] : l1[s]; });
   {
-    // k_ck_miller's digit-form loop (fpd.h, bounds asserted: DG_FD_CHECK)
-    const Fp12 fd = ck_miller_d((uint32_t)np, p1.x, p1.y, [&](uint32_t s, uint32_t pair) { return pair ? l2[s] : l1[s]; });
     const Fp2* u[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
-    const Fp2* v[6] = {&fd.c0.c0, &fd.c0.c1, &fd.c0.c2, &fd.c1.c0, &fd.c1.c1, &fd.c1.c2};
+    // k_ck_miller's digit-form loop with the accumulator in a column (fpd.h; bounds asserted: DG_FD_CHECK)
+    uint32_t col[144];
+    Fd12Col<1> fc{col};
+    const Fp12 fl =
+        ck_miller_col((uint32_t)np, p1.x, p1.y, [&](uint32_t s, uint32_t pair) { return pair ? l2[s] : l1[s]; }, fc);
+    const Fp2* w[6] = {&fl.c0.c0, &fl.c0.c1, &fl.c0.c2, &fl.c1.c0, &fl.c1.c1, &fl.c1.c2};
     for (int i = 0; i < 6; ++i)
-      if (!fp2_eq(*u[i], *v[i])) return 6;
+      if (!fp2_eq(*u[i], *w[i])) return 9;
     if (g_fd_bad) return 7;
   }
   // each pair in a lane of its own (its own squarings; xr.h k_xg_miller), the two values multiplied by k_ck_easy

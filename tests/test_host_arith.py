@@ -325,7 +325,7 @@ def test_check_pipeline_matches_pair_check(hc):
     (ck_miller1_fly, the isolation's k_xg_miller) -- the final exponentiation with in-lane
     inversions, the compressed chains and the fused next factors) equals
     final_exp_cubed(miller_loop<2>) on the host: valid and invalid (key, H, sigma) triples of the golden chain, each
-    pair dropped alone (np = 1, 2) and both.  k_ck_miller's digit-form loop (fpd.h ck_miller_d) must give the same
+    pair dropped alone (np = 1, 2) and both.  k_ck_miller's digit-form loop (fpd.h, checks.h ck_miller_col) must give the same
     Miller value with every digit-form bound holding."""
     from tests.fixtures import chain, chain_arrays
 
