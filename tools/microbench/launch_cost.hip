@@ -15,6 +15,7 @@ __global__ void k_args(int* a, int* b, int* c, int* d, int* e, int* f, int* g, i
 }
 // a private array indexed by a runtime value: the compiler keeps it in scratch (in-bounds: idx < 256)
 __global__ void k_scratch(int* p, int idx) {
+  if (p[2] == 0 && idx < 0) return;  // (idx < 0: the gated form below, every lane leaves at once)
   volatile int loc[256];
   for (int t = 0; t < 256; ++t) loc[t] = t + threadIdx.x;
   if (p[0] == 12345) p[1] = loc[idx & 255];
@@ -41,6 +42,12 @@ int main() {
       if (kind == 1) hipLaunchKernelGGL(k_args, dim3(1), dim3(64), 0, s, d, d, d, d, d, d, d, d, d, d, d, d);
       if (kind == 2) hipLaunchKernelGGL(k_scratch, dim3(1), dim3(64), 0, s, d, i);
       if (kind == 3) hipLaunchKernelGGL(k_nop, dim3(782), dim3(128), 0, s, d);
+      // a gated launch with a private segment that finds nothing to do (the isolation's launches on a passed batch)
+      if (kind == 4) hipLaunchKernelGGL(k_scratch, dim3(1563), dim3(64), 0, s, d, -1);
+      if (kind == 5) {
+        if (i & 1) hipLaunchKernelGGL(k_nop, dim3(1), dim3(64), 0, s, d);
+        else hipLaunchKernelGGL(k_scratch, dim3(1563), dim3(64), 0, s, d, -1);
+      }
     }
     const double t1 = now_us();
     (void)hipDeviceSynchronize();
@@ -48,8 +55,8 @@ int main() {
     return std::make_pair((t1 - t0) / N, (t2 - t0) / N);
   };
   printf("{");
-  const char* names[] = {"nop", "args12", "scratch", "nop_782wg"};
-  for (int kind = 0; kind < 4; ++kind)
+  const char* names[] = {"nop", "args12", "scratch", "nop_782wg", "scratch_dead_1563wg", "alt_nop_scratch_dead"};
+  for (int kind = 0; kind < 6; ++kind)
     for (int ns : {1, 8}) {
       auto r = run(ns, kind);
       printf("\"%s_%dstreams\": {\"host_us\": %.2f, \"total_us\": %.2f}, ", names[kind], ns, r.first, r.second);
