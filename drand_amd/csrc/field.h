@@ -737,6 +737,55 @@ DGI Fp2 fp2_mul_dig(const Fp2& a, const Fp2& b) {
   const Fp t2 = fp28_product_packed<kSos>(xs, ys);
   return Fp2{fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
+// fp2_mul_dig with two Montgomery reductions instead of three (the Karatsuba columns combined before reducing, as
+// fpd.h fd2_mul): c0 = a0 b0 - a1 b1 from signed columns lies in (-p^2 / R, p^2 / R + p) for inputs below p, so p is
+// added where the reduced top digit is negative and one conditional subtraction follows; c1 = a0 b1 + a1 b0 from the
+// non-negative columns T2 - T0 - T1, below 2 p^2 / R + p.  The same values as fp2_mul (hostcheck.cpp)
+DGI Fp2 fp2_mul_dig2(const Fp2& a, const Fp2& b) {
+  uint32_t x0[14], x1[14], y0[14], y1[14];
+  fp28_unpack(a.c0.l, x0);
+  fp28_unpack(a.c1.l, x1);
+  fp28_unpack(b.c0.l, y0);
+  fp28_unpack(b.c1.l, y1);
+  uint64_t d[27], s[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) d[k] = s[k] = 0;
+  fp28_cols(x0, y0, d);
+  DG_PIN_D14(x1);
+  DG_PIN_D14(y1);
+  fp28_cols(x1, y1, s);
+#pragma unroll
+  for (int k = 0; k < 27; ++k) {
+    const uint64_t t0 = d[k], t1 = s[k];
+    d[k] = t0 - t1;
+    s[k] = 0 - (t0 + t1);
+  }
+  uint32_t r[14];
+  fp28_sos_reduce_signed(d, r);
+  const uint32_t neg = (uint32_t)((int32_t)r[13] >> 31);
+#pragma unroll
+  for (int i = 0; i < 14; ++i) r[i] += P28[i] & neg;
+#pragma unroll
+  for (int i = 0; i < 13; ++i) {
+    r[i + 1] += r[i] >> 28;
+    r[i] &= FP28_MASK;
+  }
+  Fp c0;
+  fp28_pack(r, c0.l);
+  c0 = fp_reduce_once(c0);
+  DG_PIN_T12(c0);
+  uint32_t xs[14], ys[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    xs[i] = x0[i] + x1[i];
+    ys[i] = y0[i] + y1[i];
+  }
+  fp28_cols(xs, ys, s);
+  fp28_sos_reduce(s, r);
+  Fp c1;
+  fp28_pack(r, c1.l);
+  return Fp2{c0, fp_reduce_once(c1)};
+}
 // a^2 = ((a0 + a1)(a0 - a1), 2 a0 a1): a0, a1 unpacked once, a0 + a1 digit-wise, a0 - a1 (mod p) unpacked
 template <bool kSos = true>
 DGI Fp2 fp2_sqr_dig(const Fp2& a) {
@@ -763,7 +812,11 @@ DGH Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
   DG_PIN_FP12(x.c1);
   DG_PIN_FP12(y.c0);
   DG_PIN_FP12(y.c1);
+#if DG_FP2_DIG == 2
+  Fp2 r = fp2_mul_dig2(x, y);  // two reductions
+#else
   Fp2 r = fp2_mul_dig(x, y);
+#endif
   DG_PIN_FP12(r.c0);
   DG_PIN_FP12(r.c1);
   return r;

@@ -115,6 +115,32 @@ DGI void fp28_sos_reduce(uint64_t (&t)[27], uint32_t (&r)[14]) {
   r[12] = (uint32_t)t[26] & FP28_MASK;
   r[13] = (uint32_t)(t[26] >> 28);
 }
+// fp28_sos_reduce for signed columns (two's complement in the 64-bit words): arithmetic carries, digits 0..12 below
+// 2^28, the top one signed; the value is (T + m p) / 2^392 for the signed column value T (the two-reduction Fp2
+// products: field.h fp2_mul_dig2, fpd.h fd2_mul)
+DGI void fp28_sos_reduce_signed(uint64_t (&t)[27], uint32_t (&r)[14]) {
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    const uint32_t m = ((uint32_t)t[i] * P_INV28) & FP28_MASK;
+#pragma unroll
+    for (int j = 0; j < 14; ++j) t[i + j] += (uint64_t)m * P28[j];
+    t[i + 1] += (uint64_t)((int64_t)t[i] >> 28);
+  }
+#pragma unroll
+  for (int k = 14; k < 26; ++k) {
+    r[k - 14] = (uint32_t)t[k] & FP28_MASK;
+    t[k + 1] += (uint64_t)((int64_t)t[k] >> 28);
+  }
+  r[12] = (uint32_t)t[26] & FP28_MASK;
+  r[13] = (uint32_t)((int64_t)t[26] >> 28);
+}
+// t += x y as 27 column sums
+DGI void fp28_cols(const uint32_t (&x)[14], const uint32_t (&y)[14], uint64_t (&t)[27]) {
+#pragma unroll
+  for (int i = 0; i < 14; ++i)
+#pragma unroll
+    for (int j = 0; j < 14; ++j) t[i + j] += (uint64_t)x[i] * y[j];
+}
 DGI void fp28_sos_mul_d(const uint32_t (&x)[14], const uint32_t (&y)[14], uint32_t (&r)[14]) {
   uint64_t t[27];
 #pragma unroll

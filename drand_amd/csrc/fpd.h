@@ -165,13 +165,52 @@ DGI Fd2 fd2_sub(const Fd2& a, const Fd2& b) {
   return Fd2{fd_sub<M>(a.c0, b.c0), fd_sub<M>(a.c1, b.c1)};
 }
 DGI Fd2 fd2_red(const Fd2& a) { return Fd2{fd_red(a.c0), fd_red(a.c1)}; }
-// inputs below 40 p: c0 below 6 p, c1 below 10 p
-DGI Fd2 fd2_mul(const Fd2& a, const Fd2& b) {
+// inputs below 40 p: c0 below 6 p, c1 below 10 p (three reductions: the form fd2_mul replaced, kept for the host check)
+DGI Fd2 fd2_mul3(const Fd2& a, const Fd2& b) {
   const Fd t0 = fd_mul(a.c0, b.c0), t1 = fd_mul(a.c1, b.c1);
   const Fd t2 = fd_mul(fd_add_lazy(a.c0, a.c1), fd_add_lazy(b.c0, b.c1));
   Fd2 r{fd_sub<4>(t0, t1), fd_sub<8>(t2, fd_add(t0, t1))};
-  DG_PIN_D14(r.c0.d);  // (the combination materialised here: the next product's temporaries do not overlap it)
+  DG_PIN_D14(r.c0.d);
   DG_PIN_D14(r.c1.d);
+  return r;
+}
+// Fp2 product with two Montgomery reductions instead of three (~15% fewer instructions): the Karatsuba columns are
+// combined before reducing.  c0 = a0 b0 - a1 b1 from signed columns: |a0 b0 - a1 b1| < 1600 p^2 for inputs below 40 p,
+// so the reduced value lies in (-0.64 p, 1.64 p) (R ~ 2520 p), and 2 p added digit-wise (the top digit wrapping modulo
+// 2^32 back to the true non-negative value) leaves it below 3.7 p.  c1 = (a0 + a1)(b0 + b1) - (a0 b0 + a1 b1): the
+// columns of a0 b1 + a1 b0, non-negative; below 2.3 p.  Same bound contract as fd2_mul3 (tighter outputs).
+DGI Fd2 fd2_mul(const Fd2& a, const Fd2& b) {
+  DG_FD_ASSERT(a.c0.d[13] < (1u << 25) && a.c1.d[13] < (1u << 25) && b.c0.d[13] < (1u << 25) &&
+                   b.c1.d[13] < (1u << 25),
+               "fd2_mul: operand too large");
+  Fd x0 = a.c0, x1 = a.c1, y0 = b.c0, y1 = b.c1;
+  DG_PIN_D14(x0.d);
+  DG_PIN_D14(y0.d);
+  uint64_t d[27], s[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) d[k] = s[k] = 0;
+  fp28_cols(x0.d, y0.d, d);
+  DG_PIN_D14(x1.d);
+  DG_PIN_D14(y1.d);
+  fp28_cols(x1.d, y1.d, s);
+#pragma unroll
+  for (int k = 0; k < 27; ++k) {
+    const uint64_t t0 = d[k], t1 = s[k];
+    d[k] = t0 - t1;
+    s[k] = 0 - (t0 + t1);
+  }
+  Fd2 r;
+  fp28_sos_reduce_signed(d, r.c0.d);
+  constexpr fdc::Fat P2 = fdc::fat(2);  // 2 p with every digit >= 2^28 - 1 (digit-wise addition, then carries)
+#pragma unroll
+  for (int i = 0; i < 14; ++i) r.c0.d[i] += P2.k[i];
+  fd_norm(r.c0);
+  DG_PIN_D14(r.c0.d);
+  const Fd xs = fd_add_lazy(x0, x1), ys = fd_add_lazy(y0, y1);
+  fp28_cols(xs.d, ys.d, s);
+  fp28_sos_reduce(s, r.c1.d);
+  DG_PIN_D14(r.c1.d);
+  DG_FD_ASSERT(r.c0.d[13] <= 4u * fdc::PD[13] && r.c1.d[13] <= 3u * fdc::PD[13], "fd2_mul: output above bound");
   return r;
 }
 // (a0 + a1)(a0 - a1), 2 a0 a1 (inputs below 20 p): c0 below 2 p, c1 below 4 p

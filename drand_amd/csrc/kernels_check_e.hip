@@ -6,6 +6,6 @@
 #define DG_INLINE12 1
 #define DG_CYC_SQR 1
 #define DG_FP2_ILV 1
-#define DG_FP2_DIG 1  // Fp2 products in digit form: each operand unpacked once (field.h fp2_mul_dig, +3% C5 measured)
+#define DG_FP2_DIG 2  // Fp2 products in digit form, each operand unpacked once, two Montgomery reductions (field.h fp2_mul_dig2)
 #define DG_SEQ_DIG 1  // ... and the serialised forms (subgroup checks, column loops, compressed squarings: -1% C5)
 #include "kernels.h"

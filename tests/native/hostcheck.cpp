@@ -326,6 +326,7 @@ extern "C" int hc_fp2_mul_dig_check(uint64_t seed, uint32_t n) {
     }
     const Fp2 x = fp2_mul_dig(a, b), y = fp2_mul(a, b);
     if (!fp2_eq(x, y)) return 0;
+    if (!fp2_eq(fp2_mul_dig2(a, b), y) || !fp2_eq(fp2_mul_dig2(b, a), y)) return 0;
     if (!fp2_eq(fp2_sqr_dig(a), fp2_sqr(a)) || !fp2_eq(fp2_sqr_dig(b), fp2_sqr(b))) return 0;
     if (!fp2_eq(fp2_mul_dig<false>(a, b), y) || !fp2_eq(fp2_sqr_dig<false>(a), fp2_sqr(a))) return 0;
   }
@@ -697,6 +698,18 @@ extern "C" int hc_fd_check(uint64_t seed, int n) {
     // chained: the reduced outputs of one operation as the next one's inputs
     const Fp12 q1 = fp12_mul_014(fp12_sqr(s1), l0, l1, l4);
     const Fp12 q2 = fd12_to(fd12_mul_014(fd12_sqr(fd12_sqr(fd12_from(a))), fd2_from(l0), fd2_from(l1), fd2_from(l4)));
+    // fd2_mul (two reductions, signed c0 columns) against fd2_mul3 (three), operands up to 40 p
+    for (int sc : {1, 7, 40}) {
+      auto big = [&](const Fp& v) {
+        const Fd r = fd_from(v);
+        Fd acc = r;
+        for (int i = 1; i < sc; ++i) acc = fd_add(acc, r);
+        return acc;
+      };
+      const Fd2 a2{big(rfp(top)), big(rfp(false))}, b2{big(rfp(false)), big(rfp(top))};
+      bad += !fp2_eq(fd2_to(fd2_mul(a2, b2)), fd2_to(fd2_mul3(a2, b2)));
+      bad += !fp2_eq(fd2_to(fd2_mul(b2, a2)), fd2_to(fd2_mul3(a2, b2)));
+    }
     const Fp12* x[3] = {&s1, &m1, &q1};
     const Fp12* y[3] = {&s2, &m2, &q2};
     for (int k = 0; k < 3; ++k) {
