@@ -277,11 +277,10 @@ int ws(Slot s, size_t bytes, void** out) {
 // 4, 3, 2, 1.  Taking the sets in index order sent batches 3, 4 to queue 4 and 7, 0 to queue 1, so a
 // window of 20 batches gave queue 4 six heads and queue 1 four, and the region waited for queue 4 alone at its end
 // (DESIGN.md §5.5).  With 8 sets on 4 queues the order 0, 1, 2, 3, 7, 6, 5, 4 visits queues 1, 2, 3, 4, 1, 2, 3, 4:
-// every window of batches is spread over the queues to within one.  DG_SET_ORDER=0: index order (A/B).
+// every window of batches is spread over the queues to within one.
 int set_at(int slot) {
-  static const bool zigzag = env_int("DG_SET_ORDER", 1) != 0;
   const int n = active_sets();
-  if (!zigzag || n != 8 || env_hw_queues() != 4) return slot;
+  if (n != 8 || env_hw_queues() != 4) return slot;
   static const int order[8] = {0, 1, 2, 3, 7, 6, 5, 4};
   return order[slot];
 }

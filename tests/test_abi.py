@@ -163,9 +163,10 @@ def test_queue_plan():
 
 
 def test_release_build_reads_no_retired_switches():
-    """Round-4 verdict (hygiene): DG_NO_BIND (and the removed A/B switches) have no effect on the release build -- the
-    library never reads them, so their names are absent from its strings (getenv takes the name as a literal)."""
+    """Round-4 verdict (hygiene): DG_NO_BIND (and the removed A/B switches, round 6's DG_XR_SKIP among them) have no
+    effect on the release build -- the library never reads them, so their names are absent from its strings (getenv
+    takes the name as a literal)."""
     blob = open(L.LIB_PATH, "rb").read()
     for name in (b"DG_NO_BIND", b"DG_CK_OLD", b"DG_FUSED", b"DG_MSM_JAC", b"DG_FP2_LAZY", b"DG_FP6_DIG",
-                 b"DG_SUB_SEPARATE"):
+                 b"DG_SUB_SEPARATE", b"DG_XR_SKIP", b"DG_STAGGER", b"DG_GRAPH", b"DG_SET_ORDER"):
         assert name not in blob, name
